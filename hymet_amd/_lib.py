@@ -1,0 +1,115 @@
+"""ctypes binding of libhymet_gpu.so (include/hymet_gpu.h).
+
+This is the product's only path to the device: if the library or a gfx950 GPU is missing
+every call raises -- there is no CPU fallback (the CPU oracle under oracle/ is test
+infrastructure and is never imported here)."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhymet_gpu.so")
+
+_c = ctypes
+_i64, _u64, _i32, _u32, _vp = _c.c_int64, _c.c_uint64, _c.c_int, _c.c_uint32, _c.c_void_p
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "hymet_version": (_i32, []),
+    "hymet_init": (_i32, [_i32, _c.POINTER(_vp)]),
+    "hymet_destroy": (_i32, [_vp]),
+    "hymet_last_error": (_c.c_char_p, []),
+    "hymet_set_stream": (_i32, [_vp, _vp]),
+    "hymet_sync": (_i32, [_vp]),
+    "hymet_pack": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "hymet_screen_table_slots": (_i64, [_i64]),
+    "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
+    "hymet_screen_count": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _u32, _i32, _c.POINTER(_vp), _c.POINTER(_i64),
+                                  _c.POINTER(_vp), _u64, _vp, _i64, _vp, _vp]),
+    "hymet_screen_stats": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
+}
+
+_lib = None
+
+
+class HymetError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP library (build it first with `python -m hymet_amd.build` or
+    __graft_entry__.build()).  Raises loudly when it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HymetError(f"{LIB_PATH} not found: build the HIP extension (python -m hymet_amd.build); "
+                         "hymet_amd has no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().hymet_last_error()
+        raise HymetError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+class Gpu:
+    """One libhymet context bound to a torch CUDA(HIP) device and its current stream."""
+
+    def __init__(self, device: int = 0):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise HymetError("no GPU visible: hymet_amd runs on MI355X (gfx950) only")
+        self.torch = torch
+        self.device = device
+        torch.cuda.set_device(device)
+        self.dev = torch.device("cuda", device)
+        self.lib = load()
+        h = _vp()
+        check(self.lib.hymet_init(device, _c.byref(h)), "hymet_init")
+        self.ctx = h
+        self.bind_stream()
+
+    def bind_stream(self, stream=None):
+        s = stream if stream is not None else self.torch.cuda.current_stream(self.device)
+        check(self.lib.hymet_set_stream(self.ctx, _vp(s.cuda_stream)), "hymet_set_stream")
+
+    def call(self, name, *args):
+        check(getattr(self.lib, name)(self.ctx, *args), name)
+
+    def sync(self):
+        check(self.lib.hymet_sync(self.ctx), "hymet_sync")
+
+    def empty(self, n, dtype):
+        return self.torch.empty(int(n), dtype=dtype, device=self.dev)
+
+    def zeros(self, n, dtype):
+        return self.torch.zeros(int(n), dtype=dtype, device=self.dev)
+
+    def close(self):
+        if self.ctx:
+            self.lib.hymet_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def ptr(t) -> _vp:
+    return _vp(t.data_ptr())

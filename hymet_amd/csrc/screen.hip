@@ -1,0 +1,343 @@
+// Mash `screen` on MI355X (replaces scripts/mash.sh:14).
+//
+// Kernels
+//   table_insert   : distinct sketch hashes -> open-addressing uint64 table in HBM
+//                    (linear probing, slot = top bits of the hash), one atomicCAS per hash.
+//   screen_count<K>: one thread = one 64-position tile of the pooled, packed query bases.
+//                    Rolling 2-bit forward / reverse-complement words decide the canonical
+//                    strand by integer compare (== Mash's memcmp on ASCII, since A<C<G<T);
+//                    rolling ASCII byte windows feed MurmurHash3_x64_128 (seeded, word 0)
+//                    without re-expanding the k-mer; each hash probes up to 4 DB tables and
+//                    bumps a uint32 count; hashes under a threshold are appended as bottom-s
+//                    candidates for the pool set-size estimate (MinHashHeap::estimateSetSize).
+//   screen_stats   : one 256-thread block per reference: gather its counts through the
+//                    slot map, shared = #>0, median = k-th smallest positive count by a
+//                    bisection over the value range with block reductions (no sort).
+// Roofline: HBM/latency bound (random 8-B key probes); algorithmic bytes per k-mer are
+// 0.375 (packed read) + 8 per DB probe (+4 per hit), DESIGN.md §Screen.
+#include "common.hpp"
+
+namespace {
+
+constexpr uint64_t kEmpty = ~0ull;
+constexpr int kTile = 64;  // k-mer start positions per thread (multiple of 32: lanes stay in phase)
+constexpr int kMaxDb = 4;
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33;
+    return k;
+}
+
+// MurmurHash3_x64_128 word 0 of a K-byte key held little-endian in w[0..3].
+template <int K>
+__device__ __forceinline__ uint64_t murmur3_h0(const uint64_t (&w)[4], uint32_t seed) {
+    constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+    constexpr int NB = K / 16, TAIL = K & 15;
+    uint64_t h1 = seed, h2 = seed;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        uint64_t k1 = w[2 * b], k2 = w[2 * b + 1];
+        k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+        h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+        k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+        h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+    }
+    if constexpr (TAIL > 8) {
+        uint64_t k2 = w[2 * NB + 1];
+        k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    }
+    if constexpr (TAIL > 0) {
+        uint64_t k1 = w[2 * NB];
+        k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    }
+    h1 ^= (uint64_t)K;
+    h2 ^= (uint64_t)K;
+    h1 += h2;
+    h2 += h1;
+    h1 = fmix64(h1);
+    h2 = fmix64(h2);
+    return h1 + h2;
+}
+
+struct CountParams {
+    const uint32_t *w2b;
+    const uint32_t *wm;
+    int64_t n_bases, pos_begin, pos_end;
+    uint32_t seed;
+    int ndb;
+    const uint64_t *keys[kMaxDb];
+    uint64_t mask[kMaxDb];
+    int shift[kMaxDb];
+    uint32_t *counts[kMaxDb];
+    uint64_t nslots[kMaxDb];
+    uint64_t cand_thr;
+    uint64_t *cand;
+    int64_t cand_cap;
+    unsigned long long *cand_n;
+    unsigned long long *nkmers;
+};
+
+__device__ __forceinline__ uint32_t ascii_of(uint32_t c) { return (0x54474341u >> (8 * c)) & 0xFFu; }
+
+template <int K>
+__global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
+    constexpr int NW = (K + 7) / 8;
+    constexpr int TOPB = K - 8 * (NW - 1);
+    constexpr uint64_t TOPMASK = TOPB == 8 ? ~0ull : ((1ull << (8 * TOPB)) - 1);
+    constexpr uint64_t KMASK = K == 32 ? ~0ull : ((1ull << (2 * K)) - 1);
+    const int64_t n_pos = P.pos_end - P.pos_begin;
+    const int64_t n_tiles = (n_pos + kTile - 1) / kTile;
+    uint64_t nk = 0;
+    for (int64_t tile = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; tile < n_tiles;
+         tile += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p0 = P.pos_begin + tile * kTile;                 // first k-mer start
+        const int64_t p1 = min(p0 + kTile, P.pos_end);                 // one past last start
+        const int64_t iend = min(p1 + K - 1, P.n_bases);                // bases to read: [p0, iend)
+        uint64_t fwd = 0, rc = 0;
+        uint64_t F[4] = {0, 0, 0, 0}, R[4] = {0, 0, 0, 0};
+        int run = 0;
+        uint32_t cw = 0, mw = 0;
+        for (int64_t i = p0; i < iend; i++) {
+            if (((i & 15) == 0) || i == p0) cw = P.w2b[i >> 4];
+            if (((i & 31) == 0) || i == p0) mw = P.wm[i >> 5];
+            const uint32_t c = (cw >> (2 * (i & 15))) & 3u;
+            const uint32_t bad = (mw >> (i & 31)) & 1u;
+            run = bad ? 0 : run + 1;
+            fwd = ((fwd << 2) | c) & KMASK;
+            rc = (rc >> 2) | ((uint64_t)(3u - c) << (2 * (K - 1)));
+#pragma unroll
+            for (int j = 0; j < NW - 1; j++) F[j] = (F[j] >> 8) | (F[j + 1] << 56);
+            F[NW - 1] = (F[NW - 1] >> 8) | ((uint64_t)ascii_of(c) << (8 * (TOPB - 1)));
+#pragma unroll
+            for (int j = NW - 1; j > 0; j--) R[j] = (R[j] << 8) | (R[j - 1] >> 56);
+            R[0] = (R[0] << 8) | ascii_of(3u - c);
+            R[NW - 1] &= TOPMASK;
+            if (run < K) continue;                                       // invalid base inside the k-mer
+            const int64_t p = i - (K - 1);
+            if (p < p0) continue;                                        // warm-up only
+            const uint64_t h = (rc < fwd) ? murmur3_h0<K>(R, P.seed) : murmur3_h0<K>(F, P.seed);
+            nk++;
+            if (h < P.cand_thr) {
+                unsigned long long idx = atomicAdd(P.cand_n, 1ull);
+                if ((int64_t)idx < P.cand_cap) P.cand[idx] = h;
+            }
+#pragma unroll
+            for (int d = 0; d < kMaxDb; d++) {
+                if (d >= P.ndb) break;
+                if (h == kEmpty) {
+                    atomicAdd(&P.counts[d][P.nslots[d]], 1u);
+                    continue;
+                }
+                const uint64_t *keys = P.keys[d];
+                uint64_t s = h >> P.shift[d];
+                for (;;) {
+                    const uint64_t key = keys[s];
+                    if (key == h) {
+                        atomicAdd(&P.counts[d][s], 1u);
+                        break;
+                    }
+                    if (key == kEmpty) break;
+                    s = (s + 1) & P.mask[d];
+                }
+            }
+        }
+    }
+    // wave reduction of the k-mer count, one atomic per wave
+    unsigned long long v = nk;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(P.nkmers, v);
+}
+
+__global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t *__restrict__ hashes, int64_t n,
+                                                           unsigned long long *keys, uint64_t mask, int shift,
+                                                           int64_t nslots, int64_t *slot_of) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t h = hashes[i];
+    if (h == kEmpty) {
+        slot_of[i] = nslots;
+        return;
+    }
+    uint64_t s = h >> shift;
+    for (;;) {
+        unsigned long long prev = atomicCAS(&keys[s], (unsigned long long)kEmpty, (unsigned long long)h);
+        if (prev == kEmpty || prev == h) break;
+        s = (s + 1) & mask;
+    }
+    slot_of[i] = (int64_t)s;
+}
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T *red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    T s = 0;
+    for (int j = 0; j < (int)(blockDim.x >> 6); j++) s += red[j];
+    return s;
+}
+
+__device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t *red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_down(v, o, 64));
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    uint32_t s = 0;
+    for (int j = 0; j < (int)(blockDim.x >> 6); j++) s = max(s, red[j]);
+    return s;
+}
+
+constexpr int kStatsLds = 4096;
+
+__global__ __launch_bounds__(256) void screen_stats_kernel(const int64_t *__restrict__ ref_off,
+                                                           const int64_t *__restrict__ slot_of,
+                                                           const uint32_t *__restrict__ counts, uint32_t *shared,
+                                                           uint32_t *median) {
+    __shared__ uint32_t vals[kStatsLds];
+    __shared__ uint32_t red[8];
+    const int64_t r = blockIdx.x;
+    const int64_t b = ref_off[r], n = ref_off[r + 1] - b;
+    const bool in_lds = n <= kStatsLds;
+    uint32_t pos = 0, mx = 0;
+    for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
+        const uint32_t c = counts[slot_of[b + j]];
+        if (in_lds) vals[j] = c;
+        pos += c > 0;
+        mx = max(mx, c);
+    }
+    const uint32_t sh = block_sum<uint32_t>(pos, red);
+    const uint32_t vmax = block_max(mx, red);
+    uint32_t med = 0;
+    if (sh > 0) {
+        const uint32_t kk = sh / 2;  // Mash: depths sorted ascending, element shared/2
+        uint32_t lo = 1, hi = vmax;
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            uint32_t cnt = 0;
+            for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
+                const uint32_t c = in_lds ? vals[j] : counts[slot_of[b + j]];
+                cnt += (c > 0 && c <= mid);
+            }
+            cnt = block_sum<uint32_t>(cnt, red);
+            if (cnt > kk) hi = mid;
+            else lo = mid + 1;
+        }
+        med = lo;
+    }
+    if (threadIdx.x == 0) {
+        shared[r] = sh;
+        median[r] = med;
+    }
+}
+
+template <int K>
+int launch_count(hymet_ctx *ctx, const CountParams &P, int64_t n_tiles) {
+    int64_t blocks = hymet::cdiv(n_tiles, 256);
+    const int64_t cap = (int64_t)ctx->n_cu * 16;
+    if (blocks > cap) blocks = cap;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(screen_count_kernel<K>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, P);
+    HY_CHECK_LAUNCH("screen_count_kernel");
+    return HYMET_OK;
+}
+
+int log2_exact(int64_t v) {
+    int l = 0;
+    while ((1ll << l) < v) l++;
+    return l;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t hymet_screen_table_slots(int64_t n_hashes) {
+    int64_t s = 1024;
+    while (s < 2 * n_hashes) s <<= 1;
+    return s;
+}
+
+int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n, uint64_t *d_keys, int64_t n_slots,
+                             int64_t *d_slot_of) {
+    HY_ARG(ctx && d_keys && d_slot_of, "hymet_screen_table_build: null argument");
+    HY_ARG(n_slots >= 1024 && (n_slots & (n_slots - 1)) == 0, "hymet_screen_table_build: n_slots must be a power of two >= 1024");
+    HY_ARG(n_slots >= 2 * n, "hymet_screen_table_build: n_slots must be >= 2*n_hashes");
+    HY_HIP(hipSetDevice(ctx->device));
+    HY_HIP(hipMemsetAsync(d_keys, 0xFF, (size_t)n_slots * 8, ctx->stream));
+    if (n <= 0) return HYMET_OK;
+    const int lg = log2_exact(n_slots);
+    hipLaunchKernelGGL(table_insert_kernel, dim3((unsigned)hymet::cdiv(n, 256)), dim3(256), 0, ctx->stream, d_hashes, n,
+                       (unsigned long long *)d_keys, (uint64_t)(n_slots - 1), 64 - lg, n_slots, d_slot_of);
+    HY_CHECK_LAUNCH("table_insert_kernel");
+    return HYMET_OK;
+}
+
+int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask, int64_t n_bases, int64_t pos_begin,
+                       int64_t pos_end, int k, uint32_t seed, int ndb, const uint64_t *const *h_d_keys,
+                       const int64_t *h_n_slots, uint32_t *const *h_d_counts, uint64_t cand_thr, uint64_t *d_cand,
+                       int64_t cand_cap, unsigned long long *d_cand_n, unsigned long long *d_nkmers) {
+    HY_ARG(ctx && d_2b && d_mask && d_cand_n && d_nkmers, "hymet_screen_count: null argument");
+    HY_ARG(k >= 17 && k <= 32, "hymet_screen_count: k must be in 17..32 (64-bit Mash hashes)");
+    HY_ARG(ndb >= 0 && ndb <= kMaxDb, "hymet_screen_count: ndb must be 0..4");
+    HY_ARG(cand_cap == 0 || d_cand, "hymet_screen_count: d_cand is null");
+    if (pos_end > n_bases - k + 1) pos_end = n_bases - k + 1;
+    if (pos_begin < 0) pos_begin = 0;
+    if (pos_end <= pos_begin) return HYMET_OK;
+    CountParams P{};
+    P.w2b = d_2b;
+    P.wm = d_mask;
+    P.n_bases = n_bases;
+    P.pos_begin = pos_begin;
+    P.pos_end = pos_end;
+    P.seed = seed;
+    P.ndb = ndb;
+    for (int d = 0; d < ndb; d++) {
+        const int64_t ns = h_n_slots[d];
+        HY_ARG(ns >= 1024 && (ns & (ns - 1)) == 0, "hymet_screen_count: table size must be a power of two");
+        P.keys[d] = h_d_keys[d];
+        P.mask[d] = (uint64_t)(ns - 1);
+        P.shift[d] = 64 - log2_exact(ns);
+        P.counts[d] = h_d_counts[d];
+        P.nslots[d] = (uint64_t)ns;
+    }
+    P.cand_thr = cand_thr;
+    P.cand = d_cand;
+    P.cand_cap = cand_cap;
+    P.cand_n = d_cand_n;
+    P.nkmers = d_nkmers;
+    HY_HIP(hipSetDevice(ctx->device));
+    const int64_t n_tiles = hymet::cdiv(pos_end - pos_begin, kTile);
+    switch (k) {
+#define HY_K(KK) \
+    case KK: return launch_count<KK>(ctx, P, n_tiles);
+        HY_K(17) HY_K(18) HY_K(19) HY_K(20) HY_K(21) HY_K(22) HY_K(23) HY_K(24)
+        HY_K(25) HY_K(26) HY_K(27) HY_K(28) HY_K(29) HY_K(30) HY_K(31) HY_K(32)
+#undef HY_K
+    }
+    return hymet::fail(HYMET_E_ARG, "unreachable k");
+}
+
+int hymet_screen_stats(hymet_ctx *ctx, const int64_t *d_ref_off, int64_t n_refs, const int64_t *d_slot_of,
+                       const uint32_t *d_counts, uint32_t *d_shared, uint32_t *d_median) {
+    HY_ARG(ctx && d_ref_off && d_slot_of && d_counts && d_shared && d_median, "hymet_screen_stats: null argument");
+    if (n_refs <= 0) return HYMET_OK;
+    HY_ARG(n_refs < (1ll << 31), "hymet_screen_stats: too many references");
+    HY_HIP(hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(screen_stats_kernel, dim3((unsigned)n_refs), dim3(256), 0, ctx->stream, d_ref_off, d_slot_of,
+                       d_counts, d_shared, d_median);
+    HY_CHECK_LAUNCH("screen_stats_kernel");
+    return HYMET_OK;
+}
+
+}  // extern "C"

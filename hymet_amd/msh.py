@@ -1,0 +1,295 @@
+"""Mash sketch databases (`data/sketch{1,2,3}.msh`, read by scripts/mash.sh:14).
+
+A .msh file is a Cap'n Proto message (unpacked framing) with Mash's `MinHash` schema.
+Mash is third-party and unpinned (environment.yml:9) and no .msh file ships with the
+reference, so the schema below is restated from the public Mash 2.x source and is
+PARITY-UNPINNED:
+
+    struct MinHash {
+      kmerSize @0 :UInt32;  windowSize @1 :UInt32;  minHashesPerWindow @2 :UInt32;
+      concatenated @3 :Bool;  error @4 :Float32;  noncanonical @5 :Bool;
+      referenceListOld @6 :ReferenceList;  referenceList @7 :ReferenceList;
+      locusList @8 :LocusList;  alphabet @9 :Text;  preserveCase @10 :Bool;
+      hashSeed @11 :UInt32 = 42;
+      struct ReferenceList { references @0 :List(Reference);
+        struct Reference { sequence @0 :Text; quality @1 :Text; length @2 :UInt32;
+          name @3 :Text; comment @4 :Text; hashes32 @5 :List(UInt32);
+          hashes64 @6 :List(UInt64); length64 @7 :UInt64; counts32 @8 :List(UInt32);
+          counts32Sorted @9 :Bool; } } }
+
+Resulting layouts (Cap'n Proto field-slot allocation): MinHash data = 3 words
+{kmerSize@0B, windowSize@4B, minHashesPerWindow@8B, concatenated bit96, noncanonical bit97,
+preserveCase bit98, error@16B, hashSeed@20B (xor 42)}, 4 pointers {refListOld, refList,
+locusList, alphabet}; Reference data = 2 words {length@0B, counts32Sorted bit32,
+length64@8B}, 7 pointers {sequence, quality, name, comment, hashes32, hashes64, counts32}.
+
+Besides .msh, `load_db` accepts the repo's own `.npz` sketch format (same fields).
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass, field
+from typing import List
+
+import numpy as np
+
+
+@dataclass
+class SketchDB:
+    k: int = 21
+    seed: int = 42
+    sketch_size: int = 1000          # minHashesPerWindow
+    alphabet: str = "ACGT"
+    preserve_case: bool = False
+    noncanonical: bool = False
+    window_size: int = 0
+    names: List[str] = field(default_factory=list)
+    comments: List[str] = field(default_factory=list)
+    lengths: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
+    offsets: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int64))   # CSR into hashes
+    hashes: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint64))   # each ref sorted
+
+    @property
+    def n_refs(self):
+        return len(self.names)
+
+    def ref_hashes(self, i):
+        return self.hashes[self.offsets[i]:self.offsets[i + 1]]
+
+
+# ------------------------------------------------------------------ capnp reader
+class _Msg:
+    def __init__(self, data: bytes):
+        n = struct.unpack_from("<I", data, 0)[0] + 1
+        sizes = struct.unpack_from(f"<{n}I", data, 4)
+        off = 4 + 4 * n
+        off += (8 - off % 8) % 8
+        self.segs = []
+        for s in sizes:
+            self.segs.append(memoryview(data)[off:off + 8 * s])
+            off += 8 * s
+
+    def word(self, seg, w):
+        return struct.unpack_from("<Q", self.segs[seg], 8 * w)[0]
+
+    def resolve(self, seg, w):
+        """Follow a pointer at (seg, word w). Returns (kind, seg, target_word, ptr_value)."""
+        p = self.word(seg, w)
+        if p == 0:
+            return None
+        kind = p & 3
+        if kind == 2:  # far
+            double = (p >> 2) & 1
+            land = (p >> 3) & ((1 << 29) - 1)
+            tseg = p >> 32
+            if not double:
+                return self.resolve(tseg, land)
+            pad0 = self.word(tseg, land)
+            pad1 = self.word(tseg, land + 1)
+            seg2 = pad0 >> 32
+            start = (pad0 >> 3) & ((1 << 29) - 1)
+            return (pad1 & 3, seg2, start, pad1)
+        off = (p >> 2) & ((1 << 30) - 1)
+        if off & (1 << 29):
+            off -= 1 << 30
+        return (kind, seg, w + 1 + off, p)
+
+    def struct_at(self, seg, w):
+        r = self.resolve(seg, w)
+        if r is None:
+            return None
+        kind, s, t, p = r
+        assert kind == 0, "expected struct pointer"
+        return _Struct(self, s, t, (p >> 32) & 0xFFFF, p >> 48)
+
+    def list_at(self, seg, w):
+        r = self.resolve(seg, w)
+        if r is None:
+            return None
+        kind, s, t, p = r
+        assert kind == 1, "expected list pointer"
+        return (s, t, (p >> 32) & 7, p >> 35)
+
+
+class _Struct:
+    def __init__(self, msg, seg, w, dwords, nptrs):
+        self.m, self.seg, self.w, self.dw, self.np = msg, seg, w, dwords, nptrs
+
+    def u32(self, byte_off, default=0):
+        if byte_off + 4 > 8 * self.dw:
+            return default
+        return struct.unpack_from("<I", self.m.segs[self.seg], 8 * self.w + byte_off)[0] ^ default
+
+    def u64(self, byte_off):
+        if byte_off + 8 > 8 * self.dw:
+            return 0
+        return struct.unpack_from("<Q", self.m.segs[self.seg], 8 * self.w + byte_off)[0]
+
+    def f32(self, byte_off):
+        if byte_off + 4 > 8 * self.dw:
+            return 0.0
+        return struct.unpack_from("<f", self.m.segs[self.seg], 8 * self.w + byte_off)[0]
+
+    def bit(self, bit):
+        if bit >= 64 * self.dw:
+            return False
+        b = self.m.segs[self.seg][8 * self.w + bit // 8]
+        return bool((b >> (bit % 8)) & 1)
+
+    def ptr_word(self, i):
+        return self.w + self.dw + i
+
+    def text(self, i):
+        if i >= self.np:
+            return ""
+        l = self.m.list_at(self.seg, self.ptr_word(i))
+        if l is None:
+            return ""
+        s, t, es, n = l
+        raw = bytes(self.m.segs[s][8 * t:8 * t + n])
+        return raw[:-1].decode("utf-8", "replace") if raw.endswith(b"\0") else raw.decode("utf-8", "replace")
+
+    def prim_list(self, i, dtype):
+        if i >= self.np:
+            return np.zeros(0, dtype)
+        l = self.m.list_at(self.seg, self.ptr_word(i))
+        if l is None:
+            return np.zeros(0, dtype)
+        s, t, es, n = l
+        item = np.dtype(dtype).itemsize
+        return np.frombuffer(self.m.segs[s], dtype=dtype, count=n, offset=8 * t).copy()
+
+    def struct_list(self, i):
+        if i >= self.np:
+            return []
+        l = self.m.list_at(self.seg, self.ptr_word(i))
+        if l is None:
+            return []
+        s, t, es, n = l
+        assert es == 7, "expected composite list"
+        tag = self.m.word(s, t)
+        cnt = (tag >> 2) & ((1 << 30) - 1)
+        dw, npt = (tag >> 32) & 0xFFFF, tag >> 48
+        step = dw + npt
+        return [_Struct(self.m, s, t + 1 + j * step, dw, npt) for j in range(cnt)]
+
+
+def read_msh(path) -> SketchDB:
+    data = open(path, "rb").read()
+    m = _Msg(data)
+    root = m.struct_at(0, 0)
+    db = SketchDB()
+    db.k = root.u32(0)
+    db.window_size = root.u32(4)
+    db.sketch_size = root.u32(8)
+    db.noncanonical = root.bit(97)
+    db.preserve_case = root.bit(98)
+    db.seed = root.u32(20, default=42)
+    db.alphabet = root.text(3) or "ACGT"
+    rl = m.struct_at(root.seg, root.ptr_word(1))
+    if rl is None:
+        rl = m.struct_at(root.seg, root.ptr_word(0))  # referenceListOld
+    refs = rl.struct_list(0) if rl is not None else []
+    names, comments, lengths, hl = [], [], [], []
+    use64 = db.k > 16
+    for r in refs:
+        names.append(r.text(2))
+        comments.append(r.text(3))
+        L64 = r.u64(8)
+        lengths.append(L64 if L64 else r.u32(0))
+        h = r.prim_list(5, np.uint64) if use64 else r.prim_list(4, np.uint32).astype(np.uint64)
+        hl.append(np.sort(h))
+    db.names, db.comments = names, comments
+    db.lengths = np.array(lengths, dtype=np.int64)
+    db.offsets = np.zeros(len(hl) + 1, dtype=np.int64)
+    if hl:
+        db.offsets[1:] = np.cumsum([len(h) for h in hl])
+        db.hashes = np.concatenate(hl).astype(np.uint64)
+    return db
+
+
+# ------------------------------------------------------------------ capnp writer
+class _Builder:
+    """Single-segment Cap'n Proto message builder (enough for the MinHash schema)."""
+
+    def __init__(self):
+        self.buf = bytearray()
+
+    def alloc(self, words):
+        w = len(self.buf) // 8
+        self.buf += b"\0" * (8 * words)
+        return w
+
+    def set_ptr(self, at_word, target_word, kind, hi):
+        off = target_word - (at_word + 1)
+        v = (kind & 3) | ((off & ((1 << 30) - 1)) << 2) | (hi << 32)
+        struct.pack_into("<Q", self.buf, 8 * at_word, v)
+
+    def struct_ptr(self, at, target, dw, np_):
+        self.set_ptr(at, target, 0, dw | (np_ << 16))
+
+    def text(self, at, s: str):
+        b = s.encode() + b"\0"
+        w = self.alloc((len(b) + 7) // 8)
+        self.buf[8 * w:8 * w + len(b)] = b
+        self.set_ptr(at, w, 1, 2 | (len(b) << 3))
+
+    def prim_list(self, at, arr: np.ndarray, es: int):
+        b = arr.tobytes()
+        w = self.alloc((len(b) + 7) // 8)
+        self.buf[8 * w:8 * w + len(b)] = b
+        self.set_ptr(at, w, 1, es | (len(arr) << 3))
+
+    def message(self):
+        n = len(self.buf) // 8
+        return struct.pack("<II", 0, n) + bytes(self.buf)
+
+
+def write_msh(db: SketchDB, path):
+    b = _Builder()
+    root_ptr = b.alloc(1)
+    root = b.alloc(3 + 4)
+    b.struct_ptr(root_ptr, root, 3, 4)
+    struct.pack_into("<III", b.buf, 8 * root, db.k, db.window_size, db.sketch_size)
+    flags = (int(db.noncanonical) << 1) | (int(db.preserve_case) << 2)
+    b.buf[8 * root + 12] = flags
+    struct.pack_into("<f", b.buf, 8 * root + 16, 0.0)
+    struct.pack_into("<I", b.buf, 8 * root + 20, db.seed ^ 42)
+    rl = b.alloc(1)
+    b.struct_ptr(root + 3 + 1, rl, 0, 1)
+    n = db.n_refs
+    DW, NP = 2, 7
+    tag = b.alloc(1 + n * (DW + NP))
+    b.set_ptr(rl, tag, 1, 7 | ((n * (DW + NP)) << 3))
+    struct.pack_into("<Q", b.buf, 8 * tag, (n << 2) | (DW << 32) | (NP << 48))
+    for i in range(n):
+        e = tag + 1 + i * (DW + NP)
+        L = int(db.lengths[i]) if len(db.lengths) > i else 0
+        struct.pack_into("<I", b.buf, 8 * e, L & 0xFFFFFFFF)
+        struct.pack_into("<Q", b.buf, 8 * e + 8, L)
+        p = e + DW
+        b.text(p + 2, db.names[i])
+        b.text(p + 3, db.comments[i] if i < len(db.comments) else "")
+        b.prim_list(p + 5, np.ascontiguousarray(db.ref_hashes(i), dtype=np.uint64), 5)
+    b.text(root + 3 + 3, db.alphabet)
+    with open(path, "wb") as f:
+        f.write(b.message())
+
+
+def save_npz(db: SketchDB, path):
+    np.savez(path, k=db.k, seed=db.seed, sketch_size=db.sketch_size, alphabet=db.alphabet,
+             preserve_case=db.preserve_case, noncanonical=db.noncanonical,
+             names=np.array(db.names, dtype=object).astype(str), comments=np.array(db.comments, dtype=object).astype(str),
+             lengths=db.lengths, offsets=db.offsets, hashes=db.hashes)
+
+
+def load_db(path) -> SketchDB:
+    p = str(path)
+    if p.endswith(".npz"):
+        z = np.load(p, allow_pickle=False)
+        return SketchDB(k=int(z["k"]), seed=int(z["seed"]), sketch_size=int(z["sketch_size"]), alphabet=str(z["alphabet"]),
+                        preserve_case=bool(z["preserve_case"]), noncanonical=bool(z["noncanonical"]),
+                        names=[str(x) for x in z["names"]], comments=[str(x) for x in z["comments"]],
+                        lengths=z["lengths"].astype(np.int64), offsets=z["offsets"].astype(np.int64),
+                        hashes=z["hashes"].astype(np.uint64))
+    return read_msh(p)

@@ -1,0 +1,84 @@
+/* hymet_gpu.h -- C ABI of libhymet_gpu.so, the MI355X (gfx950) implementation of HYMET's
+ * contig-classification hot path (Mash screen -> candidate limit -> minimizer
+ * seed-chain mapping -> PAF -> weighted LCA).
+ *
+ * Drop-in boundary.  The reference calls each stage as a subprocess:
+ *   scripts/mash.sh:14              mash screen -p 8 -v 0.9 DB input/ *.fna      -> hymet_screen_*
+ *   scripts/minimap2.sh:12          minimap2 -I2g -d reference.mmi refs.fasta    -> hymet_mm_index_*
+ *   scripts/minimap2.sh:23          minimap2 -x asm10 reference.mmi input/ *.fna -> hymet_mm_map_*
+ *   scripts/classification_cami.py:290-308 (_process_one / _weighted_lca)      -> hymet_lca_*
+ *   scripts/classification.py:141-157      (process_query / determine_lca)     -> hymet_lca_*
+ * The Python drop-ins in scripts/ keep those scripts' argv/file/exit-code contracts and
+ * bind this ABI with ctypes (hymet_amd/_lib.py); INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - every entry point returns 0 on success, a negative HYMET_E* code on failure;
+ *     hymet_last_error() returns a thread-local message for the last failure.
+ *   - pointers named d_* are DEVICE pointers (HBM), owned by the caller (the Python host
+ *     allocates them through torch); h_* pointers are host pointers.
+ *   - all device work is enqueued on the context's stream (hymet_set_stream) and is
+ *     asynchronous unless the function says it synchronises.
+ *   - no torch / HIP types appear in signatures; a stream is passed as void*.
+ */
+#ifndef HYMET_GPU_H
+#define HYMET_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HYMET_OK 0
+#define HYMET_E_HIP (-1)       /* a HIP runtime call failed */
+#define HYMET_E_ARG (-2)       /* invalid argument / unsupported parameter */
+#define HYMET_E_CAPACITY (-3)  /* caller-provided buffer too small; retry with the size reported */
+
+typedef struct hymet_ctx hymet_ctx;
+
+/* ---------------------------------------------------------------- context */
+int hymet_init(int device, hymet_ctx **out);
+int hymet_destroy(hymet_ctx *ctx);
+const char *hymet_last_error(void);
+int hymet_set_stream(hymet_ctx *ctx, void *hip_stream);
+int hymet_sync(hymet_ctx *ctx);
+int hymet_version(void);
+
+/* ------------------------------------------------------- sequence packing
+ * ASCII bases (device) -> 2-bit codes (16 bases per uint32, base i at bits 2*(i%16)) and an
+ * invalid-base bitmask (32 bases per uint32).  `alphabet`: 0 = Mash ACGT with upper-casing
+ * (CommandScreen hashSequence), 1 = Mash with preserveCase, 2 = minimap2 seq_nt4_table
+ * (ACGTU, either case).  n_words2b = ceil(n/16), n_words_mask = ceil(n/32). */
+int hymet_pack(hymet_ctx *ctx, const uint8_t *d_ascii, int64_t n, int alphabet,
+               uint32_t *d_2b, uint32_t *d_mask);
+
+/* ------------------------------------------------------------ Mash screen
+ * Replaces `mash screen` (scripts/mash.sh:14): one open-addressing table of the distinct
+ * sketch hashes of a DB, counts of every pooled canonical k-mer hash that hits it, and the
+ * per-reference shared / median-depth statistics. */
+int64_t hymet_screen_table_slots(int64_t n_hashes);
+/* d_keys: n_slots uint64; d_slot_of: n_hashes int64 (slot of each input hash, n_slots for
+ * the reserved all-ones key).  Resets d_keys itself. */
+int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n_hashes,
+                             uint64_t *d_keys, int64_t n_slots, int64_t *d_slot_of);
+/* Hash every valid canonical k-mer of the packed pool (k in 17..32, MurmurHash3_x64_128
+ * word 0 with `seed`), probe ndb (<= 4) tables, count hits into d_counts[i] (n_slots[i]+1
+ * uint32 each, caller-zeroed), and append every hash < cand_thr to d_cand (bottom-s
+ * candidates; d_cand_n counts appends, may exceed cand_cap).  d_nkmers += valid k-mers.
+ * seq_begin/seq_end limit the k-mer START positions processed (for sharding). */
+int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask,
+                       int64_t n_bases, int64_t pos_begin, int64_t pos_end, int k, uint32_t seed,
+                       int ndb, const uint64_t *const *h_d_keys, const int64_t *h_n_slots,
+                       uint32_t *const *h_d_counts, uint64_t cand_thr, uint64_t *d_cand,
+                       int64_t cand_cap, unsigned long long *d_cand_n,
+                       unsigned long long *d_nkmers);
+/* Per reference r (hashes d_ref_off[r]..d_ref_off[r+1] of the table input):
+ * shared[r] = #hashes with count > 0; median[r] = sorted positive counts[shared/2]. */
+int hymet_screen_stats(hymet_ctx *ctx, const int64_t *d_ref_off, int64_t n_refs,
+                       const int64_t *d_slot_of, const uint32_t *d_counts, uint32_t *d_shared,
+                       uint32_t *d_median);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,41 @@
+"""The C-ABI library loads on the CPU host and exports every symbol include/*.h declares
+(no compute calls: there is no GPU here)."""
+import ctypes
+import re
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared_symbols():
+    names = set()
+    for h in (ROOT / "include").glob("*.h"):
+        txt = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        names.update(re.findall(r"\b(hymet_[a-z0-9_]+)\s*\(", txt))
+    return sorted(names)
+
+
+def test_library_exports_every_declared_symbol():
+    from hymet_amd import _lib
+    lib = _lib.load()
+    syms = declared_symbols()
+    assert len(syms) >= 10
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_bindings_cover_declared_symbols():
+    from hymet_amd import _lib
+    assert set(declared_symbols()) == set(_lib.exported_symbols())
+
+
+def test_error_path_without_gpu():
+    from hymet_amd import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    rc = lib.hymet_init(0, ctypes.byref(h))
+    if rc != 0:  # no device in the build container: must fail loudly with a message
+        assert lib.hymet_last_error()
+    else:
+        lib.hymet_destroy(h)
+    assert lib.hymet_version() >= 1

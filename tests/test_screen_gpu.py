@@ -1,0 +1,121 @@
+"""GPU screen vs the CPU oracle (bit-exact counts, shared, median, set size, output rows)."""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from tests._data import add_noise, mutate, rand_seq, revcomp
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    from hymet_amd._lib import Gpu
+    return Gpu(0)
+
+
+def _make_db(rng, genomes, k, seed, s, n_decoys=50):
+    from hymet_amd.msh import SketchDB
+    from oracle import oracle_lib
+    hl, names = [], []
+    for i, g in enumerate(genomes):
+        hl.append(np.sort(oracle_lib.sketch([g], k, seed, s)))
+        names.append(f"GCF_{i:09d}.1_genome{i}.fna.gz")
+    for j in range(n_decoys):
+        hl.append(np.sort(rng.integers(0, 2**63, size=s, dtype=np.int64).astype(np.uint64) * 2 + 1))
+        names.append(f"decoy_{j}")
+    off = np.zeros(len(hl) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(h) for h in hl])
+    return SketchDB(k=k, seed=seed, sketch_size=s, names=names, comments=[f"[1 seqs] {n} comment" for n in names],
+                    lengths=np.array([len(g) for g in genomes] + [10**6] * n_decoys), offsets=off,
+                    hashes=np.concatenate(hl))
+
+
+def _pool(rng, genomes, n_contigs, lo, hi, rate=0.01):
+    recs = []
+    for c in range(n_contigs):
+        g = genomes[int(rng.integers(len(genomes)))]
+        L = int(rng.integers(lo, hi))
+        st = int(rng.integers(0, len(g) - L))
+        s = mutate(rng, g[st:st + L], rate)
+        if rng.random() < 0.5:
+            s = revcomp(s)
+        if rng.random() < 0.3:
+            s = add_noise(rng, s)
+        recs.append((f"ctg{c}", "", s))
+    recs.append(("short", "", b"ACGTACGT"))   # shorter than k: skipped
+    recs.append(("empty", "", b""))
+    return recs
+
+
+@pytest.mark.parametrize("k,seed,s", [(21, 42, 1000), (17, 7, 500), (32, 42, 200), (25, 0, 300)])
+def test_screen_matches_oracle(gpu, k, seed, s):
+    from hymet_amd import screen as scr
+    from hymet_amd.seqio import DevicePool, from_records
+    from oracle import oracle_lib, select_oracle
+    rng = np.random.default_rng(k * 1000 + seed)
+    genomes = [rand_seq(rng, int(rng.integers(200_000, 400_000)), gc=0.4 + 0.05 * i) for i in range(6)]
+    db = _make_db(rng, genomes[:4], k, seed, s)
+    recs = _pool(rng, genomes, 120, 2_000, 30_000)
+    ss = from_records(recs)
+    pool = DevicePool(gpu, ss, DevicePool.ALPHA_MASH)
+    res = scr.screen(gpu, pool, [db])[0]
+    sh, md, set_size, nk = oracle_lib.screen([r[2] for r in recs], k, seed, s, [db.ref_hashes(i) for i in range(db.n_refs)])
+    assert res.n_kmers == nk
+    np.testing.assert_array_equal(res.shared, sh)
+    np.testing.assert_array_equal(res.median, md)
+    assert res.set_size == set_size
+    refs = [(db.names[i], db.comments[i], int(db.offsets[i + 1] - db.offsets[i])) for i in range(db.n_refs)]
+    assert res.lines() == select_oracle.screen_lines(refs, sh, md, set_size, k)
+    assert sum(1 for x in res.shared[:4] if x > 0) == 4
+
+
+def test_screen_three_dbs_one_pass(gpu):
+    from hymet_amd import screen as scr
+    from hymet_amd.seqio import DevicePool, from_records
+    from oracle import oracle_lib
+    rng = np.random.default_rng(5)
+    genomes = [rand_seq(rng, 150_000) for _ in range(5)]
+    dbs = [_make_db(rng, genomes[i:i + 2], 21, 42, 1000, n_decoys=10) for i in range(3)]
+    recs = _pool(rng, genomes, 40, 1_000, 20_000)
+    pool = DevicePool(gpu, from_records(recs), DevicePool.ALPHA_MASH)
+    out = scr.screen(gpu, pool, dbs)
+    for db, r in zip(dbs, out):
+        sh, md, set_size, nk = oracle_lib.screen([x[2] for x in recs], 21, 42, 1000, [db.ref_hashes(i) for i in range(db.n_refs)])
+        np.testing.assert_array_equal(r.shared, sh)
+        np.testing.assert_array_equal(r.median, md)
+        assert r.set_size == set_size and r.n_kmers == nk
+
+
+def test_screen_repetitive_pool_set_size(gpu):
+    """A pool with fewer distinct k-mers than s exercises the candidate re-run path."""
+    from hymet_amd import screen as scr
+    from hymet_amd.seqio import DevicePool, from_records
+    from oracle import oracle_lib
+    rng = np.random.default_rng(9)
+    unit = rand_seq(rng, 300)
+    recs = [(f"r{i}", "", unit * 200) for i in range(20)]
+    g = [rand_seq(rng, 50_000)]
+    db = _make_db(rng, g, 21, 42, 1000, n_decoys=3)
+    pool = DevicePool(gpu, from_records(recs), DevicePool.ALPHA_MASH)
+    r = scr.screen(gpu, pool, [db])[0]
+    sh, md, set_size, nk = oracle_lib.screen([x[2] for x in recs], 21, 42, 1000, [db.ref_hashes(i) for i in range(db.n_refs)])
+    assert r.set_size == set_size and r.n_kmers == nk
+
+
+def test_gpu_hash_kat(gpu):
+    """Each KAT string is a one-k-mer record: its canonical hash must hit the table."""
+    from hymet_amd import screen as scr
+    from hymet_amd.msh import SketchDB
+    from hymet_amd.seqio import DevicePool, from_records
+    kat = json.loads((Path(__file__).resolve().parent / "golden" / "murmur3_kat.json").read_text())
+    vecs = kat["zymo_canonical_k21_seed42"]
+    hs = np.array([int(v["h0"], 16) for v in vecs], dtype=np.uint64)
+    db = SketchDB(k=21, seed=42, sketch_size=len(vecs), names=[f"v{i}" for i in range(len(vecs))], comments=[""] * len(vecs),
+                  lengths=np.ones(len(vecs), np.int64), offsets=np.arange(len(vecs) + 1, dtype=np.int64), hashes=hs)
+    pool = DevicePool(gpu, from_records([(f"q{i}", "", v["s"].encode()) for i, v in enumerate(vecs)]), DevicePool.ALPHA_MASH)
+    r = scr.screen(gpu, pool, [db])[0]
+    # duplicates among the vectors make some counts > 1; every vector must be found
+    assert (r.shared == 1).all()
