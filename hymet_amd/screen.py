@@ -81,22 +81,28 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
     gpu.call("hymet_screen_count", ptr(pool.w2b), ptr(pool.wmask), n_bases, pos_begin, pos_end, k, seed,
              len(tables), keys_arr, slots_arr, cnt_arr, thr, ptr(cand), cap, ptr(cand_n), ptr(nk))
     n_kmers = int(nk.item())
+    dummy = gpu.zeros(1, torch.int64)
+
+    def rerun(thr_, cap_):
+        buf = gpu.empty(cap_, torch.int64)
+        cand_n.zero_()
+        gpu.call("hymet_screen_count", ptr(pool.w2b), ptr(pool.wmask), n_bases, pos_begin, pos_end, k, seed,
+                 0, keys_arr, slots_arr, cnt_arr, thr_, ptr(buf), cap_, ptr(cand_n), ptr(dummy))
+        return buf
+
     while True:
         n = int(cand_n.item())
-        vals = cand[:min(n, cap)].cpu().numpy().view(np.uint64)
-        bottom = _bottom_s(vals, s)
-        if n <= cap and (len(bottom) >= s or thr == U64_MAX):
+        if n > cap:  # overflow: same threshold again with an exact-size buffer (candidates only)
+            cap = n
+            cand = rerun(thr, cap)
+            n = int(cand_n.item())
+        bottom = _bottom_s(cand[:n].cpu().numpy().view(np.uint64), s)
+        if len(bottom) >= s or thr == U64_MAX:
             break
-        # too few distinct candidates under the threshold (repetitive pool) or overflow:
-        # re-run the hash pass in candidates-only mode (ndb = 0) with a new threshold.
-        if n > cap:
-            thr = int(bottom[-1]) if len(bottom) >= s else max(1, thr // 2)
-        else:
-            thr = U64_MAX if thr > U64_MAX // 16 else thr * 16
-        cand_n.zero_()
-        dummy = gpu.zeros(1, torch.int64)
-        gpu.call("hymet_screen_count", ptr(pool.w2b), ptr(pool.wmask), n_bases, pos_begin, pos_end, k, seed,
-                 0, keys_arr, slots_arr, cnt_arr, thr, ptr(cand), cap, ptr(cand_n), ptr(dummy))
+        # fewer than s distinct hashes under the threshold (repetitive pool): raise it
+        # monotonically and re-run the hash pass in candidates-only mode (ndb = 0)
+        thr = U64_MAX if thr > U64_MAX // 16 else thr * 16
+        cand = rerun(thr, cap)
     return counts, bottom, n_kmers
 
 
