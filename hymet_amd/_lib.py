@@ -28,6 +28,12 @@ _SIGS = {
     "hymet_screen_count": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _u32, _i32, _c.POINTER(_vp), _c.POINTER(_i64),
                                   _c.POINTER(_vp), _u64, _vp, _i64, _vp, _vp]),
     "hymet_screen_stats": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
+    "hymet_mm_sketch": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i64, _c.POINTER(_i64)]),
+    "hymet_mm_index_build": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _c.POINTER(_vp)]),
+    "hymet_mm_index_destroy": (_i32, [_vp]),
+    "hymet_mm_index_info": (_i32, [_vp, _c.POINTER(_i32), _c.POINTER(_i32), _c.POINTER(_i32), _c.POINTER(_i64)]),
+    "hymet_mm_index_max_occ": (_i32, [_vp, _vp, _c.c_float, _c.POINTER(_i32)]),
+    "hymet_mm_index_export": (_i32, [_vp, _vp, _vp, _vp]),
 }
 
 _lib = None

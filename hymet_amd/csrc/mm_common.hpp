@@ -1,0 +1,109 @@
+// Shared device/host helpers for the minimizer index and mapper (minimap2 restatement).
+#pragma once
+#include "common.hpp"
+
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <vector>
+
+namespace hymet {
+namespace mm {
+
+constexpr uint64_t kMax64 = ~0ull;
+constexpr int kChunk = 512;  // sequence positions per sketch thread
+
+// sketch.c hash64: invertible integer hash restricted to 2k bits
+__host__ __device__ __forceinline__ uint64_t hash64m(uint64_t key, uint64_t mask) {
+    key = (~key + (key << 21)) & mask;
+    key = key ^ key >> 24;
+    key = ((key + (key << 3)) + (key << 8)) & mask;
+    key = key ^ key >> 14;
+    key = ((key + (key << 2)) + (key << 4)) & mask;
+    key = key ^ key >> 28;
+    key = (key + (key << 31)) & mask;
+    return key;
+}
+// hit.c hash64 (Thomas Wang, full 64 bits)
+__host__ __device__ __forceinline__ uint64_t hash64(uint64_t key) {
+    key = (~key + (key << 21));
+    key = key ^ key >> 24;
+    key = ((key + (key << 3)) + (key << 8));
+    key = key ^ key >> 14;
+    key = ((key + (key << 2)) + (key << 4));
+    key = key ^ key >> 28;
+    key = (key + (key << 31));
+    return key;
+}
+
+// Stream-ordered device scratch, freed at scope exit.
+struct DevBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    hipStream_t s = nullptr;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    hipError_t alloc(size_t bytes, hipStream_t st) {
+        release();
+        s = st;
+        n = bytes;
+        if (bytes == 0) bytes = 16;
+        return hipMallocAsync(&p, bytes, st);
+    }
+    void release() {
+        if (p) (void)hipFreeAsync(p, s);
+        p = nullptr;
+        n = 0;
+    }
+    template <typename T>
+    T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+struct SketchParams {
+    const uint32_t *w2b;
+    const uint32_t *wm;
+    const int64_t *seq_start;  // pool offset of every sequence
+    const int64_t *seq_len;
+    const int64_t *chunk_off;  // n_seq + 1: first chunk of every sequence
+    int64_t n_chunks;
+    int n_seq;
+    int k;
+    int warm;
+    int rid_mode;  // 0: rid = 0 (queries) ; 1: rid = sequence index (index build)
+    uint32_t *counts;          // per chunk (count pass)
+    const int64_t *out_off;    // per chunk (write pass)
+    uint64_t *out_x;
+    uint64_t *out_y;
+};
+
+// Count (WRITE=false) or emit (WRITE=true) the minimizers of every chunk; defined in
+// mm_sketch.hip and used by the index builder and the mapper.
+int launch_sketch(hymet_ctx *ctx, int w, bool write, const SketchParams &P);
+
+// exclusive scan of n uint32 counts into int64 offsets; returns the total through *total
+int exclusive_scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, int64_t *total);
+
+// Minimizers of a packed set of sequences: host-side chunk bookkeeping + both passes.
+// On success d_x / d_y hold *n_out minimizers in sequence order (sequence-major); if
+// d_seq_off is non-null it receives n_seq+1 per-sequence offsets (device, int64).
+int sketch_sequences(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask, const int64_t *h_starts,
+                     const int64_t *h_lens, int n_seq, int w, int k, int rid_mode, DevBuf &d_x, DevBuf &d_y,
+                     int64_t *n_out, DevBuf *d_seq_off);
+
+}  // namespace mm
+}  // namespace hymet
+
+// opaque index handle (include/hymet_gpu.h)
+struct hymet_mm_index {
+    int w = 10, k = 15, n_seq = 0;
+    int64_t n_pos = 0;
+    int64_t n_buckets = 0;   // 4^k direct-address buckets
+    uint32_t *d_koff = nullptr;   // n_buckets + 1 offsets into d_pos
+    uint64_t *d_pos = nullptr;    // y = rid<<32 | pos<<1 | strand, sorted per bucket
+    uint32_t *d_hash = nullptr;   // bucket of every d_pos entry (kept for export / stats)
+    int64_t *d_len = nullptr;     // sequence lengths
+    std::vector<int64_t> h_len;
+    int device = 0;
+};

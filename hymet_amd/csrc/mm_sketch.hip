@@ -1,0 +1,404 @@
+// Minimizer sketching + the direct-address minimizer index (replaces `minimap2 -I2g -d`,
+// scripts/minimap2.sh:12).
+//
+// mm_sketch_kernel<W, WRITE>: one thread = one 512-position chunk of one sequence.  The
+// thread replays minimap2's sequential robust-winnowing sketch (sketch.c mm_sketch) from
+// a warm-up point w+k+16 bases before its chunk, emitting only the pushes made while it is
+// inside the chunk (and the end-of-sequence flush).  After warm-up the winnowing state
+// (window contents, current minimum = rightmost minimum of the window, the valid-base run)
+// equals the state of a single pass over the whole sequence, so the concatenated chunk
+// outputs are bit-identical to mm_sketch, push order included.  The
+// window lives in registers as a shift register (W compile-time), so the oldest slot is
+// index 0 and "the minimum left the window" is min_step == step - W.
+// Two launches: count (WRITE=false) -> exclusive scan -> write (WRITE=true).
+//
+// Index: minimizer (hash = x>>8, y) pairs are sorted by (hash, y) with two stable rocPRIM
+// radix passes and laid out as a CSR over ALL 4^k hash values (k <= 15: 2^30+1 uint32
+// offsets = 4.3 GB per index part, which MI355X's 288 GB HBM affords), so a seed lookup is
+// two adjacent loads instead of a hash-table probe chain.
+#include "mm_common.hpp"
+
+namespace hymet {
+namespace mm {
+namespace {
+
+template <int W, bool WRITE>
+__global__ __launch_bounds__(256) void mm_sketch_kernel(SketchParams P) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= P.n_chunks) return;
+    // sequence owning chunk g: last s with chunk_off[s] <= g
+    int lo = 0, hi = P.n_seq - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (P.chunk_off[mid] <= g) lo = mid;
+        else hi = mid - 1;
+    }
+    const int s = lo;
+    const int64_t L = P.seq_len[s];
+    const int64_t cst = (g - P.chunk_off[s]) * kChunk;
+    const int64_t cen = min(cst + kChunk, L);
+    const int64_t wst = max((int64_t)0, cst - P.warm);
+    const int64_t base = P.seq_start[s];
+    const int k = P.k;
+    const uint64_t shift1 = 2 * (k - 1), mask = (1ULL << 2 * k) - 1;
+    const uint64_t ridhi = P.rid_mode ? ((uint64_t)s << 32) : 0;
+    uint64_t km0 = 0, km1 = 0;
+    int l = 0, kmer_span = 0;
+    uint64_t bx[W], by[W];
+#pragma unroll
+    for (int j = 0; j < W; j++) bx[j] = by[j] = kMax64;
+    uint64_t minx = kMax64, miny = kMax64;
+    int64_t step = 0, min_step = -W;
+    uint32_t cnt = 0;
+    const int64_t out0 = WRITE ? P.out_off[g] : 0;
+    uint32_t cw = 0, mw = 0;
+    auto push = [&](uint64_t x, uint64_t y) {
+        if (WRITE) {
+            P.out_x[out0 + cnt] = x;
+            P.out_y[out0 + cnt] = y;
+        }
+        cnt++;
+    };
+    for (int64_t i = wst; i < cen; ++i) {
+        const int64_t pi = base + i;
+        if (i == wst || (pi & 15) == 0) cw = P.w2b[pi >> 4];
+        if (i == wst || (pi & 31) == 0) mw = P.wm[pi >> 5];
+        const bool emit = i >= cst;
+        const uint32_t c = (cw >> (2 * (pi & 15))) & 3u;
+        const bool bad = (mw >> (pi & 31)) & 1u;
+        uint64_t ix = kMax64, iy = kMax64;
+        if (!bad) {
+            kmer_span = l + 1 < k ? l + 1 : k;
+            km0 = (km0 << 2 | c) & mask;
+            km1 = (km1 >> 2) | (uint64_t)(3u ^ c) << shift1;
+            if (km0 == km1) continue;  // symmetric k-mer: no window slot (sketch.c)
+            const int z = km0 < km1 ? 0 : 1;
+            ++l;
+            if (l >= k && kmer_span < 256) {
+                ix = hash64m(z ? km1 : km0, mask) << 8 | (uint64_t)kmer_span;
+                iy = ridhi | (uint64_t)(uint32_t)i << 1 | (uint64_t)z;
+            }
+        } else {
+            l = 0;
+            kmer_span = 0;
+        }
+        // buf[buf_pos] = info  ==  shift the register file, newest at W-1
+#pragma unroll
+        for (int j = 0; j < W - 1; j++) {
+            bx[j] = bx[j + 1];
+            by[j] = by[j + 1];
+        }
+        bx[W - 1] = ix;
+        by[W - 1] = iy;
+        if (l == W + k - 1 && minx != kMax64 && emit) {  // first window: identical k-mers
+#pragma unroll
+            for (int j = 0; j < W - 1; j++)
+                if (minx == bx[j] && by[j] != miny) push(bx[j], by[j]);
+        }
+        if (ix <= minx) {
+            if (l >= W + k && minx != kMax64 && emit) push(minx, miny);
+            minx = ix;
+            miny = iy;
+            min_step = step;
+        } else if (min_step == step - W) {  // the minimum just left the window
+            if (l >= W + k - 1 && minx != kMax64 && emit) push(minx, miny);
+            minx = kMax64;
+#pragma unroll
+            for (int j = 0; j < W; j++)
+                if (minx >= bx[j]) {
+                    minx = bx[j];
+                    miny = by[j];
+                    min_step = step - (W - 1 - j);
+                }
+            if (l >= W + k - 1 && minx != kMax64 && emit) {
+#pragma unroll
+                for (int j = 0; j < W; j++)
+                    if (minx == bx[j] && miny != by[j]) push(bx[j], by[j]);
+            }
+        }
+        ++step;
+    }
+    if (cen == L && minx != kMax64) push(minx, miny);
+    if (!WRITE) P.counts[g] = cnt;
+}
+
+__global__ void bucket_hist_kernel(const uint64_t *__restrict__ x, int64_t n, uint32_t *__restrict__ cnt,
+                                   uint32_t *__restrict__ hash_out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t h = (uint32_t)(x[i] >> 8);
+    hash_out[i] = h;
+    atomicAdd(&cnt[h], 1u);
+}
+
+__global__ void occ_hist_kernel(const uint32_t *__restrict__ koff, int64_t n_buckets, uint32_t *hist, int cap) {
+    for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_buckets;
+         h += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = koff[h + 1] - koff[h];
+        if (c) atomicAdd(&hist[c < (uint32_t)cap ? c : (uint32_t)cap], 1u);
+    }
+}
+
+}  // namespace
+
+int launch_sketch(hymet_ctx *ctx, int w, bool write, const SketchParams &P) {
+    if (P.n_chunks <= 0) return HYMET_OK;
+    const dim3 grid((unsigned)cdiv(P.n_chunks, 256)), block(256);
+    switch (w) {
+#define HY_W(WW)                                                                                   \
+    case WW:                                                                                       \
+        if (write) hipLaunchKernelGGL((mm_sketch_kernel<WW, true>), grid, block, 0, ctx->stream, P); \
+        else hipLaunchKernelGGL((mm_sketch_kernel<WW, false>), grid, block, 0, ctx->stream, P);    \
+        break;
+        HY_W(2) HY_W(3) HY_W(4) HY_W(5) HY_W(6) HY_W(7) HY_W(8) HY_W(9) HY_W(10) HY_W(11) HY_W(12)
+        HY_W(13) HY_W(14) HY_W(15) HY_W(16) HY_W(17) HY_W(18) HY_W(19) HY_W(20) HY_W(24) HY_W(25) HY_W(28) HY_W(32)
+#undef HY_W
+    default:
+        return fail(HYMET_E_ARG, "minimizer window w must be one of 2..20, 24, 25, 28, 32");
+    }
+    HY_CHECK_LAUNCH("mm_sketch_kernel");
+    return HYMET_OK;
+}
+
+int exclusive_scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, int64_t *total) {
+    *total = 0;
+    if (n <= 0) return HYMET_OK;
+    size_t tmp = 0;
+    HY_HIP(rocprim::exclusive_scan(nullptr, tmp, in, out, (int64_t)0, (size_t)n, rocprim::plus<int64_t>(), ctx->stream));
+    DevBuf t;
+    HY_HIP(t.alloc(tmp, ctx->stream));
+    HY_HIP(rocprim::exclusive_scan(t.p, tmp, in, out, (int64_t)0, (size_t)n, rocprim::plus<int64_t>(), ctx->stream));
+    int64_t last_off = 0;
+    uint32_t last_cnt = 0;
+    HY_HIP(hipMemcpyAsync(&last_off, out + n - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HY_HIP(hipMemcpyAsync(&last_cnt, in + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HY_HIP(hipStreamSynchronize(ctx->stream));
+    *total = last_off + last_cnt;
+    return HYMET_OK;
+}
+
+int sketch_sequences(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask, const int64_t *h_starts,
+                     const int64_t *h_lens, int n_seq, int w, int k, int rid_mode, DevBuf &d_x, DevBuf &d_y,
+                     int64_t *n_out, DevBuf *d_seq_off) {
+    *n_out = 0;
+    if (k < 1 || k > 28) return fail(HYMET_E_ARG, "k must be in 1..28 (minimap2)");
+    std::vector<int64_t> coff(n_seq + 1, 0);
+    for (int i = 0; i < n_seq; i++) coff[i + 1] = coff[i] + (h_lens[i] + kChunk - 1) / kChunk;
+    const int64_t n_chunks = coff[n_seq];
+    DevBuf d_starts, d_lens, d_coff, d_cnt, d_off;
+    HY_HIP(d_starts.alloc(8 * (size_t)n_seq, ctx->stream));
+    HY_HIP(d_lens.alloc(8 * (size_t)n_seq, ctx->stream));
+    HY_HIP(d_coff.alloc(8 * (size_t)(n_seq + 1), ctx->stream));
+    HY_HIP(hipMemcpyAsync(d_starts.p, h_starts, 8 * (size_t)n_seq, hipMemcpyHostToDevice, ctx->stream));
+    HY_HIP(hipMemcpyAsync(d_lens.p, h_lens, 8 * (size_t)n_seq, hipMemcpyHostToDevice, ctx->stream));
+    HY_HIP(hipMemcpyAsync(d_coff.p, coff.data(), 8 * (size_t)(n_seq + 1), hipMemcpyHostToDevice, ctx->stream));
+    HY_HIP(d_cnt.alloc(4 * (size_t)(n_chunks + 1), ctx->stream));
+    HY_HIP(d_off.alloc(8 * (size_t)(n_chunks + 1), ctx->stream));
+    SketchParams P{};
+    P.w2b = d_2b;
+    P.wm = d_mask;
+    P.seq_start = d_starts.as<int64_t>();
+    P.seq_len = d_lens.as<int64_t>();
+    P.chunk_off = d_coff.as<int64_t>();
+    P.n_chunks = n_chunks;
+    P.n_seq = n_seq;
+    P.k = k;
+    P.warm = w + k + 16;
+    P.rid_mode = rid_mode;
+    P.counts = d_cnt.as<uint32_t>();
+    int rc = launch_sketch(ctx, w, false, P);
+    if (rc) return rc;
+    int64_t total = 0;
+    rc = exclusive_scan_u32_i64(ctx, d_cnt.as<uint32_t>(), d_off.as<int64_t>(), n_chunks, &total);
+    if (rc) return rc;
+    HY_HIP(d_x.alloc(8 * (size_t)total, ctx->stream));
+    HY_HIP(d_y.alloc(8 * (size_t)total, ctx->stream));
+    P.out_off = d_off.as<int64_t>();
+    P.out_x = d_x.as<uint64_t>();
+    P.out_y = d_y.as<uint64_t>();
+    rc = launch_sketch(ctx, w, true, P);
+    if (rc) return rc;
+    if (d_seq_off) {
+        // per-sequence offsets = chunk offsets sampled at each sequence's first chunk
+        std::vector<int64_t> so(n_seq + 1);
+        std::vector<int64_t> choff(n_chunks + 1);
+        if (n_chunks) HY_HIP(hipMemcpyAsync(choff.data(), d_off.p, 8 * (size_t)n_chunks, hipMemcpyDeviceToHost, ctx->stream));
+        HY_HIP(hipStreamSynchronize(ctx->stream));
+        choff[n_chunks] = total;
+        for (int i = 0; i <= n_seq; i++) so[i] = choff[coff[i]];
+        HY_HIP(d_seq_off->alloc(8 * (size_t)(n_seq + 1), ctx->stream));
+        HY_HIP(hipMemcpyAsync(d_seq_off->p, so.data(), 8 * (size_t)(n_seq + 1), hipMemcpyHostToDevice, ctx->stream));
+        HY_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    *n_out = total;
+    return HYMET_OK;
+}
+
+}  // namespace mm
+}  // namespace hymet
+
+using namespace hymet;
+using namespace hymet::mm;
+
+extern "C" {
+
+int hymet_mm_sketch(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask, const int64_t *h_starts,
+                    const int64_t *h_lens, int32_t n_seq, int w, int k, int rid_mode, uint64_t *h_x, uint64_t *h_y,
+                    int64_t cap, int64_t *n_out) {
+    HY_ARG(ctx && d_2b && d_mask && n_out, "hymet_mm_sketch: null argument");
+    HY_HIP(hipSetDevice(ctx->device));
+    DevBuf dx, dy;
+    int64_t n = 0;
+    int rc = sketch_sequences(ctx, d_2b, d_mask, h_starts, h_lens, n_seq, w, k, rid_mode, dx, dy, &n, nullptr);
+    if (rc) return rc;
+    *n_out = n;
+    if (n > cap) return fail(HYMET_E_CAPACITY, "hymet_mm_sketch: output capacity too small");
+    if (n) {
+        HY_HIP(hipMemcpyAsync(h_x, dx.p, 8 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+        HY_HIP(hipMemcpyAsync(h_y, dy.p, 8 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HY_HIP(hipStreamSynchronize(ctx->stream));
+    return HYMET_OK;
+}
+
+int hymet_mm_index_build(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask, const int64_t *h_starts,
+                         const int64_t *h_lens, int32_t n_seq, int w, int k, hymet_mm_index **out) {
+    HY_ARG(ctx && d_2b && d_mask && out, "hymet_mm_index_build: null argument");
+    HY_ARG(k >= 1 && k <= 15, "hymet_mm_index_build: direct-address index supports k <= 15 (minimap2 default 15)");
+    HY_ARG(n_seq >= 0, "hymet_mm_index_build: n_seq < 0");
+    HY_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    DevBuf dx, dy;
+    int64_t n = 0;
+    int rc = sketch_sequences(ctx, d_2b, d_mask, h_starts, h_lens, n_seq, w, k, 1, dx, dy, &n, nullptr);
+    if (rc) return rc;
+    HY_ARG(n < (1ll << 32), "hymet_mm_index_build: more than 2^32 minimizers in one index part");
+    const int64_t nb = 1ll << (2 * k);
+    hymet_mm_index *idx = new hymet_mm_index();
+    idx->w = w, idx->k = k, idx->n_seq = n_seq, idx->n_pos = n, idx->n_buckets = nb, idx->device = ctx->device;
+    idx->h_len.assign(h_lens, h_lens + n_seq);
+    auto cleanup = [&](int code) {
+        hymet_mm_index_destroy(idx);
+        return code;
+    };
+    if (hipMalloc(&idx->d_koff, 4 * (size_t)(nb + 1)) != hipSuccess || hipMalloc(&idx->d_pos, 8 * (size_t)(n + 1)) != hipSuccess ||
+        hipMalloc(&idx->d_hash, 4 * (size_t)(n + 1)) != hipSuccess || hipMalloc(&idx->d_len, 8 * (size_t)(n_seq + 1)) != hipSuccess)
+        return cleanup(fail(HYMET_E_HIP, "hymet_mm_index_build: out of device memory"));
+    if (n_seq) {
+        if (hipMemcpyAsync(idx->d_len, h_lens, 8 * (size_t)n_seq, hipMemcpyHostToDevice, st) != hipSuccess)
+            return cleanup(fail(HYMET_E_HIP, "copy lengths"));
+    }
+    // bucket histogram (counts) -> CSR offsets
+    DevBuf cnt, hsh, hsh2, pos2;
+    if (cnt.alloc(4 * (size_t)(nb + 1), st) || hsh.alloc(4 * (size_t)(n + 1), st) || hsh2.alloc(4 * (size_t)(n + 1), st) ||
+        pos2.alloc(8 * (size_t)(n + 1), st))
+        return cleanup(fail(HYMET_E_HIP, "hymet_mm_index_build: out of device memory (scratch)"));
+    if (hipMemsetAsync(cnt.p, 0, 4 * (size_t)(nb + 1), st)) return cleanup(fail(HYMET_E_HIP, "memset"));
+    if (n) {
+        hipLaunchKernelGGL(bucket_hist_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, dx.as<uint64_t>(), n,
+                           cnt.as<uint32_t>(), hsh.as<uint32_t>());
+        if (hipGetLastError() != hipSuccess) return cleanup(fail(HYMET_E_HIP, "bucket_hist_kernel"));
+    }
+    {
+        size_t tmp = 0;
+        if (rocprim::exclusive_scan(nullptr, tmp, cnt.as<uint32_t>(), idx->d_koff, 0u, (size_t)(nb + 1),
+                                    rocprim::plus<uint32_t>(), st))
+            return cleanup(fail(HYMET_E_HIP, "scan size"));
+        DevBuf t;
+        if (t.alloc(tmp, st) || rocprim::exclusive_scan(t.p, tmp, cnt.as<uint32_t>(), idx->d_koff, 0u, (size_t)(nb + 1),
+                                                         rocprim::plus<uint32_t>(), st))
+            return cleanup(fail(HYMET_E_HIP, "scan"));
+    }
+    // sort (hash, y): y first, then a stable pass on the hash (2k bits)
+    if (n) {
+        size_t tmp1 = 0, tmp2 = 0;
+        if (rocprim::radix_sort_pairs(nullptr, tmp1, dy.as<uint64_t>(), pos2.as<uint64_t>(), hsh.as<uint32_t>(),
+                                      hsh2.as<uint32_t>(), (size_t)n, 0, 64, st) ||
+            rocprim::radix_sort_pairs(nullptr, tmp2, hsh2.as<uint32_t>(), idx->d_hash, pos2.as<uint64_t>(), idx->d_pos,
+                                      (size_t)n, 0, 2 * k, st))
+            return cleanup(fail(HYMET_E_HIP, "sort size"));
+        DevBuf t;
+        if (t.alloc(tmp1 > tmp2 ? tmp1 : tmp2, st) ||
+            rocprim::radix_sort_pairs(t.p, tmp1, dy.as<uint64_t>(), pos2.as<uint64_t>(), hsh.as<uint32_t>(),
+                                      hsh2.as<uint32_t>(), (size_t)n, 0, 64, st) ||
+            rocprim::radix_sort_pairs(t.p, tmp2, hsh2.as<uint32_t>(), idx->d_hash, pos2.as<uint64_t>(), idx->d_pos,
+                                      (size_t)n, 0, 2 * k, st))
+            return cleanup(fail(HYMET_E_HIP, "sort"));
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return cleanup(fail(HYMET_E_HIP, "hymet_mm_index_build: sync"));
+    *out = idx;
+    return HYMET_OK;
+}
+
+int hymet_mm_index_destroy(hymet_mm_index *idx) {
+    if (!idx) return HYMET_OK;
+    (void)hipSetDevice(idx->device);
+    if (idx->d_koff) (void)hipFree(idx->d_koff);
+    if (idx->d_pos) (void)hipFree(idx->d_pos);
+    if (idx->d_hash) (void)hipFree(idx->d_hash);
+    if (idx->d_len) (void)hipFree(idx->d_len);
+    delete idx;
+    return HYMET_OK;
+}
+
+int hymet_mm_index_info(const hymet_mm_index *idx, int32_t *w, int32_t *k, int32_t *n_seq, int64_t *n_pos) {
+    HY_ARG(idx, "hymet_mm_index_info: null index");
+    if (w) *w = idx->w;
+    if (k) *k = idx->k;
+    if (n_seq) *n_seq = idx->n_seq;
+    if (n_pos) *n_pos = idx->n_pos;
+    return HYMET_OK;
+}
+
+// index.c mm_idx_cal_max_occ: ((1-f) * n_keys)-th smallest per-key count, + 1
+int hymet_mm_index_max_occ(hymet_ctx *ctx, const hymet_mm_index *idx, float frac, int32_t *out) {
+    HY_ARG(ctx && idx && out, "hymet_mm_index_max_occ: null argument");
+    if (frac <= 0.f) {
+        *out = INT32_MAX;
+        return HYMET_OK;
+    }
+    HY_HIP(hipSetDevice(ctx->device));
+    const int cap = 1 << 20;
+    DevBuf hist;
+    HY_HIP(hist.alloc(4 * (size_t)(cap + 1), ctx->stream));
+    HY_HIP(hipMemsetAsync(hist.p, 0, 4 * (size_t)(cap + 1), ctx->stream));
+    hipLaunchKernelGGL(occ_hist_kernel, dim3(ctx->n_cu * 8), dim3(256), 0, ctx->stream, idx->d_koff, idx->n_buckets,
+                       hist.as<uint32_t>(), cap);
+    HY_CHECK_LAUNCH("occ_hist_kernel");
+    std::vector<uint32_t> h(cap + 1);
+    HY_HIP(hipMemcpyAsync(h.data(), hist.p, 4 * (size_t)(cap + 1), hipMemcpyDeviceToHost, ctx->stream));
+    HY_HIP(hipStreamSynchronize(ctx->stream));
+    uint64_t n_keys = 0;
+    for (int c = 1; c <= cap; c++) n_keys += h[c];
+    if (n_keys == 0) {
+        *out = INT32_MAX;
+        return HYMET_OK;
+    }
+    const uint64_t kk = (uint64_t)(uint32_t)((1. - frac) * (double)n_keys);
+    uint64_t acc = 0;
+    int val = cap;
+    for (int c = 1; c <= cap; c++) {
+        acc += h[c];
+        if (acc > kk) {
+            val = c;
+            break;
+        }
+    }
+    HY_ARG(val < cap, "hymet_mm_index_max_occ: occurrence above histogram range");
+    *out = val + 1;
+    return HYMET_OK;
+}
+
+// host copies of the sorted (bucket, y) arrays, for tests
+int hymet_mm_index_export(hymet_ctx *ctx, const hymet_mm_index *idx, uint32_t *h_hash, uint64_t *h_pos) {
+    HY_ARG(ctx && idx && h_hash && h_pos, "hymet_mm_index_export: null argument");
+    HY_HIP(hipSetDevice(ctx->device));
+    if (idx->n_pos) {
+        HY_HIP(hipMemcpyAsync(h_hash, idx->d_hash, 4 * (size_t)idx->n_pos, hipMemcpyDeviceToHost, ctx->stream));
+        HY_HIP(hipMemcpyAsync(h_pos, idx->d_pos, 8 * (size_t)idx->n_pos, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HY_HIP(hipStreamSynchronize(ctx->stream));
+    return HYMET_OK;
+}
+
+}  // extern "C"

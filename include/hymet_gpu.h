@@ -78,6 +78,26 @@ int hymet_screen_stats(hymet_ctx *ctx, const int64_t *d_ref_off, int64_t n_refs,
                        const int64_t *d_slot_of, const uint32_t *d_counts, uint32_t *d_shared,
                        uint32_t *d_median);
 
+/* --------------------------------------------------- minimizer index (minimap2 -d)
+ * Replaces `minimap2 -I2g -d reference.mmi combined_genomes.fasta` (scripts/minimap2.sh:12):
+ * default indexing parameters k=15, w=10 (no -x at build time), one handle per -I part.
+ * Sequences are given as a packed pool (hymet_pack, alphabet 2) + host start/length arrays
+ * (pool offsets); rid = position of the sequence in the arrays. */
+typedef struct hymet_mm_index hymet_mm_index;
+/* Minimizers (sketch.c mm_sketch semantics) of every sequence, copied to host arrays of
+ * capacity cap; rid_mode 0 -> rid 0 (queries), 1 -> rid = sequence index. */
+int hymet_mm_sketch(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask, const int64_t *h_starts,
+                    const int64_t *h_lens, int32_t n_seq, int w, int k, int rid_mode, uint64_t *h_x,
+                    uint64_t *h_y, int64_t cap, int64_t *n_out);
+int hymet_mm_index_build(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask, const int64_t *h_starts,
+                         const int64_t *h_lens, int32_t n_seq, int w, int k, hymet_mm_index **out);
+int hymet_mm_index_destroy(hymet_mm_index *idx);
+int hymet_mm_index_info(const hymet_mm_index *idx, int32_t *w, int32_t *k, int32_t *n_seq, int64_t *n_pos);
+/* index.c mm_idx_cal_max_occ: the occurrence threshold for a fraction f (-f 2e-4) */
+int hymet_mm_index_max_occ(hymet_ctx *ctx, const hymet_mm_index *idx, float frac, int32_t *out);
+/* sorted (bucket = minimizer hash, y) arrays, n_pos entries each (tests / persistence) */
+int hymet_mm_index_export(hymet_ctx *ctx, const hymet_mm_index *idx, uint32_t *h_hash, uint64_t *h_pos);
+
 #ifdef __cplusplus
 }
 #endif

@@ -931,3 +931,18 @@ int64_t mmo_debug_chain(const m128 *a_in, int64_t n, int max_dist, int max_dist_
     free(v); free(t);
     return n;
 }
+
+/* exported for tests: mm_set_mapq for one primary region (hit.c), given the query's
+ * sum of primary scores and rep_len */
+int mmo_mapq_one(int score, int subsc, int cnt, int n_sub, int64_t sum_sc, int rep_len, int min_chain_sc) {
+    mmo_reg_t r;
+    memset(&r, 0, sizeof(r));
+    r.score = score, r.subsc = subsc, r.cnt = cnt, r.n_sub = n_sub, r.parent = 0, r.id = 0;
+    mmo_reg_t pad;
+    memset(&pad, 0, sizeof(pad));
+    /* emulate sum_sc with a second primary holding the remainder */
+    pad.parent = 1, pad.id = 1, pad.score = (int)(sum_sc - score);
+    mmo_reg_t two[2] = {r, pad};
+    set_mapq(sum_sc - score > 0 ? 2 : 1, two, min_chain_sc, rep_len);
+    return two[0].mapq;
+}
