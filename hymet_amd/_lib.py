@@ -34,6 +34,10 @@ _SIGS = {
     "hymet_mm_index_info": (_i32, [_vp, _c.POINTER(_i32), _c.POINTER(_i32), _c.POINTER(_i32), _c.POINTER(_i64)]),
     "hymet_mm_index_max_occ": (_i32, [_vp, _vp, _c.c_float, _c.POINTER(_i32)]),
     "hymet_mm_index_export": (_i32, [_vp, _vp, _vp, _vp]),
+    "hymet_mm_map": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _c.POINTER(_vp)]),
+    "hymet_mm_result_size": (_i32, [_vp, _c.POINTER(_i64)]),
+    "hymet_mm_result_copy": (_i32, [_vp, _vp, _vp, _vp]),
+    "hymet_mm_result_destroy": (_i32, [_vp]),
 }
 
 _lib = None

@@ -1,0 +1,912 @@
+// Mapping of query contigs against one minimizer-index part with minimap2's asm10 settings
+// (replaces `minimap2 -x asm10 reference.mmi input/ *.fna`, scripts/minimap2.sh:23;
+// SURVEY.md §3.4, §8a rows A2-A4).  Stage by stage (map.c mm_map_frag):
+//   1 sketch every query (mm_sketch_kernel, rid 0)
+//   2 mm_seed_mz_flt: per-query over-represented minimizers, by a (query, x) sort + runs
+//   3 seeds: CSR lookup of every minimizer (two adjacent loads), then one thread per query
+//     replays mm_seed_select / mm_collect_matches (high-occurrence streaks, rep_len,
+//     mini_pos) -- sequential by nature but O(minimizers) and parallel over queries
+//   4 anchors: exclusive scan of seed occurrence counts, one thread per seed writes them
+//   5 sort anchors by (query, strand, target, tpos, qpos) with stable rocPRIM radix passes
+//   6 groups (query, strand, target) -> chain_groups_kernel (one wave per group) ->
+//     backtrack_groups_kernel -> chains ordered by first anchor (compact_a)
+//   7 long-join re-chain of the chained anchors with bw_long for the queries that need it
+//   8 one thread per query: mm_gen_regs, mm_set_parent, mm_select_sub, mm_est_err,
+//     mm_filter_strand_retained, mm_set_mapq
+// Canonical tie-breaks T1-T4 are those of oracle/mm_oracle.c.
+#include "mm_common.hpp"
+
+#include <algorithm>
+
+struct hymet_mm_result {
+    int n_q = 0;
+    std::vector<int64_t> reg_off;   // n_q + 1
+    std::vector<int32_t> rep_len;   // n_q
+    std::vector<hymet_mm_reg> regs;
+};
+
+namespace hymet {
+namespace mm {
+
+int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *g_start, const int32_t *order,
+                 int32_t n_work, int32_t *f, int64_t *p, int32_t *t_global, int max_dist, int max_dist_inner, int bw,
+                 int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip);
+int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, const int64_t *p, int32_t *t,
+                     const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, int min_cnt, int min_sc,
+                     int max_drop, int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first, int32_t *n_chains);
+
+namespace {
+
+__device__ __forceinline__ int upper_idx(const int64_t *off, int n, int64_t v) {  // last s with off[s] <= v
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= v) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ void fill_qid_kernel(const int64_t *off, int n_q, int64_t n, uint32_t *qid) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) qid[i] = (uint32_t)upper_idx(off, n_q, i);
+}
+
+__global__ void iota_u32_kernel(uint32_t *a, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = (uint32_t)i;
+}
+
+template <typename T>
+__global__ void gather_kernel(const T *__restrict__ src, const uint32_t *__restrict__ idx, T *__restrict__ dst, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[idx[i]];
+}
+
+// seed.c mm_seed_mz_flt: runs of equal (query, x) in the sorted order
+__global__ void mzflt_runs_kernel(const uint32_t *sq, const uint64_t *sx, const uint32_t *sidx, const int64_t *qm_off,
+                                  int64_t n, int q_occ_max, float q_occ_frac, uint8_t *drop) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    if (p > 0 && sq[p] == sq[p - 1] && sx[p] == sx[p - 1]) return;  // not a run start
+    int64_t e = p + 1;
+    while (e < n && sq[e] == sq[p] && sx[e] == sx[p]) e++;
+    const uint32_t q = sq[p];
+    const int64_t nq = qm_off[q + 1] - qm_off[q];
+    if (nq <= q_occ_max) return;  // mm_seed_mz_flt returns early for this query
+    const int32_t cnt = (int32_t)(e - p);
+    if (cnt > q_occ_max && (float)cnt > (float)nq * q_occ_frac)
+        for (int64_t j = p; j < e; j++) drop[sidx[j]] = 1;
+}
+
+__global__ void flag_keep_kernel(const uint8_t *drop, int64_t n, uint32_t *keep) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) keep[i] = drop[i] ? 0u : 1u;
+}
+
+__global__ void compact_mz_kernel(const uint64_t *x, const uint64_t *y, const uint32_t *keep, const int64_t *pos, int64_t n,
+                                  uint64_t *ox, uint64_t *oy) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && keep[i]) {
+        ox[pos[i]] = x[i];
+        oy[pos[i]] = y[i];
+    }
+}
+
+__global__ void sample_off_kernel(const int64_t *pos, const int64_t *qm_off, int n_q, int64_t total, int64_t *out) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q > n_q) return;
+    out[q] = q == n_q ? total : pos[qm_off[q]];
+}
+
+struct SeedParams {
+    const uint64_t *mx, *my;
+    const int64_t *qm_off;
+    const int64_t *qlen;
+    const uint32_t *koff;
+    int64_t n_buckets;
+    int n_q;
+    int max_occ, max_max_occ, dist;
+    uint32_t *seed_n;    // out: occurrences of every minimizer (0 = not a seed or filtered)
+    int32_t *rep_len;    // out per query
+};
+
+// one thread per query: mm_seed_collect_all + mm_seed_select + mm_collect_matches
+__global__ __launch_bounds__(64) void seed_select_kernel(SeedParams P) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= P.n_q) return;
+    const int64_t m0 = P.qm_off[q], m1 = P.qm_off[q + 1];
+    const int len = (int)P.qlen[q];
+    int n_seed = 0, n_high = 0;
+    for (int64_t i = m0; i < m1; i++) {
+        const uint64_t h = P.mx[i] >> 8;
+        uint32_t n = 0;
+        if ((int64_t)h < P.n_buckets) n = P.koff[h + 1] - P.koff[h];
+        P.seed_n[i] = n;
+        if (n) {
+            n_seed++;
+            if ((int)n > P.max_occ) n_high++;
+        }
+    }
+    // flt flags are kept in bit 31 of seed_n (n < 2^31)
+    const uint32_t FLT = 0x80000000u;
+    if (P.dist > 0 && P.max_max_occ > P.max_occ) {
+        if (n_seed > 1 && n_high > 0) {
+            int64_t last0 = -1;  // minimizer index of the last low-occurrence seed
+            int last0_j = -1;    // its seed number
+            int j = 0;           // seed number
+            int64_t st_i = -1;   // first minimizer of the current streak
+            int st_j = 0;
+            for (int64_t i = m0; i <= m1; i++) {
+                uint32_t n = 0;
+                if (i < m1) {
+                    n = P.seed_n[i];
+                    if (!n) continue;
+                }
+                const bool low = (i == m1) || (int)n <= P.max_occ;
+                if (low) {
+                    if (st_i >= 0 && j - last0_j > 1) {
+                        const int32_t ps = last0 < 0 ? 0 : (int32_t)((uint32_t)P.my[last0] >> 1);
+                        const int32_t pe = i == m1 ? len : (int32_t)((uint32_t)P.my[i] >> 1);
+                        int32_t mh = (int32_t)((double)(pe - ps) / P.dist + .499);
+                        if (mh > 128) mh = 128;
+                        const int cnt = j - st_j;
+                        uint64_t thr = 0;  // keep seeds with key <= thr (the mh smallest (n, j))
+                        bool keep_all = mh >= cnt, keep_none = mh <= 0;
+                        if (!keep_all && !keep_none) {
+                            uint64_t lo = 0, hi = ~0ull;
+                            while (lo < hi) {  // smallest T with #(key <= T) >= mh
+                                const uint64_t mid = lo + (hi - lo) / 2;
+                                int c = 0, jj = st_j;
+                                for (int64_t a = st_i; a < i; a++) {
+                                    const uint32_t na = P.seed_n[a] & ~FLT;
+                                    if (!na) continue;
+                                    const uint64_t key = (uint64_t)na << 32 | (uint32_t)jj;
+                                    c += key <= mid;
+                                    jj++;
+                                }
+                                if (c >= mh) hi = mid;
+                                else lo = mid + 1;
+                            }
+                            thr = lo;
+                        }
+                        int jj = st_j;
+                        for (int64_t a = st_i; a < i; a++) {
+                            uint32_t na = P.seed_n[a] & ~FLT;
+                            if (!na) continue;
+                            const uint64_t key = (uint64_t)na << 32 | (uint32_t)jj;
+                            bool chosen = keep_all || (!keep_none && key <= thr);
+                            bool flt = !chosen;
+                            if ((int)na > P.max_max_occ) flt = true;
+                            P.seed_n[a] = na | (flt ? FLT : 0u);
+                            jj++;
+                        }
+                    }
+                    if (i < m1) {
+                        last0 = i;
+                        last0_j = j;
+                    }
+                    st_i = -1;
+                } else if (st_i < 0) {
+                    st_i = i;
+                    st_j = j;
+                }
+                if (i < m1) j++;
+            }
+        }
+    } else {
+        for (int64_t i = m0; i < m1; i++)
+            if ((int)P.seed_n[i] > P.max_occ) P.seed_n[i] |= FLT;
+    }
+    // mm_collect_matches: rep_len over filtered seeds, then clear filtered counts
+    int rep_st = 0, rep_en = 0, rep = 0;
+    for (int64_t i = m0; i < m1; i++) {
+        const uint32_t n = P.seed_n[i];
+        if (!n) continue;
+        if (n & FLT) {
+            const int en = (int)((uint32_t)P.my[i] >> 1) + 1, st = en - (int)(P.mx[i] & 0xff);
+            if (st > rep_en) {
+                rep += rep_en - rep_st;
+                rep_st = st, rep_en = en;
+            } else rep_en = en;
+            P.seed_n[i] = 0;
+        }
+    }
+    rep += rep_en - rep_st;
+    P.rep_len[q] = rep;
+}
+
+__global__ void nz_flag_kernel(const uint32_t *v, int64_t n, uint32_t *flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = v[i] ? 1u : 0u;
+}
+
+struct AnchorParams {
+    const uint64_t *mx, *my;
+    const uint32_t *seed_n;
+    const int64_t *a_pos;     // anchor offset of every minimizer
+    const uint32_t *qid;
+    const int64_t *qlen;
+    const uint32_t *koff;
+    const uint64_t *ipos;
+    int64_t n;
+    int rb;                   // bits for rid
+    uint64_t *ax, *ay, *k1, *k2;
+    uint32_t *val;
+    // mini_pos
+    const int64_t *mp_pos;
+    uint64_t *mini_pos;
+};
+
+__global__ void write_anchors_kernel(AnchorParams P) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    const uint32_t n = P.seed_n[i];
+    if (!n) return;
+    const uint64_t mx = P.mx[i], my = P.my[i];
+    const uint32_t q_pos = (uint32_t)my, q_span = (uint32_t)(mx & 0xff);
+    P.mini_pos[P.mp_pos[i]] = (uint64_t)q_span << 32 | (q_pos >> 1);
+    const uint32_t q = P.qid[i];
+    const int32_t qlen = (int32_t)P.qlen[q];
+    const uint32_t *kp = P.koff + (mx >> 8);
+    const uint64_t *r = P.ipos + kp[0];
+    int64_t a = P.a_pos[i];
+    for (uint32_t k = 0; k < n; k++, a++) {
+        const uint64_t rk = r[k];
+        const uint32_t rpos = (uint32_t)rk >> 1;
+        const uint32_t rid = (uint32_t)(rk >> 32);
+        uint64_t x, y;
+        uint32_t rev;
+        if ((rk & 1) == (q_pos & 1)) {
+            rev = 0;
+            x = (rk & 0xffffffff00000000ULL) | rpos;
+            y = (uint64_t)q_span << 32 | (q_pos >> 1);
+        } else {
+            rev = 1;
+            x = 1ULL << 63 | (rk & 0xffffffff00000000ULL) | rpos;
+            y = (uint64_t)q_span << 32 | (uint32_t)(qlen - (int32_t)((q_pos >> 1) + 1 - q_span) - 1);
+        }
+        P.ax[a] = x;
+        P.ay[a] = y;
+        P.k1[a] = (uint64_t)q << (1 + P.rb) | (uint64_t)rev << P.rb | rid;
+        P.k2[a] = (uint64_t)rpos << 32 | (uint32_t)y;
+        P.val[a] = (uint32_t)a;
+    }
+}
+
+__global__ void group_flag_kernel(const uint64_t *k1, int64_t n, uint32_t *flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = (i == 0 || k1[i] != k1[i - 1]) ? 1u : 0u;
+}
+
+__global__ void group_start_kernel(const uint32_t *flag, const int64_t *gpos, int64_t n, int64_t *g_start, int32_t *gid) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t g = gpos[i] + flag[i] - 1;
+    gid[i] = (int32_t)g;
+    if (flag[i]) g_start[g] = i;
+}
+
+__global__ void group_size_kernel(const int64_t *g_start, int32_t G, int min_cnt, uint32_t *key, uint32_t *gidx,
+                                  uint32_t *is_work) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    const int64_t sz = g_start[g + 1] - g_start[g];
+    key[g] = ~(uint32_t)min(sz, (int64_t)0xffffffff);  // descending size
+    gidx[g] = (uint32_t)g;
+    is_work[g] = sz >= min_cnt ? 1u : 0u;
+}
+
+__global__ void zflag_kernel(const int32_t *f, int64_t n, int min_sc, uint32_t *flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = f[i] >= min_sc ? 1u : 0u;
+}
+
+__global__ void zfill_kernel(const int32_t *f, const uint32_t *flag, const int64_t *pos, const int32_t *gid, int64_t n,
+                             uint32_t *zf, uint32_t *zi, uint32_t *zg) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    const int64_t o = pos[i];
+    zf[o] = (uint32_t)f[i];
+    zi[o] = (uint32_t)i;
+    zg[o] = (uint32_t)gid[i];
+}
+
+__global__ void zoff_kernel(const uint32_t *zg_sorted, int64_t nz, int32_t G, int64_t *z_off) {
+    // z_off[g] = first position with group >= g
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p > nz) return;
+    const int64_t gp = p == 0 ? -1 : (int64_t)zg_sorted[p - 1];
+    const int64_t gc = p == nz ? (int64_t)G : (int64_t)zg_sorted[p];
+    for (int64_t g = gp + 1; g <= gc; g++) z_off[g] = p;
+}
+
+// chain list entries: (key = first anchor index) -> sorted
+__global__ void chain_list_kernel(const int64_t *g_start, const int32_t *n_chains, const int64_t *c_pos, int32_t G,
+                                  const uint64_t *chain_u, const int64_t *chain_first, const int64_t *chain_ids,
+                                  uint64_t *ckey, uint64_t *cu, int64_t *cfirst) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    const int64_t g0 = g_start[g];
+    int64_t o = c_pos[g];
+    for (int c = 0; c < n_chains[g]; c++, o++) {
+        const int64_t fo = chain_first[g0 + c];
+        ckey[o] = (uint64_t)chain_ids[fo];
+        cu[o] = chain_u[g0 + c];
+        cfirst[o] = fo;
+    }
+}
+
+__global__ void chain_cnt_kernel(const uint64_t *cu, int64_t n, uint32_t *cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) cnt[i] = (uint32_t)cu[i];
+}
+
+__global__ void chain_copy_kernel(const uint64_t *cu, const int64_t *cfirst, const int64_t *bpos, const int64_t *chain_ids,
+                                  const uint64_t *ax, const uint64_t *ay, int64_t n, uint64_t *bx, uint64_t *by) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const int32_t m = (int32_t)cu[c];
+    const int64_t f = cfirst[c], o = bpos[c];
+    for (int32_t j = 0; j < m; j++) {
+        const int64_t a = chain_ids[f + j];
+        bx[o + j] = ax[a];
+        by[o + j] = ay[a];
+    }
+}
+
+// query of each chain (from the sorted first-anchor key, via the anchor query offsets)
+__global__ void chain_query_kernel(const uint64_t *ckey, int64_t n, const int64_t *a_off, int n_q, uint32_t *cq) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < n) cq[c] = (uint32_t)upper_idx(a_off, n_q, (int64_t)ckey[c]);
+}
+
+__global__ void count_per_query_kernel(const uint32_t *cq, int64_t n, int n_q, int64_t *q_first) {
+    // q_first[q] = first chain index of query q (lower bound), q_first[n_q] = n
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p > n) return;
+    const int64_t qp = p == 0 ? -1 : (int64_t)cq[p - 1];
+    const int64_t qc = p == n ? (int64_t)n_q : (int64_t)cq[p];
+    for (int64_t q = qp + 1; q <= qc; q++) q_first[q] = p;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host helpers
+template <typename K, typename V>
+static int sort_pairs(hymet_ctx *ctx, K *&keys, K *&keys_alt, V *&vals, V *&vals_alt, int64_t n, int begin_bit, int end_bit) {
+    if (n <= 1) return HYMET_OK;
+    size_t tmp = 0;
+    HY_HIP(rocprim::radix_sort_pairs(nullptr, tmp, keys, keys_alt, vals, vals_alt, (size_t)n, begin_bit, end_bit, ctx->stream));
+    DevBuf t;
+    HY_HIP(t.alloc(tmp, ctx->stream));
+    HY_HIP(rocprim::radix_sort_pairs(t.p, tmp, keys, keys_alt, vals, vals_alt, (size_t)n, begin_bit, end_bit, ctx->stream));
+    std::swap(keys, keys_alt);
+    std::swap(vals, vals_alt);
+    return HYMET_OK;
+}
+
+static int scan_flags(hymet_ctx *ctx, const uint32_t *flag, int64_t n, DevBuf &pos, int64_t *total) {
+    HY_HIP(pos.alloc(8 * (size_t)(n + 1), ctx->stream));
+    return exclusive_scan_u32_i64(ctx, flag, pos.as<int64_t>(), n, total);
+}
+
+static int bits_for(int64_t v) {
+    int b = 0;
+    while ((1ll << b) <= v) b++;
+    return b < 1 ? 1 : b;
+}
+
+#define LAUNCH1(kern, n, ...)                                                                           \
+    do {                                                                                                \
+        if ((n) > 0) {                                                                                  \
+            hipLaunchKernelGGL(kern, dim3((unsigned)cdiv((n), 256)), dim3(256), 0, ctx->stream, __VA_ARGS__); \
+            HY_CHECK_LAUNCH(#kern);                                                                     \
+        }                                                                                               \
+    } while (0)
+
+// An anchor set sorted by (query, x, y): arrays + per-query offsets (device + host).
+struct AnchorSet {
+    DevBuf ax, ay, k1;
+    int64_t n = 0;
+    std::vector<int64_t> h_off;  // n_q + 1
+    DevBuf d_off;
+};
+
+// Chains of an anchor set: compacted anchors (chain by chain, chains ordered by first
+// anchor) + chain scores/counts + per-query chain offsets.
+struct ChainSet {
+    DevBuf bx, by, cu, cboff;  // cboff: offset of each chain's anchors in bx/by
+    int64_t n_anchor = 0, n_chain = 0;
+    std::vector<int64_t> h_qc;   // n_q + 1 chain offsets per query
+    std::vector<int64_t> h_qb;   // n_q + 1 anchor offsets per query
+    DevBuf d_qc, d_qb;
+};
+
+// sort raw anchors (x, y, k1 with k2 keys) into an AnchorSet
+static int sort_anchor_set(hymet_ctx *ctx, DevBuf &x, DevBuf &y, DevBuf &k1, DevBuf &k2, DevBuf &val, int64_t n,
+                           int key1_bits, AnchorSet &out) {
+    DevBuf k2b, valb, k1g, k1b;
+    HY_HIP(k2b.alloc(8 * (size_t)n, ctx->stream));
+    HY_HIP(valb.alloc(4 * (size_t)n, ctx->stream));
+    uint64_t *kk = k2.as<uint64_t>(), *kka = k2b.as<uint64_t>();
+    uint32_t *vv = val.as<uint32_t>(), *vva = valb.as<uint32_t>();
+    int rc = sort_pairs(ctx, kk, kka, vv, vva, n, 0, 64);
+    if (rc) return rc;
+    HY_HIP(k1g.alloc(8 * (size_t)n, ctx->stream));
+    HY_HIP(k1b.alloc(8 * (size_t)n, ctx->stream));
+    LAUNCH1(gather_kernel<uint64_t>, n, k1.as<uint64_t>(), vv, k1g.as<uint64_t>(), n);
+    uint64_t *k1p = k1g.as<uint64_t>(), *k1a = k1b.as<uint64_t>();
+    rc = sort_pairs(ctx, k1p, k1a, vv, vva, n, 0, key1_bits);
+    if (rc) return rc;
+    HY_HIP(out.ax.alloc(8 * (size_t)n, ctx->stream));
+    HY_HIP(out.ay.alloc(8 * (size_t)n, ctx->stream));
+    HY_HIP(out.k1.alloc(8 * (size_t)n, ctx->stream));
+    LAUNCH1(gather_kernel<uint64_t>, n, x.as<uint64_t>(), vv, out.ax.as<uint64_t>(), n);
+    LAUNCH1(gather_kernel<uint64_t>, n, y.as<uint64_t>(), vv, out.ay.as<uint64_t>(), n);
+    HY_HIP(hipMemcpyAsync(out.k1.p, k1p, 8 * (size_t)n, hipMemcpyDeviceToDevice, ctx->stream));
+    out.n = n;
+    return HYMET_OK;
+}
+
+// chaining + backtrack + compact_a over an anchor set
+static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, float pen_skip, int bw, AnchorSet &A,
+                     int n_q, ChainSet &C) {
+    const int64_t n = A.n;
+    C.h_qc.assign(n_q + 1, 0);
+    C.h_qb.assign(n_q + 1, 0);
+    if (n == 0) {
+        HY_HIP(C.d_qc.alloc(8 * (size_t)(n_q + 1), ctx->stream));
+        HY_HIP(C.d_qb.alloc(8 * (size_t)(n_q + 1), ctx->stream));
+        HY_HIP(hipMemsetAsync(C.d_qc.p, 0, 8 * (size_t)(n_q + 1), ctx->stream));
+        HY_HIP(hipMemsetAsync(C.d_qb.p, 0, 8 * (size_t)(n_q + 1), ctx->stream));
+        return HYMET_OK;
+    }
+    // groups
+    DevBuf flag, gpos, gid;
+    HY_HIP(flag.alloc(4 * (size_t)n, ctx->stream));
+    LAUNCH1(group_flag_kernel, n, A.k1.as<uint64_t>(), n, flag.as<uint32_t>());
+    int64_t G = 0;
+    int rc = scan_flags(ctx, flag.as<uint32_t>(), n, gpos, &G);
+    if (rc) return rc;
+    DevBuf g_start;
+    HY_HIP(g_start.alloc(8 * (size_t)(G + 1), ctx->stream));
+    HY_HIP(gid.alloc(4 * (size_t)n, ctx->stream));
+    LAUNCH1(group_start_kernel, n, flag.as<uint32_t>(), gpos.as<int64_t>(), n, g_start.as<int64_t>(), gid.as<int32_t>());
+    HY_HIP(hipMemcpyAsync(g_start.as<int64_t>() + G, &n, 8, hipMemcpyHostToDevice, ctx->stream));
+    // work list: groups with >= min_cnt anchors, biggest first
+    DevBuf skey, sidx, swork, skey2, sidx2;
+    HY_HIP(skey.alloc(4 * (size_t)G, ctx->stream));
+    HY_HIP(sidx.alloc(4 * (size_t)G, ctx->stream));
+    HY_HIP(swork.alloc(4 * (size_t)G, ctx->stream));
+    HY_HIP(skey2.alloc(4 * (size_t)G, ctx->stream));
+    HY_HIP(sidx2.alloc(4 * (size_t)G, ctx->stream));
+    LAUNCH1(group_size_kernel, G, g_start.as<int64_t>(), (int32_t)G, opt->min_cnt, skey.as<uint32_t>(), sidx.as<uint32_t>(),
+            swork.as<uint32_t>());
+    // drop non-work groups: key of those = 0xffffffff (sorted last), count them on the host
+    {
+        DevBuf wpos;
+        int64_t n_work = 0;
+        rc = scan_flags(ctx, swork.as<uint32_t>(), G, wpos, &n_work);
+        if (rc) return rc;
+        uint32_t *kp = skey.as<uint32_t>(), *ka = skey2.as<uint32_t>(), *vp = sidx.as<uint32_t>(), *va = sidx2.as<uint32_t>();
+        rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 32);
+        if (rc) return rc;
+        DevBuf f, p, t;
+        HY_HIP(f.alloc(4 * (size_t)n, ctx->stream));
+        HY_HIP(p.alloc(8 * (size_t)n, ctx->stream));
+        HY_HIP(t.alloc(4 * (size_t)n, ctx->stream));
+        HY_HIP(hipMemsetAsync(f.p, 0, 4 * (size_t)n, ctx->stream));
+        HY_HIP(hipMemsetAsync(p.p, 0xFF, 8 * (size_t)n, ctx->stream));
+        HY_HIP(hipMemsetAsync(t.p, 0xFF, 4 * (size_t)n, ctx->stream));
+        rc = launch_chain(ctx, A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), g_start.as<int64_t>(), (const int32_t *)vp,
+                          (int32_t)n_work, f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(), opt->max_gap,
+                          opt->rmq_inner_dist, bw, opt->max_chain_skip, opt->rmq_size_cap, pen_gap, pen_skip);
+        if (rc) return rc;
+        // z = anchors with f >= min_sc ordered by (group, f, idx)
+        DevBuf zflag, zpos;
+        HY_HIP(zflag.alloc(4 * (size_t)n, ctx->stream));
+        LAUNCH1(zflag_kernel, n, f.as<int32_t>(), n, opt->min_chain_score, zflag.as<uint32_t>());
+        int64_t nz = 0;
+        rc = scan_flags(ctx, zflag.as<uint32_t>(), n, zpos, &nz);
+        if (rc) return rc;
+        DevBuf zf, zi, zg, zf2, zi2, zg2, zz;
+        const size_t zb = 4 * (size_t)(nz + 1);
+        HY_HIP(zf.alloc(zb, ctx->stream));
+        HY_HIP(zi.alloc(zb, ctx->stream));
+        HY_HIP(zg.alloc(zb, ctx->stream));
+        HY_HIP(zf2.alloc(zb, ctx->stream));
+        HY_HIP(zi2.alloc(zb, ctx->stream));
+        HY_HIP(zg2.alloc(zb, ctx->stream));
+        LAUNCH1(zfill_kernel, n, f.as<int32_t>(), zflag.as<uint32_t>(), zpos.as<int64_t>(), gid.as<int32_t>(), n,
+                zf.as<uint32_t>(), zi.as<uint32_t>(), zg.as<uint32_t>());
+        uint32_t *kf = zf.as<uint32_t>(), *kfa = zf2.as<uint32_t>(), *vi = zi.as<uint32_t>(), *via = zi2.as<uint32_t>();
+        rc = sort_pairs(ctx, kf, kfa, vi, via, nz, 0, 32);
+        if (rc) return rc;
+        DevBuf zgg;
+        HY_HIP(zgg.alloc(zb, ctx->stream));
+        LAUNCH1(gather_kernel<uint32_t>, nz, gid.as<uint32_t>(), vi, zgg.as<uint32_t>(), nz);
+        uint32_t *kg = zgg.as<uint32_t>(), *kga = zg2.as<uint32_t>();
+        rc = sort_pairs(ctx, kg, kga, vi, via, nz, 0, bits_for(G));
+        if (rc) return rc;
+        DevBuf z_off;
+        HY_HIP(z_off.alloc(8 * (size_t)(G + 1), ctx->stream));
+        if (nz > 0) {
+            hipLaunchKernelGGL(zoff_kernel, dim3((unsigned)cdiv(nz + 1, 256)), dim3(256), 0, ctx->stream, kg, nz, (int32_t)G,
+                               z_off.as<int64_t>());
+            HY_CHECK_LAUNCH("zoff_kernel");
+        } else {
+            HY_HIP(hipMemsetAsync(z_off.p, 0, 8 * (size_t)(G + 1), ctx->stream));
+        }
+        DevBuf chain_ids, chain_u, chain_first, n_chains;
+        HY_HIP(chain_ids.alloc(8 * (size_t)n, ctx->stream));
+        HY_HIP(chain_u.alloc(8 * (size_t)n, ctx->stream));
+        HY_HIP(chain_first.alloc(8 * (size_t)n, ctx->stream));
+        HY_HIP(n_chains.alloc(4 * (size_t)G, ctx->stream));
+        rc = launch_backtrack(ctx, g_start.as<int64_t>(), f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(),
+                              z_off.as<int64_t>(), (const int32_t *)vi, (int32_t)G, opt->min_cnt, opt->min_chain_score, bw,
+                              chain_ids.as<int64_t>(), chain_u.as<uint64_t>(), chain_first.as<int64_t>(),
+                              n_chains.as<int32_t>());
+        if (rc) return rc;
+        // chain list sorted by first anchor index (compact_a order)
+        DevBuf cpos;
+        int64_t NC = 0;
+        rc = scan_flags(ctx, (const uint32_t *)n_chains.p, G, cpos, &NC);
+        if (rc) return rc;
+        C.n_chain = NC;
+        DevBuf ckey, cfirst, ckey2, cu2, cfirst2;
+        HY_HIP(ckey.alloc(8 * (size_t)(NC + 1), ctx->stream));
+        HY_HIP(C.cu.alloc(8 * (size_t)(NC + 1), ctx->stream));
+        HY_HIP(cfirst.alloc(8 * (size_t)(NC + 1), ctx->stream));
+        LAUNCH1(chain_list_kernel, G, g_start.as<int64_t>(), n_chains.as<int32_t>(), cpos.as<int64_t>(), (int32_t)G,
+                chain_u.as<uint64_t>(), chain_first.as<int64_t>(), chain_ids.as<int64_t>(), ckey.as<uint64_t>(),
+                C.cu.as<uint64_t>(), cfirst.as<int64_t>());
+        // sort chains by first anchor: pairs (key, perm) then gather
+        DevBuf perm, perm2, ckeyb;
+        HY_HIP(perm.alloc(4 * (size_t)(NC + 1), ctx->stream));
+        HY_HIP(perm2.alloc(4 * (size_t)(NC + 1), ctx->stream));
+        HY_HIP(ckeyb.alloc(8 * (size_t)(NC + 1), ctx->stream));
+        LAUNCH1(iota_u32_kernel, NC, perm.as<uint32_t>(), NC);
+        uint64_t *ck = ckey.as<uint64_t>(), *cka = ckeyb.as<uint64_t>();
+        uint32_t *pp = perm.as<uint32_t>(), *ppa = perm2.as<uint32_t>();
+        rc = sort_pairs(ctx, ck, cka, pp, ppa, NC, 0, bits_for(n));
+        if (rc) return rc;
+        DevBuf cu_s, cf_s;
+        HY_HIP(cu_s.alloc(8 * (size_t)(NC + 1), ctx->stream));
+        HY_HIP(cf_s.alloc(8 * (size_t)(NC + 1), ctx->stream));
+        LAUNCH1(gather_kernel<uint64_t>, NC, C.cu.as<uint64_t>(), pp, cu_s.as<uint64_t>(), NC);
+        LAUNCH1(gather_kernel<int64_t>, NC, cfirst.as<int64_t>(), pp, cf_s.as<int64_t>(), NC);
+        std::swap(C.cu.p, cu_s.p);
+        // anchors of every chain, compacted in chain order
+        DevBuf ccnt;
+        HY_HIP(ccnt.alloc(4 * (size_t)(NC + 1), ctx->stream));
+        LAUNCH1(chain_cnt_kernel, NC, C.cu.as<uint64_t>(), NC, ccnt.as<uint32_t>());
+        int64_t NB = 0;
+        rc = scan_flags(ctx, ccnt.as<uint32_t>(), NC, C.cboff, &NB);
+        if (rc) return rc;
+        C.n_anchor = NB;
+        HY_HIP(C.bx.alloc(8 * (size_t)(NB + 1), ctx->stream));
+        HY_HIP(C.by.alloc(8 * (size_t)(NB + 1), ctx->stream));
+        LAUNCH1(chain_copy_kernel, NC, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), C.cboff.as<int64_t>(),
+                chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, C.bx.as<uint64_t>(),
+                C.by.as<uint64_t>());
+        // per-query chain offsets
+        DevBuf cq;
+        HY_HIP(cq.alloc(4 * (size_t)(NC + 1), ctx->stream));
+        LAUNCH1(chain_query_kernel, NC, ck, NC, A.d_off.as<int64_t>(), n_q, cq.as<uint32_t>());
+        HY_HIP(C.d_qc.alloc(8 * (size_t)(n_q + 1), ctx->stream));
+        hipLaunchKernelGGL(count_per_query_kernel, dim3((unsigned)cdiv(NC + 1, 256)), dim3(256), 0, ctx->stream,
+                           cq.as<uint32_t>(), NC, n_q, C.d_qc.as<int64_t>());
+        HY_CHECK_LAUNCH("count_per_query_kernel");
+        HY_HIP(hipMemcpyAsync(C.h_qc.data(), C.d_qc.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, ctx->stream));
+        std::vector<int64_t> cbo(NC + 1);
+        if (NC) HY_HIP(hipMemcpyAsync(cbo.data(), C.cboff.p, 8 * (size_t)NC, hipMemcpyDeviceToHost, ctx->stream));
+        HY_HIP(hipStreamSynchronize(ctx->stream));
+        cbo[NC] = NB;
+        for (int q = 0; q <= n_q; q++) C.h_qb[q] = cbo[C.h_qc[q]];
+        HY_HIP(C.d_qb.alloc(8 * (size_t)(n_q + 1), ctx->stream));
+        HY_HIP(hipMemcpyAsync(C.d_qb.p, C.h_qb.data(), 8 * (size_t)(n_q + 1), hipMemcpyHostToDevice, ctx->stream));
+        HY_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return HYMET_OK;
+}
+
+}  // namespace mm
+}  // namespace hymet
+
+namespace hymet {
+namespace mm {
+int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const uint64_t *cu, const int64_t *cboff,
+                   const int64_t *qc, const int64_t *qb, const uint64_t *mini_pos, const int64_t *mp_off, const int64_t *qlen,
+                   const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
+                   int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs);
+
+namespace {
+__global__ void rechain_flag_kernel(const uint64_t *by, const uint64_t *cu, const int64_t *qc, const int64_t *qb,
+                                    const int64_t *qlen, int n_q, int rescue_size, float rescue_ratio, uint32_t *flag) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n_q) return;
+    const int64_t c0 = qc[q], nc = qc[q + 1] - c0;
+    uint32_t f = 0;
+    if (nc > 1) {  // map.c: re-chain / long-join for long sequences
+        const int64_t b0 = qb[q];
+        const int32_t st = (int32_t)by[b0], en = (int32_t)by[b0 + (int32_t)cu[c0] - 1];
+        const int32_t ql = (int32_t)qlen[q];
+        if (ql - (en - st) > rescue_size || (float)(en - st) > __fmul_rn((float)ql, rescue_ratio)) f = 1;
+    }
+    flag[q] = f;
+}
+
+// re-chain input: the chained anchors of flagged queries (query-major), with sort keys
+__global__ void rechain_gather_kernel(const uint64_t *bx, const uint64_t *by, const int64_t *qb, const uint32_t *qflag,
+                                      const int64_t *new_off, int n_q, int rb, uint64_t *x, uint64_t *y, uint64_t *k1,
+                                      uint64_t *k2, uint32_t *val) {
+    const int q = blockIdx.x;
+    if (q >= n_q || !qflag[q]) return;
+    const int64_t b0 = qb[q], b1 = qb[q + 1], o = new_off[q];
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
+        const int64_t a = o + (i - b0);
+        const uint64_t ax = bx[i], ay = by[i];
+        x[a] = ax;
+        y[a] = ay;
+        k1[a] = (uint64_t)q << (1 + rb) | (ax >> 63) << rb | (ax << 1 >> 33);
+        k2[a] = (uint64_t)(uint32_t)ax << 32 | (uint32_t)ay;
+        val[a] = (uint32_t)a;
+    }
+}
+
+__global__ void qlen_sizes_kernel(const int64_t *off, int n_q, const uint32_t *flag, uint32_t *sz) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n_q) sz[q] = flag[q] ? (uint32_t)(off[q + 1] - off[q]) : 0u;
+}
+}  // namespace
+}  // namespace mm
+}  // namespace hymet
+
+using namespace hymet;
+using namespace hymet::mm;
+
+extern "C" {
+
+int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *opt, const uint32_t *d_2b,
+                 const uint32_t *d_mask, const int64_t *h_starts, const int64_t *h_lens, const uint32_t *h_name_hash,
+                 int32_t n_q, hymet_mm_result **out) {
+    HY_ARG(ctx && idx && opt && d_2b && d_mask && out, "hymet_mm_map: null argument");
+    HY_ARG(n_q >= 0, "hymet_mm_map: n_q < 0");
+    HY_ARG(opt->mid_occ > 0, "hymet_mm_map: opt->mid_occ must be resolved (hymet_mm_index_max_occ + clamps)");
+    HY_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    hymet_mm_result *res = new hymet_mm_result();
+    res->n_q = n_q;
+    res->reg_off.assign(n_q + 1, 0);
+    res->rep_len.assign(n_q, 0);
+    *out = res;
+    if (n_q == 0) return HYMET_OK;
+    const int k = idx->k, w = idx->w;
+    const float pen_gap = (float)(opt->chain_gap_scale * 0.01 * k);
+    const float pen_skip = (float)(opt->chain_skip_scale * 0.01 * k);
+    int rc;
+    // ---------------------------------------------------------------- 1 sketch
+    DevBuf mx, my, qm_off;
+    int64_t M = 0;
+    rc = sketch_sequences(ctx, d_2b, d_mask, h_starts, h_lens, n_q, w, k, 0, mx, my, &M, &qm_off);
+    if (rc) return rc;
+    DevBuf d_qlen, d_hash;
+    HY_HIP(d_qlen.alloc(8 * (size_t)n_q, st));
+    HY_HIP(d_hash.alloc(4 * (size_t)n_q, st));
+    HY_HIP(hipMemcpyAsync(d_qlen.p, h_lens, 8 * (size_t)n_q, hipMemcpyHostToDevice, st));
+    HY_HIP(hipMemcpyAsync(d_hash.p, h_name_hash, 4 * (size_t)n_q, hipMemcpyHostToDevice, st));
+    std::vector<int64_t> h_qm(n_q + 1);
+    HY_HIP(hipMemcpyAsync(h_qm.data(), qm_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, st));
+    HY_HIP(hipStreamSynchronize(st));
+    // ------------------------------------------------------- 2 mm_seed_mz_flt
+    bool need_flt = false;
+    if (opt->q_occ_frac > 0.0f)
+        for (int q = 0; q < n_q; q++)
+            if (h_qm[q + 1] - h_qm[q] > opt->mid_occ) need_flt = true;
+    if (need_flt && M > 0) {
+        DevBuf qid, sx, sx2, sidx, sidx2, sq, sq2, drop, keep, kpos, nx, ny;
+        HY_HIP(qid.alloc(4 * (size_t)M, st));
+        LAUNCH1(fill_qid_kernel, M, qm_off.as<int64_t>(), n_q, M, qid.as<uint32_t>());
+        HY_HIP(sx.alloc(8 * (size_t)M, st));
+        HY_HIP(sx2.alloc(8 * (size_t)M, st));
+        HY_HIP(sidx.alloc(4 * (size_t)M, st));
+        HY_HIP(sidx2.alloc(4 * (size_t)M, st));
+        HY_HIP(hipMemcpyAsync(sx.p, mx.p, 8 * (size_t)M, hipMemcpyDeviceToDevice, st));
+        LAUNCH1(iota_u32_kernel, M, sidx.as<uint32_t>(), M);
+        uint64_t *kx = sx.as<uint64_t>(), *kxa = sx2.as<uint64_t>();
+        uint32_t *vi = sidx.as<uint32_t>(), *via = sidx2.as<uint32_t>();
+        rc = sort_pairs(ctx, kx, kxa, vi, via, M, 0, 2 * k + 8);
+        if (rc) return rc;
+        HY_HIP(sq.alloc(4 * (size_t)M, st));
+        HY_HIP(sq2.alloc(4 * (size_t)M, st));
+        LAUNCH1(gather_kernel<uint32_t>, M, qid.as<uint32_t>(), vi, sq.as<uint32_t>(), M);
+        uint32_t *kq = sq.as<uint32_t>(), *kqa = sq2.as<uint32_t>();
+        rc = sort_pairs(ctx, kq, kqa, vi, via, M, 0, bits_for(n_q));
+        if (rc) return rc;
+        LAUNCH1(gather_kernel<uint64_t>, M, mx.as<uint64_t>(), vi, kxa, M);  // x in (q, x) order
+        HY_HIP(drop.alloc((size_t)M, st));
+        HY_HIP(hipMemsetAsync(drop.p, 0, (size_t)M, st));
+        LAUNCH1(mzflt_runs_kernel, M, kq, kxa, vi, qm_off.as<int64_t>(), M, opt->mid_occ, opt->q_occ_frac, drop.as<uint8_t>());
+        HY_HIP(keep.alloc(4 * (size_t)M, st));
+        LAUNCH1(flag_keep_kernel, M, drop.as<uint8_t>(), M, keep.as<uint32_t>());
+        int64_t M2 = 0;
+        rc = scan_flags(ctx, keep.as<uint32_t>(), M, kpos, &M2);
+        if (rc) return rc;
+        HY_HIP(nx.alloc(8 * (size_t)(M2 + 1), st));
+        HY_HIP(ny.alloc(8 * (size_t)(M2 + 1), st));
+        LAUNCH1(compact_mz_kernel, M, mx.as<uint64_t>(), my.as<uint64_t>(), keep.as<uint32_t>(), kpos.as<int64_t>(), M,
+                nx.as<uint64_t>(), ny.as<uint64_t>());
+        HY_HIP(hipMemcpyAsync(kpos.as<int64_t>() + M, &M2, 8, hipMemcpyHostToDevice, st));
+        DevBuf nqm;
+        HY_HIP(nqm.alloc(8 * (size_t)(n_q + 1), st));
+        hipLaunchKernelGGL(sample_off_kernel, dim3((unsigned)cdiv(n_q + 1, 256)), dim3(256), 0, st, kpos.as<int64_t>(),
+                           qm_off.as<int64_t>(), n_q, M2, nqm.as<int64_t>());
+        HY_CHECK_LAUNCH("sample_off_kernel");
+        std::swap(mx.p, nx.p);
+        std::swap(my.p, ny.p);
+        std::swap(qm_off.p, nqm.p);
+        M = M2;
+        HY_HIP(hipMemcpyAsync(h_qm.data(), qm_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, st));
+        HY_HIP(hipStreamSynchronize(st));
+    }
+    // ------------------------------------------------------------- 3 seeds
+    DevBuf seed_n, rep_len;
+    HY_HIP(seed_n.alloc(4 * (size_t)(M + 1), st));
+    HY_HIP(rep_len.alloc(4 * (size_t)n_q, st));
+    {
+        SeedParams P{mx.as<uint64_t>(), my.as<uint64_t>(), qm_off.as<int64_t>(), d_qlen.as<int64_t>(), idx->d_koff,
+                     idx->n_buckets, n_q, opt->mid_occ, opt->max_max_occ, opt->occ_dist, seed_n.as<uint32_t>(),
+                     rep_len.as<int32_t>()};
+        hipLaunchKernelGGL(seed_select_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P);
+        HY_CHECK_LAUNCH("seed_select_kernel");
+    }
+    // ------------------------------------------------------------ 4 anchors
+    DevBuf a_pos, mflag, mp_pos, qid, mini_pos, mp_off;
+    int64_t A = 0, NM = 0;
+    rc = scan_flags(ctx, seed_n.as<uint32_t>(), M, a_pos, &A);
+    if (rc) return rc;
+    HY_HIP(mflag.alloc(4 * (size_t)(M + 1), st));
+    LAUNCH1(nz_flag_kernel, M, seed_n.as<uint32_t>(), M, mflag.as<uint32_t>());
+    rc = scan_flags(ctx, mflag.as<uint32_t>(), M, mp_pos, &NM);
+    if (rc) return rc;
+    HY_HIP(hipMemcpyAsync(a_pos.as<int64_t>() + M, &A, 8, hipMemcpyHostToDevice, st));
+    HY_HIP(hipMemcpyAsync(mp_pos.as<int64_t>() + M, &NM, 8, hipMemcpyHostToDevice, st));
+    HY_HIP(qid.alloc(4 * (size_t)(M + 1), st));
+    LAUNCH1(fill_qid_kernel, M, qm_off.as<int64_t>(), n_q, M, qid.as<uint32_t>());
+    HY_HIP(mini_pos.alloc(8 * (size_t)(NM + 1), st));
+    HY_HIP(mp_off.alloc(8 * (size_t)(n_q + 1), st));
+    hipLaunchKernelGGL(sample_off_kernel, dim3((unsigned)cdiv(n_q + 1, 256)), dim3(256), 0, st, mp_pos.as<int64_t>(),
+                       qm_off.as<int64_t>(), n_q, NM, mp_off.as<int64_t>());
+    HY_CHECK_LAUNCH("sample_off_kernel");
+    AnchorSet S1;
+    HY_HIP(S1.d_off.alloc(8 * (size_t)(n_q + 1), st));
+    hipLaunchKernelGGL(sample_off_kernel, dim3((unsigned)cdiv(n_q + 1, 256)), dim3(256), 0, st, a_pos.as<int64_t>(),
+                       qm_off.as<int64_t>(), n_q, A, S1.d_off.as<int64_t>());
+    HY_CHECK_LAUNCH("sample_off_kernel");
+    const int rb = bits_for(idx->n_seq);
+    const int key1_bits = bits_for(n_q) + 1 + rb;
+    HY_ARG(key1_bits <= 64, "hymet_mm_map: too many queries x targets for the sort key");
+    {
+        DevBuf x, y, k1, k2, val;
+        HY_HIP(x.alloc(8 * (size_t)(A + 1), st));
+        HY_HIP(y.alloc(8 * (size_t)(A + 1), st));
+        HY_HIP(k1.alloc(8 * (size_t)(A + 1), st));
+        HY_HIP(k2.alloc(8 * (size_t)(A + 1), st));
+        HY_HIP(val.alloc(4 * (size_t)(A + 1), st));
+        AnchorParams P{mx.as<uint64_t>(), my.as<uint64_t>(), seed_n.as<uint32_t>(), a_pos.as<int64_t>(), qid.as<uint32_t>(),
+                       d_qlen.as<int64_t>(), idx->d_koff, idx->d_pos, M, rb, x.as<uint64_t>(), y.as<uint64_t>(),
+                       k1.as<uint64_t>(), k2.as<uint64_t>(), val.as<uint32_t>(), mp_pos.as<int64_t>(), mini_pos.as<uint64_t>()};
+        LAUNCH1(write_anchors_kernel, M, P);
+        // ------------------------------------------------------- 5 sort
+        rc = sort_anchor_set(ctx, x, y, k1, k2, val, A, key1_bits, S1);
+        if (rc) return rc;
+    }
+    // ------------------------------------------------ 6 chain (+ 7 long join)
+    ChainSet C1;
+    rc = chain_set(ctx, opt, pen_gap, pen_skip, opt->bw, S1, n_q, C1);
+    if (rc) return rc;
+    ChainSet *CF = &C1;
+    ChainSet C2;
+    std::vector<uint32_t> h_flag(n_q, 0);
+    if (opt->bw_long > opt->bw && C1.n_chain > 0) {
+        DevBuf flag;
+        HY_HIP(flag.alloc(4 * (size_t)n_q, st));
+        hipLaunchKernelGGL(rechain_flag_kernel, dim3((unsigned)cdiv(n_q, 256)), dim3(256), 0, st, C1.by.as<uint64_t>(),
+                           C1.cu.as<uint64_t>(), C1.d_qc.as<int64_t>(), C1.d_qb.as<int64_t>(), d_qlen.as<int64_t>(), n_q,
+                           opt->rmq_rescue_size, opt->rmq_rescue_ratio, flag.as<uint32_t>());
+        HY_CHECK_LAUNCH("rechain_flag_kernel");
+        HY_HIP(hipMemcpyAsync(h_flag.data(), flag.p, 4 * (size_t)n_q, hipMemcpyDeviceToHost, st));
+        HY_HIP(hipStreamSynchronize(st));
+        bool any = false;
+        for (int q = 0; q < n_q; q++) any |= h_flag[q] != 0;
+        if (any) {
+            // anchors of flagged queries only: new per-query offsets
+            AnchorSet S2;
+            S2.h_off.assign(n_q + 1, 0);
+            for (int q = 0; q < n_q; q++) S2.h_off[q + 1] = S2.h_off[q] + (h_flag[q] ? C1.h_qb[q + 1] - C1.h_qb[q] : 0);
+            const int64_t A2 = S2.h_off[n_q];
+            HY_HIP(S2.d_off.alloc(8 * (size_t)(n_q + 1), st));
+            HY_HIP(hipMemcpyAsync(S2.d_off.p, S2.h_off.data(), 8 * (size_t)(n_q + 1), hipMemcpyHostToDevice, st));
+            DevBuf x, y, k1, k2, val;
+            HY_HIP(x.alloc(8 * (size_t)(A2 + 1), st));
+            HY_HIP(y.alloc(8 * (size_t)(A2 + 1), st));
+            HY_HIP(k1.alloc(8 * (size_t)(A2 + 1), st));
+            HY_HIP(k2.alloc(8 * (size_t)(A2 + 1), st));
+            HY_HIP(val.alloc(4 * (size_t)(A2 + 1), st));
+            hipLaunchKernelGGL(rechain_gather_kernel, dim3((unsigned)n_q), dim3(256), 0, st, C1.bx.as<uint64_t>(),
+                               C1.by.as<uint64_t>(), C1.d_qb.as<int64_t>(), flag.as<uint32_t>(), S2.d_off.as<int64_t>(), n_q,
+                               rb, x.as<uint64_t>(), y.as<uint64_t>(), k1.as<uint64_t>(), k2.as<uint64_t>(), val.as<uint32_t>());
+            HY_CHECK_LAUNCH("rechain_gather_kernel");
+            rc = sort_anchor_set(ctx, x, y, k1, k2, val, A2, key1_bits, S2);
+            if (rc) return rc;
+            rc = chain_set(ctx, opt, pen_gap, pen_skip, opt->bw_long, S2, n_q, C2);
+            if (rc) return rc;
+            // merge: flagged queries take C2's chains, the others keep C1's
+            CF = nullptr;
+        }
+    }
+    // -------------------------------------------------------------- 8 regions
+    auto run_regions = [&](ChainSet &C, std::vector<hymet_mm_reg> &regs, std::vector<int32_t> &nreg) -> int {
+        const int64_t NC = C.n_chain;
+        DevBuf z, rg, wv, cov, tmp, nr;
+        HY_HIP(z.alloc(16 * (size_t)(NC + 1), st));
+        HY_HIP(rg.alloc(sizeof(hymet_mm_reg) * (size_t)(NC + 1), st));
+        HY_HIP(wv.alloc(4 * (size_t)(NC + 1), st));
+        HY_HIP(cov.alloc(8 * (size_t)(NC + 1), st));
+        HY_HIP(tmp.alloc(4 * (size_t)(NC + 1), st));
+        HY_HIP(nr.alloc(4 * (size_t)n_q, st));
+        int r2 = launch_regions(ctx, C.bx.as<uint64_t>(), C.by.as<uint64_t>(), C.cu.as<uint64_t>(), C.cboff.as<int64_t>(),
+                                C.d_qc.as<int64_t>(), C.d_qb.as<int64_t>(), mini_pos.as<uint64_t>(), mp_off.as<int64_t>(),
+                                d_qlen.as<int64_t>(), d_hash.as<uint32_t>(), rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
+                                z.p, rg.as<hymet_mm_reg>(), wv.as<int32_t>(), cov.as<uint64_t>(), tmp.as<int32_t>(),
+                                nr.as<int32_t>());
+        if (r2) return r2;
+        regs.resize(NC);
+        nreg.resize(n_q);
+        if (NC) HY_HIP(hipMemcpyAsync(regs.data(), rg.p, sizeof(hymet_mm_reg) * (size_t)NC, hipMemcpyDeviceToHost, st));
+        HY_HIP(hipMemcpyAsync(nreg.data(), nr.p, 4 * (size_t)n_q, hipMemcpyDeviceToHost, st));
+        HY_HIP(hipStreamSynchronize(st));
+        return HYMET_OK;
+    };
+    std::vector<hymet_mm_reg> r1, r2v;
+    std::vector<int32_t> n1, n2;
+    rc = run_regions(C1, r1, n1);
+    if (rc) return rc;
+    if (!CF) {
+        rc = run_regions(C2, r2v, n2);
+        if (rc) return rc;
+    }
+    HY_HIP(hipMemcpyAsync(res->rep_len.data(), rep_len.p, 4 * (size_t)n_q, hipMemcpyDeviceToHost, st));
+    HY_HIP(hipStreamSynchronize(st));
+    for (int q = 0; q < n_q; q++) {
+        const bool use2 = !CF && h_flag[q];
+        const int nr = use2 ? n2[q] : n1[q];
+        const int64_t c0 = use2 ? C2.h_qc[q] : C1.h_qc[q];
+        const std::vector<hymet_mm_reg> &src = use2 ? r2v : r1;
+        for (int i = 0; i < nr; i++) res->regs.push_back(src[c0 + i]);
+        res->reg_off[q + 1] = (int64_t)res->regs.size();
+    }
+    return HYMET_OK;
+}
+
+int hymet_mm_result_size(const hymet_mm_result *res, int64_t *n_regs) {
+    HY_ARG(res && n_regs, "hymet_mm_result_size: null argument");
+    *n_regs = (int64_t)res->regs.size();
+    return HYMET_OK;
+}
+
+int hymet_mm_result_copy(const hymet_mm_result *res, int64_t *h_off, int32_t *h_rep_len, hymet_mm_reg *h_regs) {
+    HY_ARG(res, "hymet_mm_result_copy: null result");
+    if (h_off) memcpy(h_off, res->reg_off.data(), 8 * (size_t)(res->n_q + 1));
+    if (h_rep_len && res->n_q) memcpy(h_rep_len, res->rep_len.data(), 4 * (size_t)res->n_q);
+    if (h_regs && !res->regs.empty()) memcpy(h_regs, res->regs.data(), sizeof(hymet_mm_reg) * res->regs.size());
+    return HYMET_OK;
+}
+
+int hymet_mm_result_destroy(hymet_mm_result *res) {
+    delete res;
+    return HYMET_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,326 @@
+// Per-query region selection (minimap2 hit.c / map.c after chaining):
+// mm_gen_regs (score + hash order), mm_reg_set_coor / mm_cal_fuzzy_len, mm_set_parent,
+// mm_select_sub (+ mm_sync_regs), mm_est_err, mm_filter_strand_retained, mm_set_mapq.
+// One thread per query: a query has few chains (tens) and every step is an O(n^2)-at-most
+// scan over them; the queries are independent, so the launch is wide.  Scratch lives in
+// global memory at the query's chain range.  Float/double arithmetic is written in the
+// order of hit.c (-ffp-contract=off).
+#include "mm_common.hpp"
+
+namespace hymet {
+namespace mm {
+namespace {
+
+__device__ __forceinline__ uint32_t wang32(uint32_t key) {
+    key += ~(key << 15);
+    key ^= (key >> 10);
+    key += (key << 3);
+    key ^= (key >> 6);
+    key += ~(key << 11);
+    key ^= (key >> 16);
+    return key;
+}
+
+struct U128 {
+    uint64_t x, y;
+};
+__device__ __forceinline__ bool lt128(const U128 &a, const U128 &b) { return a.x < b.x || (a.x == b.x && a.y < b.y); }
+
+template <typename T, typename Less>
+__device__ void heap_sort(T *a, int64_t n, Less less) {
+    auto sift = [&](int64_t i, int64_t m) {
+        for (;;) {
+            int64_t l = 2 * i + 1, r = l + 1, b = i;
+            if (l < m && less(a[b], a[l])) b = l;
+            if (r < m && less(a[b], a[r])) b = r;
+            if (b == i) return;
+            T t = a[b];
+            a[b] = a[i];
+            a[i] = t;
+            i = b;
+        }
+    };
+    for (int64_t i = n / 2 - 1; i >= 0; --i) sift(i, n);
+    for (int64_t e = n - 1; e > 0; --e) {
+        T t = a[0];
+        a[0] = a[e];
+        a[e] = t;
+        sift(0, e);
+    }
+}
+
+struct RegParams {
+    const uint64_t *bx, *by;       // chained anchors, chain by chain
+    const uint64_t *cu;            // score<<32 | count per chain
+    const int64_t *cboff;          // chain -> offset in bx/by
+    const int64_t *qc;             // n_q + 1 chain offsets
+    const int64_t *qb;             // n_q + 1 anchor offsets
+    const uint64_t *mini_pos;
+    const int64_t *mp_off;         // n_q + 1
+    const int64_t *qlen;
+    const uint32_t *name_hash;
+    const int32_t *rep_len;
+    const int64_t *ref_len;
+    int n_q;
+    int seed, k;
+    float mask_level, pri_ratio;
+    int mask_len, best_n, max_gap, min_chain_score;
+    U128 *z;
+    hymet_mm_reg *regs;
+    int32_t *w;
+    uint64_t *cov;
+    int32_t *tmp;
+    int32_t *n_regs;
+};
+
+__device__ void set_coor(hymet_mm_reg *r, int32_t qlen, const uint64_t *ax, const uint64_t *ay) {
+    const int32_t k = r->as, q_span = (int32_t)(ay[k] >> 32 & 0xff);
+    r->rev = (int32_t)(ax[k] >> 63);
+    r->rid = (int32_t)(ax[k] << 1 >> 33);
+    r->rs = (int32_t)ax[k] + 1 > q_span ? (int32_t)ax[k] + 1 - q_span : 0;
+    r->re = (int32_t)ax[k + r->cnt - 1] + 1;
+    if (!r->rev) {
+        r->qs = (int32_t)ay[k] + 1 - q_span;
+        r->qe = (int32_t)ay[k + r->cnt - 1] + 1;
+    } else {
+        r->qs = qlen - ((int32_t)ay[k + r->cnt - 1] + 1);
+        r->qe = qlen - ((int32_t)ay[k] + 1 - q_span);
+    }
+    r->mlen = r->blen = (int32_t)(ay[r->as] >> 32 & 0xff);
+    for (int i = r->as + 1; i < r->as + r->cnt; ++i) {
+        const int span = (int)(ay[i] >> 32 & 0xff);
+        const int tl = (int32_t)ax[i] - (int32_t)ax[i - 1];
+        const int ql = (int32_t)ay[i] - (int32_t)ay[i - 1];
+        r->blen += tl > ql ? tl : ql;
+        r->mlen += tl > span && ql > span ? span : tl < ql ? tl : ql;
+    }
+}
+
+__device__ int get_mini_idx(int qlen, uint64_t ax, uint64_t ay, int32_t n, const uint64_t *mini_pos) {
+    int32_t x = (int32_t)ay, L = 0, R = n - 1;
+    if (ax >> 63) x = qlen - 1 - (int32_t)ay + (int32_t)(ay >> 32 & 0xff) - 1;
+    while (L <= R) {
+        const int32_t m = (int32_t)(((uint64_t)L + R) >> 1);
+        const int32_t y = (int32_t)mini_pos[m];
+        if (y < x) L = m + 1;
+        else if (y > x) R = m - 1;
+        else return m;
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= P.n_q) return;
+    const int64_t c0 = P.qc[q], c1 = P.qc[q + 1];
+    int n = (int)(c1 - c0);
+    const int32_t qlen = (int32_t)P.qlen[q];
+    if (n == 0 || qlen == 0) {
+        P.n_regs[q] = 0;
+        return;
+    }
+    const int64_t b0 = P.qb[q];
+    const uint64_t *ax = P.bx + b0, *ay = P.by + b0;
+    U128 *z = P.z + c0;
+    hymet_mm_reg *r = P.regs + c0;
+    uint32_t hash = P.name_hash[q];
+    hash ^= wang32((uint32_t)qlen) + wang32((uint32_t)P.seed);
+    hash = wang32(hash);
+    // ---- mm_gen_regs
+    for (int i = 0; i < n; ++i) {
+        const int64_t k = P.cboff[c0 + i] - b0;
+        const uint64_t u = P.cu[c0 + i];
+        const uint32_t h = (uint32_t)hash64((hash64(ax[k]) + hash64(ay[k])) ^ hash);
+        z[i].x = u ^ h;
+        z[i].y = (uint64_t)k << 32 | (uint32_t)(int32_t)u;
+    }
+    heap_sort(z, n, [](const U128 &a, const U128 &b) { return lt128(a, b); });
+    for (int i = 0; i < n >> 1; ++i) {
+        U128 t = z[i];
+        z[i] = z[n - 1 - i];
+        z[n - 1 - i] = t;
+    }
+    for (int i = 0; i < n; ++i) {
+        hymet_mm_reg *ri = &r[i];
+        ri->id = i;
+        ri->parent = -1;
+        ri->score = (int32_t)(z[i].x >> 32);
+        ri->hash = (uint32_t)z[i].x;
+        ri->cnt = (int32_t)z[i].y;
+        ri->as = (int32_t)(z[i].y >> 32);
+        ri->div = -1.0f;
+        ri->subsc = 0;
+        ri->n_sub = 0;
+        ri->strand_retained = 0;
+        ri->mapq = 0;
+        ri->pad = 0;
+        set_coor(ri, qlen, ax, ay);
+    }
+    // ---- mm_set_parent (mask_level, mask_len; no alignment: no dp_max branch)
+    {
+        int32_t *w = P.w + c0;
+        uint64_t *cov = P.cov + c0;
+        for (int i = 0; i < n; ++i) r[i].id = i;
+        int i, j, k;
+        w[0] = 0, r[0].parent = 0;
+        for (i = 1, k = 1; i < n; ++i) {
+            hymet_mm_reg *ri = &r[i];
+            const int si = ri->qs, ei = ri->qe;
+            int n_cov = 0, uncov_len = 0;
+            for (j = 0; j < k; ++j) {
+                const hymet_mm_reg *rp = &r[w[j]];
+                int sj = rp->qs, ej = rp->qe;
+                if (ej <= si || sj >= ei) continue;
+                if (sj < si) sj = si;
+                if (ej > ei) ej = ei;
+                cov[n_cov++] = (uint64_t)(uint32_t)sj << 32 | (uint32_t)ej;
+            }
+            if (n_cov == 0) goto set_parent_test;
+            {
+                int x = si;
+                heap_sort(cov, n_cov, [](uint64_t a, uint64_t b) { return a < b; });
+                for (int jj = 0; jj < n_cov; ++jj) {
+                    if ((int)(cov[jj] >> 32) > x) uncov_len += (int)(cov[jj] >> 32) - x;
+                    x = (int32_t)cov[jj] > x ? (int32_t)cov[jj] : x;
+                }
+                if (ei > x) uncov_len += ei - x;
+            }
+            for (j = 0; j < k; ++j) {
+                hymet_mm_reg *rp = &r[w[j]];
+                const int sj = rp->qs, ej = rp->qe;
+                if (ej <= si || sj >= ei) continue;
+                const int mn = ej - sj < ei - si ? ej - sj : ei - si;
+                const int mx = ej - sj > ei - si ? ej - sj : ei - si;
+                const int ol = si < sj ? (ei < sj ? 0 : ei < ej ? ei - sj : ej - sj) : (ej < si ? 0 : ej < ei ? ej - si : ei - si);
+                if (__fsub_rn(__fdiv_rn((float)ol, (float)mn), __fdiv_rn((float)uncov_len, (float)mx)) > P.mask_level &&
+                    uncov_len <= P.mask_len) {
+                    const int sci = ri->score;
+                    ri->parent = rp->parent;
+                    rp->subsc = rp->subsc > sci ? rp->subsc : sci;
+                    if (ri->cnt >= rp->cnt) ++rp->n_sub;
+                    break;
+                }
+            }
+        set_parent_test:
+            if (j == k) w[k++] = i, ri->parent = i, ri->n_sub = 0;
+        }
+    }
+    // ---- mm_select_sub (check_strand = 1) + mm_sync_regs
+    {
+        const int min_diff = P.k * 2;
+        const int min_strand_sc = (int)(P.max_gap * 0.8);
+        int i, k, n_2nd = 0;
+        for (i = k = 0; i < n; ++i) {
+            const int p = r[i].parent;
+            if (p == i) {
+                r[k++] = r[i];
+            } else if (((float)r[i].score >= __fmul_rn((float)r[p].score, P.pri_ratio) || r[i].score + min_diff >= r[p].score) &&
+                       n_2nd < P.best_n) {
+                if (!(r[i].qs == r[p].qs && r[i].qe == r[p].qe && r[i].rid == r[p].rid && r[i].rs == r[p].rs && r[i].re == r[p].re))
+                    r[k++] = r[i], ++n_2nd;
+            } else if (n_2nd < P.best_n && r[i].score > min_strand_sc && r[i].rev != r[p].rev) {
+                r[i].strand_retained = 1;
+                r[k++] = r[i], ++n_2nd;
+            }
+        }
+        if (k != n) {
+            int32_t *tmp = P.tmp + c0;
+            int max_id = -1;
+            for (i = 0; i < k; ++i) max_id = max_id > r[i].id ? max_id : r[i].id;
+            for (i = 0; i <= max_id; ++i) tmp[i] = -1;
+            for (i = 0; i < k; ++i)
+                if (r[i].id >= 0) tmp[r[i].id] = i;
+            for (i = 0; i < k; ++i) {
+                r[i].id = i;
+                if (r[i].parent >= 0 && tmp[r[i].parent] >= 0) r[i].parent = tmp[r[i].parent];
+                else r[i].parent = -1;
+            }
+        }
+        n = k;
+    }
+    // ---- mm_est_err
+    {
+        const int64_t m0 = P.mp_off[q];
+        const int32_t nm = (int32_t)(P.mp_off[q + 1] - m0);
+        const uint64_t *mp = P.mini_pos + m0;
+        if (nm > 0) {
+            uint64_t sum_k = 0;
+            for (int i = 0; i < nm; ++i) sum_k += mp[i] >> 32 & 0xff;
+            const float avg_k = __fdiv_rn((float)sum_k, (float)nm);
+            for (int i = 0; i < n; ++i) {
+                hymet_mm_reg *ri = &r[i];
+                ri->div = -1.0f;
+                if (ri->cnt == 0) continue;
+                const int a0 = ri->rev ? ri->as + ri->cnt - 1 : ri->as;
+                int32_t st = get_mini_idx(qlen, ax[a0], ay[a0], nm, mp), en = st;
+                if (st < 0) continue;
+                const int32_t l_ref = (int32_t)P.ref_len[ri->rid];
+                int32_t j, kk, n_match;
+                for (kk = 1, j = st + 1, n_match = 1; j < nm && kk < ri->cnt; ++j) {
+                    const int aa = ri->rev ? ri->as + ri->cnt - 1 - kk : ri->as + kk;
+                    const int32_t x = get_mini_idx(qlen, ax[aa], ay[aa], nm, mp);
+                    if (x == j) ++kk, ++n_match;
+                    en = j;
+                }
+                int32_t n_tot = en - st + 1;
+                if ((float)ri->qs > avg_k && (float)ri->rs > avg_k) ++n_tot;
+                if ((float)(qlen - ri->qe) > avg_k && (float)(l_ref - ri->re) > avg_k) ++n_tot;
+                ri->div = n_match >= n_tot ? 0.0f : (float)(1.0 - pow((double)n_match / n_tot, 1.0 / (double)avg_k));
+            }
+        }
+    }
+    // ---- mm_filter_strand_retained
+    {
+        int i, k;
+        for (i = k = 0; i < n; ++i) {
+            const int p = r[i].parent;
+            if (!r[i].strand_retained || r[i].div < __fmul_rn(r[p].div, 5.0f) || r[i].div < 0.01f) {
+                if (k < i) r[k++] = r[i];
+                else ++k;
+            }
+        }
+        n = k;
+    }
+    // ---- mm_set_mapq (no alignment)
+    {
+        const float q_coef = 40.0f;
+        int64_t sum_sc = 0;
+        for (int i = 0; i < n; ++i)
+            if (r[i].parent == r[i].id) sum_sc += r[i].score;
+        const float uniq_ratio = __fdiv_rn((float)sum_sc, (float)(sum_sc + P.rep_len[q]));
+        for (int i = 0; i < n; ++i) {
+            hymet_mm_reg *ri = &r[i];
+            if (ri->parent == ri->id) {
+                const float pen_s1 = __fmul_rn(ri->score > 100 ? 1.0f : __fmul_rn(0.01f, (float)ri->score), uniq_ratio);
+                float pen_cm = ri->cnt > 10 ? 1.0f : __fmul_rn(0.1f, (float)ri->cnt);
+                pen_cm = pen_s1 < pen_cm ? pen_s1 : pen_cm;
+                const int subsc = ri->subsc > P.min_chain_score ? ri->subsc : P.min_chain_score;
+                const float x = __fdiv_rn((float)subsc, (float)ri->score);
+                int mapq = (int)__fmul_rn(__fmul_rn(__fmul_rn(pen_cm, q_coef), __fsub_rn(1.0f, x)), logf((float)ri->score));
+                mapq -= (int)__fadd_rn(__fmul_rn(4.343f, logf((float)(ri->n_sub + 1))), .499f);
+                mapq = mapq > 0 ? mapq : 0;
+                ri->mapq = mapq < 60 ? mapq : 60;
+            } else
+                ri->mapq = 0;
+        }
+    }
+    P.n_regs[q] = n;
+}
+
+}  // namespace
+
+int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const uint64_t *cu, const int64_t *cboff,
+                   const int64_t *qc, const int64_t *qb, const uint64_t *mini_pos, const int64_t *mp_off, const int64_t *qlen,
+                   const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
+                   int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs) {
+    if (n_q <= 0) return HYMET_OK;
+    RegParams P{bx, by, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
+                o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
+                tmp, n_regs};
+    hipLaunchKernelGGL(regions_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, ctx->stream, P);
+    HY_CHECK_LAUNCH("regions_kernel");
+    return HYMET_OK;
+}
+
+}  // namespace mm
+}  // namespace hymet

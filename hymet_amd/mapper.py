@@ -51,6 +51,78 @@ def split_parts(lengths: np.ndarray, batch_size: float = 2e9, mini_batch: float 
     return parts
 
 
+class MapOpt(_c.Structure):
+    """hymet_mm_opt == minimap2 mm_mapopt_t after mm_set_opt("asm10") (options.c)."""
+    _fields_ = [("mid_occ", _c.c_int32), ("q_occ_frac", _c.c_float), ("max_max_occ", _c.c_int32),
+                ("occ_dist", _c.c_int32), ("min_cnt", _c.c_int32), ("min_chain_score", _c.c_int32),
+                ("bw", _c.c_int32), ("bw_long", _c.c_int32), ("max_gap", _c.c_int32), ("max_chain_skip", _c.c_int32),
+                ("rmq_inner_dist", _c.c_int32), ("rmq_size_cap", _c.c_int32), ("rmq_rescue_size", _c.c_int32),
+                ("rmq_rescue_ratio", _c.c_float), ("chain_gap_scale", _c.c_float), ("chain_skip_scale", _c.c_float),
+                ("mask_level", _c.c_float), ("pri_ratio", _c.c_float), ("mask_len", _c.c_int32), ("best_n", _c.c_int32),
+                ("a", _c.c_int32), ("b", _c.c_int32), ("seed", _c.c_int32)]
+
+    # asm presets clamp mid_occ to [50, 500] (options.c mm_set_opt "asm*")
+    min_mid_occ = 50
+    max_mid_occ = 500
+    mid_occ_frac = 2e-4
+
+    @classmethod
+    def asm10(cls) -> "MapOpt":
+        o = cls()
+        o.mid_occ = 0
+        o.q_occ_frac = 0.01
+        o.max_max_occ, o.occ_dist = 4095, 500
+        o.min_cnt, o.min_chain_score = 3, 40
+        o.bw, o.bw_long, o.max_gap, o.max_chain_skip = 1000, 100000, 10000, 25
+        o.rmq_inner_dist, o.rmq_size_cap, o.rmq_rescue_size = 1000, 100000, 1000
+        o.rmq_rescue_ratio = 0.1
+        o.chain_gap_scale, o.chain_skip_scale = 0.8, 0.0
+        o.mask_level, o.pri_ratio = 0.5, 0.8
+        o.mask_len, o.best_n, o.a, o.b, o.seed = 2 ** 31 - 1, 50, 1, 9, 11
+        return o
+
+    def resolve_mid_occ(self, part: "IndexPart") -> int:
+        """options.c mm_mapopt_update: set once (from the first index part) when <= 0."""
+        if self.mid_occ <= 0:
+            m = part.max_occ(self.mid_occ_frac)
+            if m < self.min_mid_occ:
+                m = self.min_mid_occ
+            if self.max_mid_occ > self.min_mid_occ and m > self.max_mid_occ:
+                m = self.max_mid_occ
+            self.mid_occ = m
+        if self.bw_long < self.bw:
+            self.bw_long = self.bw
+        return self.mid_occ
+
+
+REG_DTYPE = np.dtype([(n, np.int32) for n in ("qs", "qe", "rs", "re", "rid", "rev", "mlen", "blen", "mapq", "cnt", "score",
+                                              "subsc", "parent", "id", "n_sub", "strand_retained")]
+                     + [("div", np.float32), ("as_", np.int32), ("hash", np.uint32), ("pad", np.int32)])
+
+
+def x31_hash(name: str) -> int:
+    """khash __ac_X31_hash_string (signed char arithmetic, 32-bit wrap)."""
+    b = name.encode()
+    if not b:
+        return 0
+    h = b[0] if b[0] < 128 else b[0] - 256
+    h &= 0xFFFFFFFF
+    for c in b[1:]:
+        c = c if c < 128 else c - 256
+        h = ((h << 5) - h + c) & 0xFFFFFFFF
+    return h
+
+
+@dataclass
+class MapResult:
+    off: np.ndarray        # n_q + 1
+    rep_len: np.ndarray    # n_q
+    regs: np.ndarray       # REG_DTYPE
+
+    def query(self, q):
+        return self.regs[self.off[q]:self.off[q + 1]]
+
+
 class IndexPart:
     """One minimizer index part resident in HBM (hymet_mm_index)."""
 
@@ -109,3 +181,46 @@ def sketch(gpu, pool: DevicePool, w: int = 10, k: int = 15, rid_mode: int = 0):
             continue
         check(rc, "hymet_mm_sketch")
         return x[:n.value], y[:n.value]
+
+
+def map_part(gpu, part: "IndexPart", qpool: DevicePool, opt: MapOpt, name_hash: Optional[np.ndarray] = None) -> MapResult:
+    """Map every query of a packed pool against one index part (minimap2 -x asm10)."""
+    ss = qpool.ss
+    nq = ss.n
+    starts = np.ascontiguousarray(ss.starts, dtype=np.int64)
+    lens = np.ascontiguousarray(ss.lengths, dtype=np.int64)
+    if name_hash is None:
+        name_hash = np.array([x31_hash(n) for n in ss.names], dtype=np.uint32)
+    name_hash = np.ascontiguousarray(name_hash, dtype=np.uint32)
+    h = _c.c_void_p()
+    gpu.call("hymet_mm_map", part.h, _c.byref(opt), ptr(qpool.w2b), ptr(qpool.wmask), starts.ctypes.data_as(_c.c_void_p),
+             lens.ctypes.data_as(_c.c_void_p), name_hash.ctypes.data_as(_c.c_void_p), nq, _c.byref(h))
+    try:
+        n = _c.c_int64()
+        check(gpu.lib.hymet_mm_result_size(h, _c.byref(n)), "hymet_mm_result_size")
+        off = np.zeros(nq + 1, np.int64)
+        rl = np.zeros(max(nq, 1), np.int32)
+        regs = np.zeros(n.value, REG_DTYPE)
+        check(gpu.lib.hymet_mm_result_copy(h, off.ctypes.data_as(_c.c_void_p), rl.ctypes.data_as(_c.c_void_p),
+                                           regs.ctypes.data_as(_c.c_void_p)), "hymet_mm_result_copy")
+    finally:
+        gpu.lib.hymet_mm_result_destroy(h)
+    return MapResult(off, rl[:nq], regs)
+
+
+def paf_lines(qname: str, qlen: int, regs, rep_len: int, tnames, tlens) -> List[str]:
+    """format.c mm_write_paf3 + write_tags without CIGAR (no `cg`/`NM` tags)."""
+    out = []
+    for r in regs:
+        prim = r["id"] == r["parent"]
+        fields = [qname, str(qlen), str(r["qs"]), str(r["qe"]), "+-"[r["rev"]], tnames[r["rid"]], str(tlens[r["rid"]]),
+                  str(r["rs"]), str(r["re"]), str(r["mlen"]), str(r["blen"]), str(r["mapq"]),
+                  "tp:A:" + ("P" if prim else "S"), f"cm:i:{r['cnt']}", f"s1:i:{r['score']}"]
+        if prim:
+            fields.append(f"s2:i:{r['subsc']}")
+        d = float(r["div"])
+        if 0.0 <= d <= 1.0:
+            fields.append("dv:f:" + ("0" if d == 0.0 else "%.4f" % d))
+        fields.append(f"rl:i:{rep_len}")
+        out.append("\t".join(fields))
+    return out

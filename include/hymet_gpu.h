@@ -98,6 +98,46 @@ int hymet_mm_index_max_occ(hymet_ctx *ctx, const hymet_mm_index *idx, float frac
 /* sorted (bucket = minimizer hash, y) arrays, n_pos entries each (tests / persistence) */
 int hymet_mm_index_export(hymet_ctx *ctx, const hymet_mm_index *idx, uint32_t *h_hash, uint64_t *h_pos);
 
+/* ------------------------------------------------ mapping (minimap2 -x asm10)
+ * Replaces `minimap2 -x asm10 reference.mmi input/ *.fna > resultados.paf`
+ * (scripts/minimap2.sh:23).  Options mirror mm_mapopt_t after mm_set_opt("asm10") and
+ * mm_mapopt_update (mid_occ resolved by the caller from hymet_mm_index_max_occ). */
+typedef struct {
+    int32_t mid_occ;
+    float q_occ_frac;
+    int32_t max_max_occ, occ_dist;
+    int32_t min_cnt, min_chain_score;
+    int32_t bw, bw_long, max_gap, max_chain_skip;
+    int32_t rmq_inner_dist, rmq_size_cap, rmq_rescue_size;
+    float rmq_rescue_ratio;
+    float chain_gap_scale, chain_skip_scale;
+    float mask_level, pri_ratio;
+    int32_t mask_len, best_n, a, b, seed;
+} hymet_mm_opt;
+
+/* one PAF record before formatting (hit.c mm_reg1_t fields that PAF prints) */
+typedef struct {
+    int32_t qs, qe, rs, re, rid, rev;
+    int32_t mlen, blen, mapq, cnt, score, subsc, parent, id, n_sub, strand_retained;
+    float div;
+    int32_t as;
+    uint32_t hash;
+    int32_t pad;
+} hymet_mm_reg;
+
+typedef struct hymet_mm_result hymet_mm_result;
+/* Map n_q queries (packed pool + host pool offsets/lengths) against one index part.
+ * h_name_hash[q] = khash X31 hash of the query name (map.c mm_map_frag). */
+int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *opt,
+                 const uint32_t *d_2b, const uint32_t *d_mask, const int64_t *h_starts,
+                 const int64_t *h_lens, const uint32_t *h_name_hash, int32_t n_q,
+                 hymet_mm_result **out);
+/* n_regs total; h_off: n_q+1 per-query offsets; h_rep_len: n_q; h_regs: n_regs records */
+int hymet_mm_result_size(const hymet_mm_result *res, int64_t *n_regs);
+int hymet_mm_result_copy(const hymet_mm_result *res, int64_t *h_off, int32_t *h_rep_len,
+                         hymet_mm_reg *h_regs);
+int hymet_mm_result_destroy(hymet_mm_result *res);
+
 #ifdef __cplusplus
 }
 #endif
