@@ -138,6 +138,20 @@ int hymet_mm_result_copy(const hymet_mm_result *res, int64_t *h_off, int32_t *h_
                          hymet_mm_reg *h_regs);
 int hymet_mm_result_destroy(hymet_mm_result *res);
 
+/* --------------------------------------------------- weighted LCA (classify)
+ * Replaces the per-query loop of scripts/classification_cami.py:290-308 (+ _weighted_lca
+ * :251-288; mode 0) and scripts/classification.py:141-157 (mode 1).  PAF lines are given
+ * per query in PAF order (d_q_off CSR); targets/taxids are integer-encoded by the host.
+ * hymet_lca_ref_counts: d_counts[t] += #lines with target t (ref_abundance, caller-zeroed;
+ * all-reduced across ranks by the caller). */
+int hymet_lca_ref_counts(hymet_ctx *ctx, const int32_t *d_line_t, int64_t n_lines, int32_t *d_counts);
+int hymet_lca(hymet_ctx *ctx, int mode, int32_t n_q, const int64_t *d_q_off, const int32_t *d_line_t,
+              const int64_t *d_line_blen, const int64_t *d_line_qlen, const uint8_t *d_line_exact,
+              const int32_t *d_ref_counts, const int32_t *d_t_tax, const int32_t *d_tax_names,
+              const uint8_t *d_tax_in_hier, int32_t *d_scr_tid, double *d_scr_w, int32_t *d_scr_nm,
+              double *d_scr_nw, int32_t *d_out_depth, int32_t *d_out_names, double *d_out_conf,
+              int32_t *d_out_tax);
+
 #ifdef __cplusplus
 }
 #endif
