@@ -302,7 +302,10 @@ class Classifier:
             v = self._tcache.get(t)
             if v is None:
                 tid = self.tax.lookup(t)
-                v = self._taxid_index(tid) if tid else -1
+                # CAMI: only truthy taxids count (_lookup_taxid :243-249); legacy: any key
+                # present in the map counts, even an empty TaxID (classification.py:88-93)
+                ok = (tid is not None) if self.variant == LEGACY else bool(tid)
+                v = self._taxid_index(tid) if ok else -1
                 self._tcache[t] = v
             out[k] = v
         return out
