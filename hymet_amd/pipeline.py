@@ -1,0 +1,180 @@
+"""The fused, device-resident hot path of `bin/hymet run` (run_hymet_cami.sh steps 1-5):
+
+    screen (3 sketch DBs, one hash pass)  -> mash.sh selection per DB -> union (sort -u)
+    -> limit_candidates -> [candidate-keyed index cache, as run_hymet_cami.sh:135-171]
+    -> minimap2 asm10 mapping per -I2g part -> classification_cami weighted LCA -> TSV
+
+Everything between the input pool and the TSV stays in HBM except the small host-side
+text steps (screen rows, candidate lists) and the region records that become PAF lines.
+Multi-GPU: every rank holds its own contig shard; the screen counts and
+the per-target PAF line counts are all-reduced; rank 0 assembles the TSV in the
+reference's query order.
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import classify as cls
+from . import mapper as mp
+from . import screen as scr
+from . import select as sel
+from .msh import SketchDB
+from .seqio import DevicePool, SeqSet, from_records
+
+
+@dataclass
+class Config:
+    mash_thresh: str = "0.9"          # MASH_THRESH (run_hymet_cami.sh:31)
+    cand_max: int = 5000              # CAND_MAX (run_hymet_cami.sh:26)
+    dedupe: bool = False              # SPECIES_DEDUP
+    split_idx: str = "2g"             # SPLIT_IDX / minimap2 -I
+    w: int = 10                       # minimap2 -d defaults
+    k: int = 15
+    map_batch_bases: int = 40_000_000  # query bases per device mapping batch (HBM budget)
+    n_input_files: int = 1            # run_hymet_cami.sh copies one FASTA into input/
+
+
+@dataclass
+class IndexSet:
+    names: List[str]
+    lens: np.ndarray
+    parts: List[mp.IndexPart]
+    part_first: List[int]             # global target index of each part's rid 0
+
+
+@dataclass
+class RunResult:
+    selected: List[str]
+    screen_rows: List[List[str]]      # per DB, rows after sort -u -k5,5 | sort -gr
+    thresholds: List[str]
+    tsv: bytes
+    n_queries: int
+    n_classified: int
+    n_paf_lines: int
+    paf: Optional[List[str]] = None
+
+
+class Pipeline:
+    def __init__(self, gpu, dbs: Sequence[SketchDB], ref_lookup, taxonomy, hierarchy, cfg: Config = None, comm=None,
+                 variant: int = cls.CAMI):
+        """ref_lookup(names) -> SeqSet of the candidate genomes in combined_genomes.fasta
+        order (the download cache; scripts/downloadDB.py is outside the accelerated path)."""
+        self.gpu, self.cfg, self.comm = gpu, cfg or Config(), comm
+        self.dbs = list(dbs)
+        self.tables = [scr.ScreenTable(gpu, db) for db in self.dbs]
+        self.ref_lookup = ref_lookup
+        self.classifier = cls.Classifier(gpu, taxonomy, hierarchy, variant)
+        self.index_cache: Dict[str, IndexSet] = {}
+        self.opt: Optional[mp.MapOpt] = None
+
+    # ------------------------------------------------------------------ stages
+    def screen_select(self, pool: DevicePool):
+        res = scr.screen(self.gpu, pool, self.dbs, self.tables, self.comm)
+        rows, thr, selections = [], [], []
+        for r in res:
+            s = sel.sort_gr(sel.sort_unique_k5(r.lines(v_max=0.9)))
+            t, top, names = sel.select_threshold(s, self.cfg.mash_thresh, self.cfg.n_input_files)
+            rows.append(s)
+            thr.append(t)
+            selections.append(names)
+        selected = sel.union_sorted(*selections) if len(selections) > 1 else sel.union_sorted(selections[0])
+        scores = sel.best_scores(rows)
+        limited = sel.limit(selected, scores, self.cfg.cand_max, self.cfg.dedupe)
+        return limited, rows, thr
+
+    def index_for(self, selected: List[str]) -> IndexSet:
+        key = hashlib.sha1(("".join(n + "\n" for n in selected)).encode()).hexdigest()
+        if key in self.index_cache:
+            return self.index_cache[key]
+        refs: SeqSet = self.ref_lookup(selected)
+        parts_idx = mp.split_parts(refs.lengths, float(mp.parse_num(self.cfg.split_idx)))
+        parts, first = [], []
+        for p in parts_idx:
+            sub = refs.subset(p) if len(parts_idx) > 1 else refs
+            parts.append(mp.IndexPart(self.gpu, sub, self.cfg.w, self.cfg.k))
+            first.append(int(p[0]))
+        ix = IndexSet(list(refs.names), np.asarray(refs.lengths, np.int64), parts, first)
+        self.index_cache = {key: ix}  # one cached candidate set, like the sha1 cache dir
+        return ix
+
+    def map_all(self, ix: IndexSet, queries: SeqSet, qpool: Optional[DevicePool] = None):
+        """Per part, per query batch -> list of (part, query offset, MapResult)."""
+        if self.opt is None:
+            self.opt = mp.MapOpt.asm10()
+            self.opt.resolve_mid_occ(ix.parts[0])   # mm_mapopt_update: first part fixes mid_occ
+        batches = _batches(queries.lengths, self.cfg.map_batch_bases)
+        out = []
+        for pi, part in enumerate(ix.parts):
+            for b0, b1 in batches:
+                if qpool is not None and len(batches) == 1:
+                    qp = qpool
+                else:
+                    qp = DevicePool(self.gpu, queries.subset(range(b0, b1)), DevicePool.ALPHA_MINIMAP2)
+                out.append((pi, b0, mp.map_part(self.gpu, part, qp, self.opt)))
+        return out
+
+    def paf_table(self, ix: IndexSet, queries: SeqSet, results, with_text=False):
+        """PAF lines in minimap2's output order (part-major, query order) as classifier arrays."""
+        qnames = queries.names
+        qidx: Dict[int, int] = {}
+        order_q: List[int] = []
+        lq, lt, lb, ll, le = [], [], [], [], []
+        text = [] if with_text else None
+        for pi, b0, res in results:
+            first = ix.part_first[pi]
+            regs = res.regs
+            if len(regs) == 0:
+                continue
+            nper = np.diff(res.off)
+            qs = np.repeat(np.arange(len(nper)) + b0, nper)
+            for q in np.flatnonzero(nper) + b0:
+                if int(q) not in qidx:
+                    qidx[int(q)] = len(order_q)
+                    order_q.append(int(q))
+            lq.append(np.array([qidx[int(q)] for q in qs], np.int32))
+            lt.append((regs["rid"] + first).astype(np.int32))
+            lb.append(regs["blen"].astype(np.int64))
+            ll.append(queries.lengths[qs].astype(np.int64))
+            le.append(np.zeros(len(regs), np.uint8))
+            if with_text:
+                for q in range(len(nper)):
+                    rr = res.query(q)
+                    if len(rr):
+                        g = q + b0
+                        text.extend(mp.paf_lines(qnames[g], int(queries.lengths[g]), rr, int(res.rep_len[q]),
+                                                 ix.names[first:], ix.lens[first:]))
+        cat = (lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt))
+        table = cls.PafTable([qnames[q] for q in order_q], cat(lq, np.int32), list(ix.names), cat(lt, np.int32),
+                             cat(lb, np.int64), cat(ll, np.int64), cat(le, np.uint8))
+        return table, text
+
+    # ------------------------------------------------------------------- run
+    def run(self, queries: SeqSet, qpool_mash: DevicePool = None, qpool_mm: DevicePool = None, with_paf=False) -> RunResult:
+        gpu = self.gpu
+        qpool_mash = qpool_mash or DevicePool(gpu, queries, DevicePool.ALPHA_MASH)
+        selected, rows, thr = self.screen_select(qpool_mash)
+        if not selected:
+            raise RuntimeError("candidate list empty after applying limit")  # run_hymet_cami.sh:126
+        ix = self.index_for(selected)
+        results = self.map_all(ix, queries, qpool_mm)
+        table, text = self.paf_table(ix, queries, results, with_paf)
+        res = self.classifier.run(table, comm=self.comm)
+        rws = self.classifier.rows(res)
+        tsv = self.classifier.tsv_bytes(res)
+        return RunResult(selected, rows, thr, tsv, len(rws), sum(1 for r in rws if r[1] != "Unknown"), table.n_lines, text)
+
+
+def _batches(lengths: np.ndarray, max_bases: int):
+    out, b0, acc = [], 0, 0
+    for i, L in enumerate(lengths):
+        if acc and acc + int(L) > max_bases:
+            out.append((b0, i))
+            b0, acc = i, 0
+        acc += int(L)
+    if b0 < len(lengths) or not out:
+        out.append((b0, len(lengths)))
+    return out

@@ -217,3 +217,20 @@ def format_screen(db: SketchDB, shared, median, set_size, v_max=0.9, identity_mi
             continue
         out.append("%g\t%d/%d\t%d\t%g\t%s\t%s" % (ident, x, sl, int(median[i]) if x else 0, pv, db.names[i], db.comments[i]))
     return out
+
+
+def sketch_sequences(gpu, pool, k: int = 21, seed: int = 42, s: int = 1000):
+    """Mash `sketch` of every record of a packed pool (one reference per record): the
+    bottom-s distinct canonical k-mer hashes, sorted.  Used to build sketch DBs (.msh) on
+    the device; hashing is the screen kernel in candidates-only mode (ndb = 0)."""
+    out = []
+    ss = pool.ss
+    for i in range(ss.n):
+        b = int(ss.starts[i])
+        L = int(ss.lengths[i])
+        if L < k:
+            out.append(np.zeros(0, np.uint64))
+            continue
+        _, bottom, _ = count_pool(gpu, pool, [], k, seed, s, b, b + L - k + 1)
+        out.append(bottom)
+    return out
