@@ -1,11 +1,18 @@
 #!/usr/bin/env python3
-"""Benchmark contract (see README/DESIGN.md §Measurement).
+"""Benchmark contract.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload screen|cami-medium]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cami-medium|screen]
 
-One "step" = one pass of the hot path over one batch of synthetic input that is already
-resident in HBM.  Rank 0 prints ONE JSON line.  Multi-GPU: launched by the driver through
-torch.distributed.run, one rank per GPU; contigs/k-mer positions are sharded (weak scaling).
+One step = one pass of the HYMET hot path (screen -> select -> limit -> map -> LCA -> TSV)
+over one batch of synthetic, HBM-resident input.  Default workload: CAMI-medium (C4,
+BASELINE.json configs[3]; it fits one MI355X): 12 taxa, ~1 Gbp of contigs per rank, 744
+candidate genomes (~3 Gbp, two -I2g index parts), a sketch1-sized DB (1e5 refs x 1000).
+The candidate-keyed index is built in the untimed cold run (run_hymet_cami.sh caches it the
+same way) and its time is reported separately.  Rank 0 prints ONE JSON line.
+
+Multi-GPU (torch.distributed.run, one rank per GPU): every rank holds its own ~1 Gbp contig
+sample of the same community (weak scaling); screen counts and per-target PAF line counts
+are all-reduced over RCCL; rank 0 writes the TSV.
 """
 from __future__ import annotations
 
@@ -13,6 +20,7 @@ import argparse
 import json
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -21,151 +29,240 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "contigs/s + Mbp/s classified, CAMI-medium, 1/2/4/8 MI355X; % HBM roofline"
 
 
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
-        print(*a, file=sys.stderr, flush=True)
+        print(f"[bench {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
 
 
-def make_screen_workload(rng, n_refs, s, n_contigs, total_bases):
-    """C2-shaped screen workload: a pooled contig set and a sketch DB with n_refs x s hashes
-    (the first 25 references are real sketches of genomes the contigs come from)."""
+def roofline_from_prof(prof, prefer=None):
+    """Dominant kernel = the largest summed device time among kernels with a byte model."""
+    cand = {k: v for k, v in prof.items() if v[2] > 0}
+    if not cand:
+        return None
+    name = prefer if prefer in cand else max(cand, key=lambda k: cand[k][0])
+    ms, n, b = cand[name]
+    achieved = b / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None, "kernel": name, "kernel_avg_ms": ms / max(n, 1), "launches": n,
+            "alg_bytes_per_launch": b / max(n, 1)}
+
+
+# ------------------------------------------------------------------ CAMI-medium
+def build_cami(args, comm, gpu):
+    from hymet_amd import pipeline, screen as scr, synth
     from hymet_amd.msh import SketchDB
-    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
-    n_src = 25
-    glen = 2_000_000
-    genomes = [acgt[rng.integers(0, 4, glen, dtype=np.uint8)].tobytes() for _ in range(n_src)]
-    lens = np.clip(rng.lognormal(np.log(14963), 1.0, n_contigs), 4404, 400_000).astype(np.int64)
-    lens = (lens * (total_bases / lens.sum())).astype(np.int64).clip(1000, glen - 1)
-    recs = []
-    for i, L in enumerate(lens):
-        g = genomes[i % n_src]
-        st = int(rng.integers(0, glen - L))
-        recs.append((f"ctg{i}", "", g[st:st + int(L)]))
-    hashes = rng.integers(0, 2 ** 63, size=(n_refs, s), dtype=np.int64).astype(np.uint64) * np.uint64(2) + np.uint64(1)
-    hashes.sort(axis=1)
-    db = SketchDB(k=21, seed=42, sketch_size=s, names=[f"GCF_{i:09d}.1_ref_genomic.fna.gz" for i in range(n_refs)],
-                  comments=["[1 seqs] synthetic"] * n_refs, lengths=np.full(n_refs, glen, np.int64),
-                  offsets=np.arange(n_refs + 1, dtype=np.int64) * s, hashes=hashes.reshape(-1))
-    return recs, db, genomes
-
-
-def bench_screen(args, comm, gpu, torch):
-    from hymet_amd import screen as scr
     from hymet_amd.seqio import DevicePool, from_records
-    rng = np.random.default_rng(1)
-    n_refs = args.screen_refs
-    recs, db, genomes = make_screen_workload(rng, n_refs, 1000, 1043, 53_800_000)
-    ss = from_records(recs)
-    pool = DevicePool(gpu, ss, DevicePool.ALPHA_MASH)
-    table = scr.ScreenTable(gpu, db)
-    torch.cuda.synchronize()
-    n_pos = max(0, pool.n_bases - 21 + 1)
-    b, e = comm.shard_range(n_pos) if comm.world > 1 else (0, n_pos)
+    t0 = time.time()
+    w = synth.make_cami(np.random.default_rng(1234), n_taxa=args.taxa, per_taxon=args.per_taxon,
+                        contig_gbp=args.contig_gbp, contig_rng=np.random.default_rng(5000 + comm.rank))
+    log(f"synth: {len(w.refs)} refs {w.ref_bases/1e9:.2f} Gbp, {len(w.contigs)} contigs {w.contig_bases/1e6:.0f} Mbp "
+        f"({time.time()-t0:.1f}s)")
+    t0 = time.time()
+    db_names = [n + ".fna.gz" for n in w.ref_names]
+    refs_ss = from_records([(n, "", s) for n, s in zip(w.ref_names, w.refs)])
+    sk = scr.sketch_sequences(gpu, DevicePool(gpu, refs_ss, DevicePool.ALPHA_MASH), 21, 42, 1000)
+    n_dec = max(0, args.screen_refs - len(sk))
+    dec = synth.decoy_sketches(np.random.default_rng(99), n_dec, 1000)
+    lens = [len(h) for h in sk] + [1000] * n_dec
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    hashes = np.concatenate(sk + [dec.reshape(-1)])
+    names = db_names + [f"GCF_{900000000 + i:09d}.1_decoy_genomic.fna.gz" for i in range(n_dec)]
+    db = SketchDB(names=names, comments=[f"[1 seqs] {n}" for n in names], lengths=np.full(len(names), 4_000_000, np.int64),
+                  offsets=off, hashes=hashes)
+    log(f"sketch DB: {db.n_refs} refs, {len(db.hashes)/1e6:.0f}M hashes ({time.time()-t0:.1f}s)")
+    td = tempfile.mkdtemp(prefix="hymet_bench_")
+    tax = os.path.join(td, "detailed_taxonomy.tsv")
+    hier = os.path.join(td, "taxonomy_hierarchy.tsv")
+    open(tax, "w").write(w.taxonomy_tsv())
+    open(hier, "w").write(w.hierarchy_tsv())
+    by_name = {n + ".fna.gz": i for i, n in enumerate(w.ref_names)}
 
-    def step():
-        counts, bottom, nk = scr.count_pool(gpu, pool, [table], 21, 42, 1000, b, e)
-        if comm.world > 1:
-            comm.allreduce_sum_(counts[0])
-        sh, md = scr.table_stats(gpu, table, counts[0])
-        return nk
+    def ref_lookup(sel):
+        return refs_ss.subset([by_name[n] for n in sel])
 
-    for _ in range(args.warmup):
-        step()
+    cfg = pipeline.Config(map_batch_bases=int(args.batch_mbp * 1e6))
+    pipe = pipeline.Pipeline(gpu, [db], ref_lookup, tax, hier, cfg, comm)
+    queries = from_records([(n, "", s) for n, s in zip(w.contig_names, w.contigs)])
+    t0 = time.time()
+    pq = pipe.prepare(queries)
+    gpu.sync()
+    log(f"queries resident: {len(pq.batches)} map batches ({time.time()-t0:.1f}s)")
+    return w, db, pipe, pq, refs_ss, tax, hier, by_name
+
+
+def bench_cami(args, comm, gpu, torch):
+    w, db, pipe, pq, refs_ss, tax, hier, by_name = build_cami(args, comm, gpu)
     comm.barrier()
+    t0 = time.time()
+    res = pipe.run(pq)                      # cold: builds the candidate index (cached afterwards)
+    gpu.sync()
+    cold = time.time() - t0
+    ix = pipe.index_for(res.selected)
+    log(f"cold run {cold:.1f}s: {len(res.selected)} candidates, {len(ix.parts)} index parts, "
+        f"{res.n_classified}/{res.n_queries} classified, {res.n_paf_lines} PAF lines")
+    for _ in range(max(0, args.warmup - 1)):
+        pipe.run(pq)
+    gpu.sync()
+    comm.barrier()
+    gpu.prof_reset()
+    gpu.prof(True)
     torch.cuda.synchronize()
-    # kernel timing with HIP events on the stream the kernels are launched on
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    comm.barrier()
     t0 = time.perf_counter()
-    ev0.record()
-    nk = 0
     for _ in range(args.steps):
-        nk = step()
-    ev1.record()
+        res = pipe.run(pq)
     torch.cuda.synchronize()
     comm.barrier()
-    t1 = time.perf_counter()
-    dt = comm.max_float(t1 - t0)
-    # dominant kernel alone (hash/probe/count), timed separately with events
-    counts = [gpu.zeros(table.n_slots + 1, torch.int32)]
-    cand = gpu.empty(1 << 20, torch.int64)
-    cn = gpu.zeros(1, torch.int64)
-    nkt = gpu.zeros(1, torch.int64)
-    import ctypes
-    from hymet_amd._lib import ptr
-    keys_arr = (ctypes.c_void_p * 4)(ptr(table.keys).value)
-    slots_arr = (ctypes.c_int64 * 4)(table.n_slots)
-    cnt_arr = (ctypes.c_void_p * 4)(ptr(counts[0]).value)
-    thr = int(16 * 1000 / max(1, e - b) * 2 ** 64)
-    kt = []
-    for _ in range(5):
-        cn.zero_()
-        a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a0.record()
-        gpu.call("hymet_screen_count", ptr(pool.w2b), ptr(pool.wmask), pool.n_bases, b, e, 21, 42, 1, keys_arr,
-                 slots_arr, cnt_arr, thr, ptr(cand), 1 << 20, ptr(cn), ptr(nkt))
-        a1.record()
-        torch.cuda.synchronize()
-        kt.append(a0.elapsed_time(a1) / 1e3)
-    k_avg = float(np.mean(kt[1:]))
-    bases = e - b
-    alg_bytes = bases * 0.375 + nk * 8.0  # packed read + one 8-B key probe per k-mer
-    achieved = alg_bytes / k_avg / 1e9
-    n_contigs = len(recs)
-    total_mbp = ss.total_bases / 1e6
-    value = n_contigs * args.steps / dt
-    res = {
-        "metric": "contigs/s (screen stage, C2 Zymo-shaped pool vs sketch1-sized DB)",
-        "value": value, "unit": "contigs/s", "n_gpus": comm.world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u64", "data": "synthetic",
-        "mbp_per_s": total_mbp * args.steps / dt,
-        "config": {"workload": "C2 screen: 1043 contigs / 53.8 Mbp vs %d refs x 1000 hashes (k=21, seed 42)" % n_refs,
-                   "parallelism": f"kmer-shard x{comm.world}"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "screen_count_kernel<21>", "kernel_ms": k_avg * 1e3,
-                     "alg_bytes_per_launch": alg_bytes},
+    dt = comm.max_float(time.perf_counter() - t0)
+    gpu.prof(False)
+    prof = gpu.prof_table()
+    n_contigs = comm.world * len(w.contigs)        # weak scaling: every rank its own sample
+    mbp = sum(comm.allgather_np(np.array([pq.queries.total_bases], np.int64)))[0] / 1e6
+    step = dt / args.steps
+    log("kernel time per step (ms): " + ", ".join(f"{k}={v[0]/args.steps:.1f}" for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])))
+    out = {
+        "metric": METRIC, "value": n_contigs / step, "unit": "contigs/s", "n_gpus": comm.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": step * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "mbp_per_s": mbp / step,
+        "config": {"workload": f"CAMI-medium (C4): {args.taxa} taxa, {len(w.contigs)} contigs / {pq.queries.total_bases/1e6:.0f} Mbp "
+                               f"per rank; {len(res.selected)} candidates / {refs_ss.total_bases/1e9:.2f} Gbp in {len(ix.parts)} "
+                               f"-I2g parts; sketch DB {db.n_refs} refs x 1000",
+                   "global_contigs": n_contigs, "parallelism": f"contig-shard x{comm.world}"},
+        "cold_run_s": cold,
+        "stage_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
+        "roofline": roofline_from_prof(prof),
     }
     if comm.rank == 0 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline_screen(recs, db)
-    return res
+        try:
+            out["cpu_baseline"] = cpu_baseline_cami(args, gpu, pipe, pq, db, res, w, tax, hier)
+        except Exception as e:  # the baseline is informative; never lose the GPU line
+            out["cpu_baseline"] = {"error": repr(e)}
+    return out
 
 
-def cpu_baseline_screen(recs, db, budget_s=15.0):
-    from oracle import oracle_lib
-    sub, tot = [], 0
-    for r in recs:
-        sub.append(r[2])
-        tot += len(r[2])
-        if tot > 4_000_000:
+def cpu_baseline_cami(args, gpu, pipe, pq, db, res, w, tax, hier, budget_s=20.0):
+    """The CPU oracle restatement on a bounded sample of the same workload: the sample
+    contigs are screened against the same DB (table prebuilt), mapped against the same
+    candidate index parts (exported from the device index, content-identical to the oracle's
+    own per tests/test_mm_index_gpu.py) and classified.  One-time table/index builds are
+    excluded, like the warm GPU step."""
+    from oracle import classify_oracle, oracle_lib, select_oracle
+    import ctypes
+    t0 = time.time()
+    so = oracle_lib.ScreenOracle(db)
+    ix = pipe.index_for(res.selected)
+    parts = []
+    for pi, part in enumerate(ix.parts):
+        hs, pos = part.export()
+        first = ix.part_first[pi]
+        n = len(part.names)
+        parts.append(oracle_lib.mm_index_from_arrays(hs, pos, ix.lens[first:first + n], ix.names[first:first + n]))
+    opt = oracle_lib.asm10_opt()
+    opt.mid_occ = pipe.opt.mid_occ
+    log(f"cpu baseline setup {time.time()-t0:.1f}s")
+    qs = pq.queries
+    order = np.random.default_rng(7).permutation(qs.n)
+    sample, t_used = [], 0.0
+    done_bases = 0
+    t_start = time.perf_counter()
+    tsv_rows = 0
+    batch = []
+    for qi in order:
+        batch.append(int(qi))
+        if len(batch) < 8:
+            continue
+        seqs = [(qs.names[i], qs.seq(i)) for i in batch]
+        so.run([s for _, s in seqs])                                  # screen
+        paf = []
+        for p in parts:                                               # map, part-major
+            for name, s in seqs:
+                regs, rl = oracle_lib.mm_map(p, opt, s, name)
+                paf.extend(oracle_lib.format_paf(name, len(s), regs, rl, p.names, p.lens))
+        fd, path = tempfile.mkstemp(suffix=".paf")
+        os.write(fd, "".join(l + "\n" for l in paf).encode())
+        os.close(fd)
+        tsv_rows += classify_oracle.classify_cami(path, tax, hier).count(b"\r\n") - 1   # classify
+        os.unlink(path)
+        sample.extend(batch)
+        done_bases += sum(len(s) for _, s in seqs)
+        batch = []
+        if time.perf_counter() - t_start > budget_s:
             break
+    dt = time.perf_counter() - t_start
+    return {"value": len(sample) / dt, "unit": "contigs/s", "cores": 1, "kind": "port",
+            "mbp_per_s": done_bases / 1e6 / dt,
+            "sample": f"{len(sample)} random contigs / {done_bases/1e6:.2f} Mbp of the rank-0 pool: oracle screen "
+                      f"(prebuilt table, {db.n_refs} refs) + oracle minimap2 asm10 vs the same {len(ix.parts)} index parts "
+                      f"+ classification_cami restatement, single thread, {dt:.1f}s"}
+
+
+# ------------------------------------------------------------------- screen only
+def bench_screen(args, comm, gpu, torch):
+    from hymet_amd import screen as scr, synth
+    from hymet_amd.msh import SketchDB
+    from hymet_amd.seqio import DevicePool, from_records
+    rng = np.random.default_rng(1)
+    w = synth.make_cami(rng, n_taxa=10, per_taxon=3, genome_mbp=(2.0, 4.0), contig_gbp=0.0538,
+                        contig_rng=np.random.default_rng(11 + comm.rank))
+    refs_ss = from_records([(n, "", s) for n, s in zip(w.ref_names, w.refs)])
+    sk = scr.sketch_sequences(gpu, DevicePool(gpu, refs_ss, DevicePool.ALPHA_MASH), 21, 42, 1000)
+    dec = synth.decoy_sketches(rng, max(0, args.screen_refs - len(sk)), 1000)
+    hl = sk + list(dec)
+    off = np.zeros(len(hl) + 1, np.int64)
+    off[1:] = np.cumsum([len(h) for h in hl])
+    db = SketchDB(names=[f"r{i}" for i in range(len(hl))], comments=[""] * len(hl), lengths=np.ones(len(hl), np.int64),
+                  offsets=off, hashes=np.concatenate(hl))
+    ss = from_records([(n, "", s) for n, s in zip(w.contig_names, w.contigs)])
+    pool = DevicePool(gpu, ss, DevicePool.ALPHA_MASH)
+    table = scr.ScreenTable(gpu, db)
+    for _ in range(args.warmup):
+        scr.screen(gpu, pool, [db], [table], comm)
+    gpu.prof_reset()
+    gpu.prof(True)
+    torch.cuda.synchronize()
+    comm.barrier()
     t0 = time.perf_counter()
-    oracle_lib.screen(sub, db.k, db.seed, db.sketch_size, [db.ref_hashes(i) for i in range(min(db.n_refs, 20000))])
-    dt = time.perf_counter() - t0
-    return {"value": len(sub) / dt, "unit": "contigs/s", "cores": 1, "kind": "port",
-            "sample": f"{len(sub)} contigs / {tot/1e6:.1f} Mbp vs 20000 refs, oracle/mash_oracle.c single thread",
-            "mbp_per_s": tot / 1e6 / dt}
+    for _ in range(args.steps):
+        scr.screen(gpu, pool, [db], [table], comm)
+    torch.cuda.synchronize()
+    comm.barrier()
+    dt = comm.max_float(time.perf_counter() - t0)
+    gpu.prof(False)
+    prof = gpu.prof_table()
+    step = dt / args.steps
+    return {"metric": "contigs/s screened (C2 Zymo-shaped pool vs sketch1-sized DB)", "value": comm.world * ss.n / step,
+            "unit": "contigs/s", "n_gpus": comm.world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": step * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "mbp_per_s": comm.world * ss.total_bases / 1e6 / step,
+            "config": {"workload": f"C2 screen: {ss.n} contigs / {ss.total_bases/1e6:.1f} Mbp vs {db.n_refs} refs x 1000"},
+            "roofline": roofline_from_prof(prof, "screen_count")}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="screen", choices=["screen"])
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="cami-medium", choices=["cami-medium", "screen"])
+    ap.add_argument("--contig-gbp", type=float, default=1.0)
+    ap.add_argument("--taxa", type=int, default=12)
+    ap.add_argument("--per-taxon", type=int, default=62)
+    ap.add_argument("--batch-mbp", type=float, default=40.0)
     ap.add_argument("--screen-refs", type=int, default=100_000)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
     import torch
+    from hymet_amd._lib import Gpu
     from hymet_amd.dist import Comm
     comm = Comm.from_env()
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    from hymet_amd._lib import Gpu
-    gpu = Gpu(local)
+    gpu = Gpu(int(os.environ.get("LOCAL_RANK", "0")))
     comm.init_backend(gpu)
-    res = bench_screen(args, comm, gpu, torch)
+    res = bench_cami(args, comm, gpu, torch) if args.workload == "cami-medium" else bench_screen(args, comm, gpu, torch)
     if comm.rank == 0:
         print(json.dumps(res), flush=True)
     comm.close()

@@ -22,6 +22,10 @@ _SIGS = {
     "hymet_last_error": (_c.c_char_p, []),
     "hymet_set_stream": (_i32, [_vp, _vp]),
     "hymet_sync": (_i32, [_vp]),
+    "hymet_prof_enable": (_i32, [_vp, _i32]),
+    "hymet_prof_reset": (_i32, [_vp]),
+    "hymet_prof_query": (_i32, [_vp, _c.c_char_p, _c.POINTER(_c.c_double), _c.POINTER(_i64), _c.POINTER(_c.c_double)]),
+    "hymet_prof_names": (_i32, [_vp, _c.c_char_p, _i64]),
     "hymet_pack": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "hymet_screen_table_slots": (_i64, [_i64]),
     "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
@@ -104,6 +108,23 @@ class Gpu:
 
     def sync(self):
         check(self.lib.hymet_sync(self.ctx), "hymet_sync")
+
+    def prof(self, on: bool = True):
+        check(self.lib.hymet_prof_enable(self.ctx, int(on)), "hymet_prof_enable")
+
+    def prof_reset(self):
+        check(self.lib.hymet_prof_reset(self.ctx), "hymet_prof_reset")
+
+    def prof_table(self):
+        """{kernel name: (total ms, launches, algorithmic bytes)} since the last reset."""
+        buf = _c.create_string_buffer(1 << 16)
+        check(self.lib.hymet_prof_names(self.ctx, buf, 1 << 16), "hymet_prof_names")
+        out = {}
+        for name in buf.value.decode().split():
+            ms, n, b = _c.c_double(), _i64(), _c.c_double()
+            check(self.lib.hymet_prof_query(self.ctx, name.encode(), _c.byref(ms), _c.byref(n), _c.byref(b)), "hymet_prof_query")
+            out[name] = (ms.value, n.value, b.value)
+        return out
 
     def empty(self, n, dtype):
         return self.torch.empty(int(n), dtype=dtype, device=self.dev)

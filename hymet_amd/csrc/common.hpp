@@ -2,7 +2,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <map>
 #include <string>
+#include <utility>
+#include <vector>
 #include "../../include/hymet_gpu.h"
 
 struct hymet_ctx {
@@ -10,7 +13,32 @@ struct hymet_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int n_cu = 256;
+    // live per-kernel timing (hymet_prof_*): HIP events recorded on `stream` around launches
+    bool prof = false;
+    std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> ev;
+    std::map<std::string, double> bytes;  // algorithmic bytes of the timed launches
 };
+
+namespace hymet {
+// RAII: records a start/stop event pair on the context stream around the enclosed launches
+struct ProfScope {
+    hymet_ctx *c;
+    const char *name;
+    hipEvent_t a = nullptr, b = nullptr;
+    ProfScope(hymet_ctx *ctx, const char *n, double alg_bytes = 0.0) : c(ctx), name(n) {
+        if (c && c->prof && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess) {
+            (void)hipEventRecord(a, c->stream);
+            c->bytes[name] += alg_bytes;
+        }
+    }
+    ~ProfScope() {
+        if (c && c->prof && a && b) {
+            (void)hipEventRecord(b, c->stream);
+            c->ev[name].push_back({a, b});
+        }
+    }
+};
+}  // namespace hymet
 
 namespace hymet {
 void set_error(const std::string &msg);

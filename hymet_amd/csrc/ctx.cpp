@@ -1,6 +1,8 @@
 // Context lifetime and thread-local error strings for the C ABI (include/hymet_gpu.h).
 #include "common.hpp"
 
+#include <cstring>
+
 namespace hymet {
 static thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
@@ -54,6 +56,51 @@ int hymet_set_stream(hymet_ctx *ctx, void *s) {
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     ctx->stream = (hipStream_t)s;
     ctx->own_stream = false;
+    return HYMET_OK;
+}
+
+int hymet_prof_enable(hymet_ctx *ctx, int on) {
+    HY_ARG(ctx != nullptr, "hymet_prof_enable: null ctx");
+    ctx->prof = on != 0;
+    return HYMET_OK;
+}
+
+int hymet_prof_reset(hymet_ctx *ctx) {
+    HY_ARG(ctx != nullptr, "hymet_prof_reset: null ctx");
+    HY_HIP(hipStreamSynchronize(ctx->stream));
+    for (auto &kv : ctx->ev)
+        for (auto &p : kv.second) {
+            (void)hipEventDestroy(p.first);
+            (void)hipEventDestroy(p.second);
+        }
+    ctx->ev.clear();
+    ctx->bytes.clear();
+    return HYMET_OK;
+}
+
+int hymet_prof_query(hymet_ctx *ctx, const char *name, double *total_ms, int64_t *count, double *alg_bytes) {
+    HY_ARG(ctx && name && total_ms && count, "hymet_prof_query: null argument");
+    HY_HIP(hipStreamSynchronize(ctx->stream));
+    *total_ms = 0.0;
+    *count = 0;
+    if (alg_bytes) *alg_bytes = ctx->bytes.count(name) ? ctx->bytes[name] : 0.0;
+    auto it = ctx->ev.find(name);
+    if (it == ctx->ev.end()) return HYMET_OK;
+    for (auto &p : it->second) {
+        float ms = 0.f;
+        HY_HIP(hipEventElapsedTime(&ms, p.first, p.second));
+        *total_ms += ms;
+        (*count)++;
+    }
+    return HYMET_OK;
+}
+
+int hymet_prof_names(hymet_ctx *ctx, char *buf, int64_t cap) {
+    HY_ARG(ctx && buf && cap > 0, "hymet_prof_names: null argument");
+    std::string all;
+    for (auto &kv : ctx->ev) all += kv.first + "\n";
+    if ((int64_t)all.size() + 1 > cap) return hymet::fail(HYMET_E_CAPACITY, "hymet_prof_names: buffer too small");
+    memcpy(buf, all.c_str(), all.size() + 1);
     return HYMET_OK;
 }
 

@@ -174,6 +174,7 @@ int hymet_lca_ref_counts(hymet_ctx *ctx, const int32_t *d_line_t, int64_t n_line
     HY_ARG(ctx && (n_lines == 0 || (d_line_t && d_counts)), "hymet_lca_ref_counts: null argument");
     if (n_lines <= 0) return HYMET_OK;
     HY_HIP(hipSetDevice(ctx->device));
+    hymet::ProfScope _ps(ctx, "lca_refcount");
     hipLaunchKernelGGL(lca_refcount_kernel, dim3((unsigned)hymet::cdiv(n_lines, 256)), dim3(256), 0, ctx->stream, d_line_t,
                        n_lines, d_counts);
     HY_CHECK_LAUNCH("lca_refcount_kernel");
@@ -192,6 +193,7 @@ int hymet_lca(hymet_ctx *ctx, int mode, int32_t n_q, const int64_t *d_q_off, con
     LcaParams P{mode,          n_q,          d_q_off,     d_line_t,    d_line_blen,   d_line_qlen, d_line_exact,
                 d_ref_counts,  d_t_tax,      d_tax_names, d_tax_in_hier, d_scr_tid,   d_scr_w,     d_scr_nm,
                 d_scr_nw,      d_out_depth,  d_out_names, d_out_conf,  d_out_tax};
+    hymet::ProfScope _ps(ctx, "lca");
     hipLaunchKernelGGL(lca_kernel, dim3((unsigned)hymet::cdiv(n_q, 64)), dim3(64), 0, ctx->stream, P);
     HY_CHECK_LAUNCH("lca_kernel");
     return HYMET_OK;

@@ -336,7 +336,7 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
 
 int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *g_start, const int32_t *order,
                  int32_t n_work, int32_t *f, int64_t *p, int32_t *t_global, int max_dist, int max_dist_inner, int bw,
-                 int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip) {
+                 int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip, int64_t n_anchors) {
     if (n_work <= 0) return HYMET_OK;
     DevBuf cnt;
     HY_HIP(cnt.alloc(4, ctx->stream));
@@ -349,6 +349,7 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
     int64_t blocks = cdiv(n_work, kWavesPerBlock);
     const int64_t cap = (int64_t)ctx->n_cu * 6;
     if (blocks > cap) blocks = cap;
+    ProfScope _ps(ctx, "mm_chain", 28.0 * (double)n_anchors);  // x,y read + f,p write per anchor
     hipLaunchKernelGGL(chain_groups_kernel, dim3((unsigned)blocks), dim3(64 * kWavesPerBlock), lds, ctx->stream, P);
     HY_CHECK_LAUNCH("chain_groups_kernel");
     return HYMET_OK;
@@ -360,6 +361,7 @@ int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, c
     if (n_groups <= 0) return HYMET_OK;
     BacktrackParams P{g_start, f, p, t, z_off, z_idx, n_groups, min_cnt, min_sc, max_drop, chain_ids, chain_u, chain_first,
                       n_chains};
+    ProfScope _ps(ctx, "mm_backtrack");
     hipLaunchKernelGGL(backtrack_groups_kernel, dim3((unsigned)cdiv(n_groups, 64)), dim3(64), 0, ctx->stream, P);
     HY_CHECK_LAUNCH("backtrack_groups_kernel");
     return HYMET_OK;

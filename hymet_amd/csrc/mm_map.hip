@@ -30,7 +30,7 @@ namespace mm {
 
 int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *g_start, const int32_t *order,
                  int32_t n_work, int32_t *f, int64_t *p, int32_t *t_global, int max_dist, int max_dist_inner, int bw,
-                 int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip);
+                 int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip, int64_t n_anchors);
 int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, const int64_t *p, int32_t *t,
                      const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, int min_cnt, int min_sc,
                      int max_drop, int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first, int32_t *n_chains);
@@ -376,6 +376,7 @@ __global__ void count_per_query_kernel(const uint32_t *cq, int64_t n, int n_q, i
 template <typename K, typename V>
 static int sort_pairs(hymet_ctx *ctx, K *&keys, K *&keys_alt, V *&vals, V *&vals_alt, int64_t n, int begin_bit, int end_bit) {
     if (n <= 1) return HYMET_OK;
+    ProfScope _ps(ctx, "radix_sort", 2.0 * (double)n * (sizeof(K) + sizeof(V)) * (double)((end_bit - begin_bit + 7) / 8));
     size_t tmp = 0;
     HY_HIP(rocprim::radix_sort_pairs(nullptr, tmp, keys, keys_alt, vals, vals_alt, (size_t)n, begin_bit, end_bit, ctx->stream));
     DevBuf t;
@@ -501,7 +502,7 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(hipMemsetAsync(t.p, 0xFF, 4 * (size_t)n, ctx->stream));
         rc = launch_chain(ctx, A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), g_start.as<int64_t>(), (const int32_t *)vp,
                           (int32_t)n_work, f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(), opt->max_gap,
-                          opt->rmq_inner_dist, bw, opt->max_chain_skip, opt->rmq_size_cap, pen_gap, pen_skip);
+                          opt->rmq_inner_dist, bw, opt->max_chain_skip, opt->rmq_size_cap, pen_gap, pen_skip, n);
         if (rc) return rc;
         // z = anchors with f >= min_sc ordered by (group, f, idx)
         DevBuf zflag, zpos;
@@ -758,6 +759,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
         SeedParams P{mx.as<uint64_t>(), my.as<uint64_t>(), qm_off.as<int64_t>(), d_qlen.as<int64_t>(), idx->d_koff,
                      idx->n_buckets, n_q, opt->mid_occ, opt->max_max_occ, opt->occ_dist, seed_n.as<uint32_t>(),
                      rep_len.as<int32_t>()};
+        ProfScope _ps(ctx, "mm_seed_select");
         hipLaunchKernelGGL(seed_select_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P);
         HY_CHECK_LAUNCH("seed_select_kernel");
     }
@@ -797,6 +799,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
         AnchorParams P{mx.as<uint64_t>(), my.as<uint64_t>(), seed_n.as<uint32_t>(), a_pos.as<int64_t>(), qid.as<uint32_t>(),
                        d_qlen.as<int64_t>(), idx->d_koff, idx->d_pos, M, rb, x.as<uint64_t>(), y.as<uint64_t>(),
                        k1.as<uint64_t>(), k2.as<uint64_t>(), val.as<uint32_t>(), mp_pos.as<int64_t>(), mini_pos.as<uint64_t>()};
+        ProfScope _ps(ctx, "mm_anchors", (double)A * (8.0 + 36.0));  // position fetch + anchor/key writes
         LAUNCH1(write_anchors_kernel, M, P);
         // ------------------------------------------------------- 5 sort
         rc = sort_anchor_set(ctx, x, y, k1, k2, val, A, key1_bits, S1);

@@ -317,6 +317,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
     RegParams P{bx, by, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
                 tmp, n_regs};
+    ProfScope _ps(ctx, "mm_regions");
     hipLaunchKernelGGL(regions_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, ctx->stream, P);
     HY_CHECK_LAUNCH("regions_kernel");
     return HYMET_OK;

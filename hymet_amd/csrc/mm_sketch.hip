@@ -143,6 +143,7 @@ __global__ void occ_hist_kernel(const uint32_t *__restrict__ koff, int64_t n_buc
 
 int launch_sketch(hymet_ctx *ctx, int w, bool write, const SketchParams &P) {
     if (P.n_chunks <= 0) return HYMET_OK;
+    ProfScope _ps(ctx, write ? "mm_sketch_write" : "mm_sketch_count", (double)P.n_chunks * (kChunk * 0.375 + 4.0));
     const dim3 grid((unsigned)cdiv(P.n_chunks, 256)), block(256);
     switch (w) {
 #define HY_W(WW)                                                                                   \

@@ -247,6 +247,7 @@ int launch_count(hymet_ctx *ctx, const CountParams &P, int64_t n_tiles) {
     const int64_t cap = (int64_t)ctx->n_cu * 16;
     if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
+    hymet::ProfScope _ps(ctx, "screen_count", (double)(P.pos_end - P.pos_begin) * (0.375 + 8.0 * P.ndb));
     hipLaunchKernelGGL(screen_count_kernel<K>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, P);
     HY_CHECK_LAUNCH("screen_count_kernel");
     return HYMET_OK;
@@ -277,6 +278,7 @@ int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n
     HY_HIP(hipMemsetAsync(d_keys, 0xFF, (size_t)n_slots * 8, ctx->stream));
     if (n <= 0) return HYMET_OK;
     const int lg = log2_exact(n_slots);
+    hymet::ProfScope _ps(ctx, "screen_table_build");
     hipLaunchKernelGGL(table_insert_kernel, dim3((unsigned)hymet::cdiv(n, 256)), dim3(256), 0, ctx->stream, d_hashes, n,
                        (unsigned long long *)d_keys, (uint64_t)(n_slots - 1), 64 - lg, n_slots, d_slot_of);
     HY_CHECK_LAUNCH("table_insert_kernel");
@@ -334,6 +336,7 @@ int hymet_screen_stats(hymet_ctx *ctx, const int64_t *d_ref_off, int64_t n_refs,
     if (n_refs <= 0) return HYMET_OK;
     HY_ARG(n_refs < (1ll << 31), "hymet_screen_stats: too many references");
     HY_HIP(hipSetDevice(ctx->device));
+    hymet::ProfScope _ps(ctx, "screen_stats");  // O(H) gather, bytes not modelled
     hipLaunchKernelGGL(screen_stats_kernel, dim3((unsigned)n_refs), dim3(256), 0, ctx->stream, d_ref_off, d_slot_of,
                        d_counts, d_shared, d_median);
     HY_CHECK_LAUNCH("screen_stats_kernel");

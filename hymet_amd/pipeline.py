@@ -32,6 +32,7 @@ class Config:
     cand_max: int = 5000              # CAND_MAX (run_hymet_cami.sh:26)
     dedupe: bool = False              # SPECIES_DEDUP
     split_idx: str = "2g"             # SPLIT_IDX / minimap2 -I
+    index_mini_batch: float = 50e6    # minimap2 indexing mini-batch (bseq reader chunk)
     w: int = 10                       # minimap2 -d defaults
     k: int = 15
     map_batch_bases: int = 40_000_000  # query bases per device mapping batch (HBM budget)
@@ -91,7 +92,7 @@ class Pipeline:
         if key in self.index_cache:
             return self.index_cache[key]
         refs: SeqSet = self.ref_lookup(selected)
-        parts_idx = mp.split_parts(refs.lengths, float(mp.parse_num(self.cfg.split_idx)))
+        parts_idx = mp.split_parts(refs.lengths, float(mp.parse_num(self.cfg.split_idx)), self.cfg.index_mini_batch)
         parts, first = [], []
         for p in parts_idx:
             sub = refs.subset(p) if len(parts_idx) > 1 else refs
@@ -101,20 +102,25 @@ class Pipeline:
         self.index_cache = {key: ix}  # one cached candidate set, like the sha1 cache dir
         return ix
 
-    def map_all(self, ix: IndexSet, queries: SeqSet, qpool: Optional[DevicePool] = None):
+    def prepare(self, queries: SeqSet) -> "Prepared":
+        """Make the query set resident in HBM: one Mash-alphabet pool for the screen and
+        minimap2-alphabet pools cut into mapping batches (sized for the anchor working set)."""
+        pq = Prepared(queries, DevicePool(self.gpu, queries, DevicePool.ALPHA_MASH), [])
+        for b0, b1 in _batches(queries.lengths, self.cfg.map_batch_bases):
+            sub = queries if (b0 == 0 and b1 == queries.n) else queries.subset(range(b0, b1))
+            names_hash = np.array([mp.x31_hash(n) for n in sub.names], np.uint32)
+            pq.batches.append((b0, DevicePool(self.gpu, sub, DevicePool.ALPHA_MINIMAP2), names_hash))
+        return pq
+
+    def map_all(self, ix: IndexSet, pq: "Prepared"):
         """Per part, per query batch -> list of (part, query offset, MapResult)."""
         if self.opt is None:
             self.opt = mp.MapOpt.asm10()
             self.opt.resolve_mid_occ(ix.parts[0])   # mm_mapopt_update: first part fixes mid_occ
-        batches = _batches(queries.lengths, self.cfg.map_batch_bases)
         out = []
         for pi, part in enumerate(ix.parts):
-            for b0, b1 in batches:
-                if qpool is not None and len(batches) == 1:
-                    qp = qpool
-                else:
-                    qp = DevicePool(self.gpu, queries.subset(range(b0, b1)), DevicePool.ALPHA_MINIMAP2)
-                out.append((pi, b0, mp.map_part(self.gpu, part, qp, self.opt)))
+            for b0, qp, nh in pq.batches:
+                out.append((pi, b0, mp.map_part(self.gpu, part, qp, self.opt, nh)))
         return out
 
     def paf_table(self, ix: IndexSet, queries: SeqSet, results, with_text=False):
@@ -153,19 +159,27 @@ class Pipeline:
         return table, text
 
     # ------------------------------------------------------------------- run
-    def run(self, queries: SeqSet, qpool_mash: DevicePool = None, qpool_mm: DevicePool = None, with_paf=False) -> RunResult:
-        gpu = self.gpu
-        qpool_mash = qpool_mash or DevicePool(gpu, queries, DevicePool.ALPHA_MASH)
-        selected, rows, thr = self.screen_select(qpool_mash)
+    def run(self, queries, with_paf=False) -> RunResult:
+        """queries: a SeqSet, or a Prepared (already resident in HBM)."""
+        pq = queries if isinstance(queries, Prepared) else self.prepare(queries)
+        queries = pq.queries
+        selected, rows, thr = self.screen_select(pq.mash_pool)
         if not selected:
             raise RuntimeError("candidate list empty after applying limit")  # run_hymet_cami.sh:126
         ix = self.index_for(selected)
-        results = self.map_all(ix, queries, qpool_mm)
+        results = self.map_all(ix, pq)
         table, text = self.paf_table(ix, queries, results, with_paf)
         res = self.classifier.run(table, comm=self.comm)
         rws = self.classifier.rows(res)
         tsv = self.classifier.tsv_bytes(res)
         return RunResult(selected, rows, thr, tsv, len(rws), sum(1 for r in rws if r[1] != "Unknown"), table.n_lines, text)
+
+
+@dataclass
+class Prepared:
+    queries: SeqSet
+    mash_pool: DevicePool
+    batches: list
 
 
 def _batches(lengths: np.ndarray, max_bases: int):

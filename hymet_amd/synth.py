@@ -84,7 +84,8 @@ class Workload:
 
 
 def make_cami(rng, n_taxa=12, per_taxon=62, genome_mbp=(3.0, 5.0), div=(0.005, 0.04), contig_gbp=1.0,
-              max_contigs=None, name="cami-medium") -> Workload:
+              max_contigs=None, name="cami-medium", contig_rng=None) -> Workload:
+    """contig_rng: separate generator for the contigs (per-rank samples of one community)."""
     taxa = [f"Species{chr(65 + t)} synthetica" for t in range(n_taxa)]
     ref_names, ref_taxon, ref_strain, refs = [], [], [], []
     sample = []
@@ -102,6 +103,7 @@ def make_cami(rng, n_taxa=12, per_taxon=62, genome_mbp=(3.0, 5.0), div=(0.005, 0
             ref_strain.append(s)
             refs.append(to_ascii(g))
     # contigs: lognormal(ln 4000, 1.0) in [1 kbp, 1 Mbp] until contig_gbp
+    rng = contig_rng if contig_rng is not None else rng
     cn, cs, ct = [], [], []
     total, target = 0, int(contig_gbp * 1e9)
     i = 0

@@ -43,6 +43,15 @@ const char *hymet_last_error(void);
 int hymet_set_stream(hymet_ctx *ctx, void *hip_stream);
 int hymet_sync(hymet_ctx *ctx);
 int hymet_version(void);
+/* Live kernel timing: while enabled, HIP events are recorded on the context stream around
+ * every hot-path kernel launch; query returns the summed elapsed ms, the launch count and
+ * the summed ALGORITHMIC bytes for a kernel name; bench.py reports
+ * the dominant kernel's roofline from these. */
+int hymet_prof_enable(hymet_ctx *ctx, int on);
+int hymet_prof_reset(hymet_ctx *ctx);
+int hymet_prof_query(hymet_ctx *ctx, const char *name, double *total_ms, int64_t *count, double *alg_bytes);
+/* newline-separated names of every timed kernel */
+int hymet_prof_names(hymet_ctx *ctx, char *buf, int64_t cap);
 
 /* ------------------------------------------------------- sequence packing
  * ASCII bases (device) -> 2-bit codes (16 bases per uint32, base i at bits 2*(i%16)) and an

@@ -87,6 +87,10 @@ static inline uint64_t omap_slot(const omap_t *m, uint64_t k) {
 }
 
 int cmp64(const void *a, const void *b);
+static int cmpu32o(const void *a, const void *b) {
+    uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+    return x < y ? -1 : x > y;
+}
 
 /* bottom-s distinct set: a buffer of candidates below the current cut, compacted
  * (sort + unique + truncate to s) whenever it fills. */
@@ -111,19 +115,36 @@ static const char *ORACLE_ACGT = "ACGT";
  *   seq/seq_off/nseq : concatenated ASCII query sequences (pool of all input files)
  *   ref_hashes/ref_off/nrefs : each reference's sorted hash list (CSR)
  * Outputs per reference: shared[i], median[i]; *set_size = pool set-size estimate.
- * Returns 0 on success, -1 for unsupported parameters. */
-int oracle_screen(const char *seq, const int64_t *seq_off, int64_t nseq, int k, uint32_t seed,
-                  int preserve_case, int64_t sketch_size,
-                  const uint64_t *ref_hashes, const int64_t *ref_off, int64_t nrefs,
-                  uint32_t *shared, uint32_t *median, uint64_t *set_size, uint64_t *n_kmers) {
-    if (k < 17 || k > 32) return -1;
+ * oracle_screen_prepare builds the hash -> count table once (Mash builds it per run);
+ * oracle_screen_run hashes a pool against it.  Returns 0, or -1 for unsupported k. */
+typedef struct { omap_t tab; const uint64_t *ref_hashes; const int64_t *ref_off; int64_t nrefs; } oscreen_t;
+
+void *oracle_screen_prepare(const uint64_t *ref_hashes, const int64_t *ref_off, int64_t nrefs) {
+    oscreen_t *o = (oscreen_t *)calloc(1, sizeof(oscreen_t));
     int64_t H = ref_off[nrefs];
-    omap_t tab;
-    omap_init(&tab, (uint64_t)H);
+    omap_init(&o->tab, (uint64_t)H);
     for (int64_t i = 0; i < H; i++) {
-        uint64_t s = omap_slot(&tab, ref_hashes[i]);
-        tab.used[s] = 1; tab.key[s] = ref_hashes[i]; tab.val[s] = 0;
+        uint64_t s = omap_slot(&o->tab, ref_hashes[i]);
+        o->tab.used[s] = 1; o->tab.key[s] = ref_hashes[i]; o->tab.val[s] = 0;
     }
+    o->ref_hashes = ref_hashes; o->ref_off = ref_off; o->nrefs = nrefs;
+    return o;
+}
+
+void oracle_screen_free(void *h) {
+    oscreen_t *o = (oscreen_t *)h;
+    if (!o) return;
+    omap_free(&o->tab);
+    free(o);
+}
+
+int oracle_screen_run(void *h, const char *seq, const int64_t *seq_off, int64_t nseq, int k, uint32_t seed,
+                      int preserve_case, int64_t sketch_size, uint32_t *shared, uint32_t *median, uint64_t *set_size,
+                      uint64_t *n_kmers) {
+    oscreen_t *o = (oscreen_t *)h;
+    if (k < 17 || k > 32) return -1;
+    omap_t *tab = &o->tab;
+    for (uint64_t i = 0; i <= tab->mask; i++) tab->val[i] = 0;
     bottom_t bt;
     bt.s = sketch_size; bt.cap = 8 * sketch_size + 64; bt.n = 0; bt.full = 0; bt.cut = 0;
     bt.b = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)bt.cap);
@@ -153,11 +174,11 @@ int oracle_screen(const char *seq, const int64_t *seq_off, int64_t nseq, int k, 
             if (!good) continue;
             const char *fw = up + j, *rv = rc + (L - j - k);
             const char *km = memcmp(rv, fw, (size_t)k) < 0 ? rv : fw;
-            uint64_t h = oracle_murmur3_x64_128_h0((const uint8_t *)km, k, seed);
+            uint64_t hh = oracle_murmur3_x64_128_h0((const uint8_t *)km, k, seed);
             nk++;
-            bottom_offer(&bt, h);
-            uint64_t s = omap_slot(&tab, h);
-            if (tab.used[s]) tab.val[s]++;
+            bottom_offer(&bt, hh);
+            uint64_t s = omap_slot(tab, hh);
+            if (tab->used[s]) tab->val[s]++;
         }
     }
     free(up); free(rc);
@@ -167,22 +188,32 @@ int oracle_screen(const char *seq, const int64_t *seq_off, int64_t nseq, int k, 
     else *set_size = (uint64_t)(18446744073709551616.0 * (double)bt.n / (double)bt.b[bt.n - 1]);
     uint32_t *dep = NULL;
     int64_t depcap = 0;
-    for (int64_t r = 0; r < nrefs; r++) {
-        int64_t n = ref_off[r + 1] - ref_off[r];
+    for (int64_t r = 0; r < o->nrefs; r++) {
+        int64_t n = o->ref_off[r + 1] - o->ref_off[r];
         if (n > depcap) { depcap = n; dep = (uint32_t *)realloc(dep, 4 * n); }
         int64_t m = 0;
         for (int64_t i = 0; i < n; i++) {
-            uint32_t c = tab.val[omap_slot(&tab, ref_hashes[ref_off[r] + i])];
+            uint32_t c = tab->val[omap_slot(tab, o->ref_hashes[o->ref_off[r] + i])];
             if (c > 0) dep[m++] = c;
         }
-        /* insertion-free median: counting sort would be overkill; qsort */
-        for (int64_t a = 1; a < m; a++) { uint32_t v = dep[a]; int64_t b = a; while (b > 0 && dep[b - 1] > v) { dep[b] = dep[b - 1]; b--; } dep[b] = v; }
+        qsort(dep, (size_t)m, 4, cmpu32o);
         shared[r] = (uint32_t)m;
         median[r] = m > 0 ? dep[m / 2] : 0;
     }
     free(dep);
-    free(bt.b); omap_free(&tab);
+    free(bt.b);
     return 0;
+}
+
+int oracle_screen(const char *seq, const int64_t *seq_off, int64_t nseq, int k, uint32_t seed,
+                  int preserve_case, int64_t sketch_size,
+                  const uint64_t *ref_hashes, const int64_t *ref_off, int64_t nrefs,
+                  uint32_t *shared, uint32_t *median, uint64_t *set_size, uint64_t *n_kmers) {
+    if (k < 17 || k > 32) return -1;
+    void *h = oracle_screen_prepare(ref_hashes, ref_off, nrefs);
+    int rc = oracle_screen_run(h, seq, seq_off, nseq, k, seed, preserve_case, sketch_size, shared, median, set_size, n_kmers);
+    oracle_screen_free(h);
+    return rc;
 }
 
 /* Mash `sketch` restatement (used to build synthetic .msh DBs in tests/bench): the

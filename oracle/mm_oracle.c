@@ -209,6 +209,24 @@ mmo_idx_t *mmo_idx_build(const char *buf, const int64_t *starts, const int64_t *
     return mi;
 }
 
+/* an index from already sorted (key, positions) arrays -- e.g. exported by the device
+ * index after tests/test_mm_index_gpu.py proved the two identical -- so that a CPU
+ * baseline need not re-sketch gigabases of references single-threaded */
+mmo_idx_t *mmo_idx_from_arrays(const uint64_t *keys, const int64_t *koff, int64_t n_keys, const uint64_t *pos,
+                               const int64_t *lens, int n_seq, int w, int k) {
+    mmo_idx_t *mi = (mmo_idx_t *)calloc(1, sizeof(mmo_idx_t));
+    mi->w = w, mi->k = k, mi->n_seq = n_seq, mi->n_keys = n_keys;
+    mi->len = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n_seq + 1));
+    memcpy(mi->len, lens, sizeof(int64_t) * (size_t)n_seq);
+    mi->keys = (uint64_t *)malloc(8 * (size_t)(n_keys + 1));
+    mi->koff = (int64_t *)malloc(8 * (size_t)(n_keys + 1));
+    mi->pos = (uint64_t *)malloc(8 * (size_t)(koff[n_keys] + 1));
+    memcpy(mi->keys, keys, 8 * (size_t)n_keys);
+    memcpy(mi->koff, koff, 8 * (size_t)(n_keys + 1));
+    memcpy(mi->pos, pos, 8 * (size_t)koff[n_keys]);
+    return mi;
+}
+
 void mmo_idx_destroy(mmo_idx_t *mi) {
     if (!mi) return;
     free(mi->len); free(mi->keys); free(mi->koff); free(mi->pos); free(mi);

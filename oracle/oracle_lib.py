@@ -216,3 +216,56 @@ def format_paf(qname, qlen, regs, rep_len, tnames, tlens):
         line += f"\trl:i:{rep_len}"
         out.append(line)
     return out
+
+
+class ScreenOracle:
+    """oracle_screen_prepare / _run: the hash table built once for repeated runs."""
+
+    def __init__(self, db):
+        L = lib()
+        L.oracle_screen_prepare.restype = ctypes.c_void_p
+        L.oracle_screen_prepare.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+        L.oracle_screen_free.argtypes = [ctypes.c_void_p]
+        L.oracle_screen_run.restype = ctypes.c_int
+        L.oracle_screen_run.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                        ctypes.c_uint32, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p]
+        self.db = db
+        self.h_hashes = np.ascontiguousarray(db.hashes, dtype=np.uint64)
+        self.h_off = np.ascontiguousarray(db.offsets, dtype=np.int64)
+        self.h = L.oracle_screen_prepare(_p(self.h_hashes), _p(self.h_off), db.n_refs)
+
+    def run(self, seqs):
+        buf, off = concat(seqs)
+        n = self.db.n_refs
+        sh = np.zeros(n, np.uint32)
+        md = np.zeros(n, np.uint32)
+        ss, nk = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = lib().oracle_screen_run(self.h, ctypes.c_char_p(buf), _p(off), len(seqs), self.db.k, self.db.seed, 0,
+                                     self.db.sketch_size, _p(sh), _p(md), ctypes.byref(ss), ctypes.byref(nk))
+        assert rc == 0
+        return sh, md, ss.value, nk.value
+
+    def __del__(self):
+        try:
+            lib().oracle_screen_free(self.h)
+        except Exception:
+            pass
+
+
+def mm_index_from_arrays(hashes_sorted: np.ndarray, pos: np.ndarray, lens, names, w=10, k=15):
+    """Build the oracle's index structure from sorted (hash, pos) arrays."""
+    L = _mm_lib()
+    L.mmo_idx_from_arrays.restype = ctypes.c_void_p
+    L.mmo_idx_from_arrays.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    h = np.asarray(hashes_sorted)
+    starts = np.flatnonzero(np.r_[True, h[1:] != h[:-1]]) if len(h) else np.zeros(0, np.int64)
+    keys = np.ascontiguousarray(h[starts].astype(np.uint64))
+    koff = np.ascontiguousarray(np.r_[starts, len(h)].astype(np.int64))
+    pos = np.ascontiguousarray(pos, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.int64)
+    idx = MmIndex.__new__(MmIndex)
+    idx.names, idx.lens, idx.w, idx.k = list(names), lens, w, k
+    idx.h = L.mmo_idx_from_arrays(_p(keys), _p(koff), len(keys), _p(pos), _p(lens), len(lens), w, k)
+    return idx

@@ -64,10 +64,10 @@ def split_parts(lengths, batch=2e9, mini=50e6):
     return parts
 
 
-def map_paf(ref_names, ref_seqs, queries, part_bases=2e9):
+def map_paf(ref_names, ref_seqs, queries, part_bases=2e9, mini_batch=50e6):
     """minimap2 -I<part_bases> -d ; minimap2 -x asm10 : PAF lines in minimap2's order."""
     lens = [len(s) for s in ref_seqs]
-    parts = split_parts(lens, part_bases)
+    parts = split_parts(lens, part_bases, mini_batch)
     out = []
     opt = None
     for p in parts:
@@ -81,11 +81,11 @@ def map_paf(ref_names, ref_seqs, queries, part_bases=2e9):
     return out
 
 
-def run(queries, dbs, ref_lookup, taxonomy, hierarchy, thresh="0.9", cand_max=5000, part_bases=2e9):
+def run(queries, dbs, ref_lookup, taxonomy, hierarchy, thresh="0.9", cand_max=5000, part_bases=2e9, mini_batch=50e6):
     """queries: list of (name, seq bytes).  Returns (selected, paf lines, tsv bytes)."""
     selected, _ = select([q[1] for q in queries], dbs, thresh, cand_max)
     names, seqs = ref_lookup(selected)
-    paf = map_paf(names, seqs, queries, part_bases)
+    paf = map_paf(names, seqs, queries, part_bases, mini_batch)
     with tempfile.TemporaryDirectory() as td:
         p = os.path.join(td, "resultados.paf")
         with open(p, "w") as f:

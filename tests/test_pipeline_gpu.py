@@ -42,7 +42,7 @@ def test_pipeline_matches_oracle(gpu, tmp_path):
     from oracle import oracle_lib, pipeline_oracle
     w, db, by_name, tax, hier = _setup(gpu, tmp_path)
     # small -I so that the candidate set spans two index parts (mid_occ from part 1)
-    cfg = pipeline.Config(split_idx="2m", map_batch_bases=300_000)
+    cfg = pipeline.Config(split_idx="2m", index_mini_batch=1e6, map_batch_bases=300_000)
 
     def ref_lookup(names):
         return from_records([(by_name[n][0], "", by_name[n][1]) for n in names])
@@ -52,7 +52,8 @@ def test_pipeline_matches_oracle(gpu, tmp_path):
     res = p.run(queries, with_paf=True)
     o_sel, o_paf, o_tsv = pipeline_oracle.run(list(zip(w.contig_names, w.contigs)), [db],
                                               lambda names: ([by_name[n][0] for n in names], [by_name[n][1] for n in names]),
-                                              tax, hier, part_bases=2e6)
+                                              tax, hier, part_bases=2e6, mini_batch=1e6)
+    assert len(p.index_for(res.selected).parts) >= 2
     assert res.selected == o_sel
     assert len(o_sel) == 12
     assert res.paf == o_paf
