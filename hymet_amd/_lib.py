@@ -42,6 +42,7 @@ _SIGS = {
     "hymet_mm_result_size": (_i32, [_vp, _c.POINTER(_i64)]),
     "hymet_mm_result_copy": (_i32, [_vp, _vp, _vp, _vp]),
     "hymet_mm_result_destroy": (_i32, [_vp]),
+    "hymet_mm_chain_dp": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _c.c_float, _c.c_float, _vp, _vp]),
     "hymet_lca_ref_counts": (_i32, [_vp, _vp, _i64, _vp]),
     "hymet_lca": (_i32, [_vp, _i32, _i32] + [_vp] * 17),
 }

@@ -1,22 +1,40 @@
 // Collinear chaining of anchors (minimap2 lchain.c mg_lchain_rmq + mg_chain_backtrack, as
 // driven by `-x asm10`: --rmq, -r1k,100k, -g10k).
 //
-// chain_groups_kernel: one WAVE per (query, strand, target) group -- mg_lchain_rmq never
-// chains across a change of x>>32, so groups are independent.  Groups are pulled from a
-// size-descending work list with one atomic per group (biggest first, no tail of giants).
-// Per anchor i the wave
-//   * slides the outer window [st, i0) (x within max_dist) and the inner window
-//     [st_in, i0) (x within max_dist_inner); the inner window is also kept as a (y, idx)
-//     sorted list in LDS (the krmq inner tree's in-order sequence), plus an LDS ring of
-//     "visited in this iteration" stamps (the t[] array restricted to the window, which is
-//     the only part of t[] the skip heuristic ever reads);
-//   * RMQ: every lane scans a strided slice of the outer window for the minimum priority
-//     -(f_j + 0.5*gap*(x_j+y_j)) with y_j in the krmq closed interval
-//     [(y_i-max_dist, INT32_MAX), (y_i, 0)], then a wave min-reduction (ties -> larger j:
-//     canonical tie-break T2);
-//   * if the RMQ winner is not an exact extension, walks the inner list downwards in
-//     chunks of 64: candidate scores are computed lane-parallel, the order-dependent
-//     n_skip / t[] logic is resolved in program order.
+// chain_groups_kernel: one WAVE (= one block) per (query, strand, target) group --
+// mg_lchain_rmq never chains across a change of x>>32, so groups are independent.  Groups
+// are pulled from a size-descending work list with one atomic per group (biggest first).
+// The DP is sequential along the group, so the kernel is latency-bound: it keeps the
+// per-anchor chain of dependent operations short (register-cached deque ends, lane-parallel
+// probes, DPP/permlane reductions, no LDS round trip where a register will do) and the LDS
+// footprint small (~15 KB) so that ~10 groups run per CU.
+//   * anchors are fetched 64 at a time with one coalesced load (double buffered) and handed
+//     out with lane shuffles; the last kRing anchors sit in an LDS ring as one int4
+//     (x, y, f, (p+1) | span<<24);
+//   * RMQ window = anchors [st, i0) (x within max_dist: 10 kbp on the first pass, bw_long =
+//     100 kbp on the long-join re-chain, ~18k anchors), cut into blocks of 64.  Every
+//     complete block gets a summary: its argmin priority -(f_j + 0.5*gap*(x_j+y_j)) (ties ->
+//     larger index, canonical T2), the y of that argmin and the block's y range; a monotone
+//     deque over the summaries gives the best complete block of the window in O(1), and the
+//     head block (partial, oldest) is cached with its suffix argmins.
+//     FAST PATH: scan the newest 64 window entries with the krmq range test
+//     [(y_i-max_dist, INT32_MAX), (y_i, 0)] and reduce; if neither the deque front nor the
+//     head suffix beats that candidate -- ignoring y, so a fortiori with it -- it is the
+//     exact RMQ answer.  On colinear chains the newest anchors carry the best priority.
+//     FULL PATH: take the summary of every block whose y range meets the query and whose
+//     argmin lies inside it (then it is the argmin of the block's in-range subset), scan
+//     entries of the partial head/tail blocks and of blocks whose argmin is out of range;
+//   * the inner window (x within rmq_inner_dist) is a (y, idx) sorted ring-deque in LDS (the
+//     krmq inner tree's in-order sequence; colinear inserts append, colinear erases pop the
+//     front) plus an LDS ring of "visited in this iteration" stamps (the t[] array
+//     restricted to the window, the only part the skip heuristic reads).  A candidate of the
+//     inner walk scores at most f_j + span_j, so when a monotone max-deque over the window
+//     says max(f_j + span_j) <= max_f the walk cannot change max_f/max_j and is skipped.
+//     Otherwise the walk is evaluated 64 candidates at a time: scores lane-parallel, the
+//     running max by a prefix-max scan, t[] marks by one LDS write round (a mark always
+//     points to a later candidate in walk order), and the saturating n_skip counter by a
+//     prefix scan of max-plus maps -- the same decisions as the sequential loop, including
+//     where it breaks.
 // All floating point follows lchain.c exactly (float mg_log2 / penalty, double priority;
 // built with -ffp-contract=off).
 //
@@ -28,19 +46,54 @@ namespace hymet {
 namespace mm {
 namespace {
 
-constexpr int kInnerCap = 1024;  // LDS inner-window capacity per wave (entries)
-constexpr int kWavesPerBlock = 4;
+constexpr int kRing = 256;      // LDS ring of recent anchors, int4 each: 4 KB
+constexpr int kRingMask = kRing - 1;
+constexpr int kStair = 4;       // staircase entries kept per block summary
+constexpr int kSumInts = kStair + 1;  // int4 words per block summary: staircase + (ymin, ymax, n|trunc, -)
+constexpr int kSumRing = 64;    // LDS ring of block summaries (the last 64 complete blocks): 5 KB
+constexpr int kInnerCap = 256;  // LDS inner-window list (ring-deque) + stamps: 3 KB
+constexpr int kBdq = 128;       // block-argmin deque, 2 int4 per element: 4 KB
+constexpr int kIdq = 256;       // inner max-deque (idx, f + span): 2 KB
+constexpr size_t kChainLds = kRing * sizeof(int4) + kSumRing * kSumInts * sizeof(int4) + 64 * 2 * sizeof(int4) +
+                             kInnerCap * (sizeof(int2) + sizeof(int32_t)) + kBdq * 2 * sizeof(int4) + kIdq * sizeof(int2);
+constexpr int kNegInf = -(1 << 29);
+constexpr int kMaxGroup = 1 << 24;  // p+1 and span share one 32-bit ring word
+
+// Section cycle counters for tools/chain_prof (built with -DHYMET_CHAIN_PROF); no-ops otherwise.
+#ifdef HYMET_CHAIN_PROF
+__device__ unsigned long long g_chain_prof[32];
+#define CPROF_DECL uint64_t _pt = clock64(), _pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _pcnt[24] = {0};
+#define CCOUNT(k) (_pcnt[k]++)
+#define CPROF(k)                       \
+    do {                               \
+        const uint64_t _n = clock64(); \
+        _pacc[k] += _n - _pt;          \
+        _pt = _n;                      \
+    } while (0)
+#define CPROF_FLUSH                                                                  \
+    do {                                                                             \
+        if (lane == 0)                                                               \
+            for (int _k = 0; _k < 24; _k++) { if (_k < 8) atomicAdd(&g_chain_prof[_k], _pacc[_k]); atomicAdd(&g_chain_prof[8 + _k], _pcnt[_k]); } \
+    } while (0)
+#else
+#define CPROF_DECL
+#define CCOUNT(k)
+#define CPROF(k)
+#define CPROF_FLUSH
+#endif
 
 struct ChainParams {
     const uint64_t *ax;
     const uint64_t *ay;
     const int64_t *g_start;   // group g = anchors [g_start[g], g_start[g+1])
+    const uint8_t *g_qfirst;  // group g starts its query's anchor array (the krmq index-0 quirk)
     const int32_t *order;     // work list of group ids (size-descending)
     int32_t n_work;
     int32_t *work_counter;
     int32_t *f;
     int64_t *p;
     int32_t *t_global;        // overflow path only
+    int4 *sum;                // block summaries of every group (group g at ((g_start[g] >> 6) + g) * kSumInts)
     int max_dist, max_dist_inner, bw, max_chn_skip, cap_rmq_size;
     float pen_gap, pen_skip;
 };
@@ -57,14 +110,14 @@ __device__ __forceinline__ float mg_log2(float x) {
     return log_2;
 }
 
-__device__ __forceinline__ int32_t comput_sc(uint64_t xi, uint64_t yi_, uint64_t xj, uint64_t yj_, float pen_gap,
-                                             float pen_skip, int32_t *exact, int32_t *width) {
-    const int32_t dq = (int32_t)yi_ - (int32_t)yj_;
-    const int32_t dr = (int32_t)(xi - xj);
+// lchain.c comput_sc on the low 32 bits (x>>32 is constant inside a group)
+__device__ __forceinline__ int32_t comput_sc(int32_t xi, int32_t yi, int32_t xj, int32_t yj, int32_t q_span,
+                                             float pen_gap, float pen_skip, int32_t *exact, int32_t *width) {
+    const int32_t dq = yi - yj;
+    const int32_t dr = (int32_t)((uint32_t)xi - (uint32_t)xj);
     const int32_t dd = dr > dq ? dr - dq : dq - dr;
     *width = dd;
     const int32_t dg = dr < dq ? dr : dq;
-    const int32_t q_span = (int32_t)(yj_ >> 32 & 0xff);
     int32_t sc = q_span < dg ? q_span : dg;
     *exact = (dd == 0 && dg <= q_span);
     if (dd || dq > q_span) {
@@ -75,164 +128,892 @@ __device__ __forceinline__ int32_t comput_sc(uint64_t xi, uint64_t yi_, uint64_t
     return sc;
 }
 
-__device__ __forceinline__ double prio(int32_t f, uint64_t x, uint64_t y, float pen_gap) {
+__device__ __forceinline__ double prio(int32_t f, int32_t x, int32_t y, double c) {
     const int32_t s = (int32_t)((uint32_t)x + (uint32_t)y);
-    const double c = 0.5 * (double)pen_gap;
-    return -((double)f + __dmul_rn(c, (double)s));
+    return -__dadd_rn((double)f, __dmul_rn(c, (double)s));
 }
 
 __device__ __forceinline__ bool key_less(int32_t ya, int32_t ja, int32_t yb, int32_t jb) {
     return ya < yb || (ya == yb && ja < jb);
 }
 
-__global__ __launch_bounds__(256) void chain_groups_kernel(ChainParams P) {
+// (pr, j) beats (bp, bj): smaller priority, ties -> larger index; bj < 0 = none
+__device__ __forceinline__ bool better(double pr, int32_t j, double bp, int32_t bj) {
+    return j >= 0 && (bj < 0 || pr < bp || (pr == bp && j > bj));
+}
+
+// ---- wave-wide reductions without LDS: DPP within rows of 16, permlane swaps across rows
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+
+// partner value across rows: xor 16 (permlane16_swap) / xor 32 (permlane32_swap)
+__device__ __forceinline__ int xrow16(int v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? r[0] : r[1];
+}
+__device__ __forceinline__ int xrow32(int v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? r[0] : r[1];
+}
+
+template <int STEP>
+__device__ __forceinline__ int xstep(int v) {
+    if constexpr (STEP == 0) return dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+    if constexpr (STEP == 1) return dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+    if constexpr (STEP == 2) return dpp<0x141>(v);  // row_half_mirror
+    if constexpr (STEP == 3) return dpp<0x140>(v);  // row_mirror
+    if constexpr (STEP == 4) return xrow16(v);
+    return xrow32(v);
+}
+
+template <int STEP>
+__device__ __forceinline__ void argmin_step(double &p, int32_t &j, int32_t &y) {
+    const int lo = xstep<STEP>(__double2loint(p)), hi = xstep<STEP>(__double2hiint(p));
+    const int oj = xstep<STEP>(j), oy = xstep<STEP>(y);
+    const double op = __hiloint2double(hi, lo);
+    if (better(op, oj, p, j)) p = op, j = oj, y = oy;
+}
+
+// every lane ends with the wave's best (p, j) and the payload y of that lane
+__device__ __forceinline__ void wave_argmin(double &p, int32_t &j, int32_t &y) {
+    argmin_step<0>(p, j, y);
+    argmin_step<1>(p, j, y);
+    argmin_step<2>(p, j, y);
+    argmin_step<3>(p, j, y);
+    argmin_step<4>(p, j, y);
+    argmin_step<5>(p, j, y);
+}
+
+template <int STEP>
+__device__ __forceinline__ void minmax_step(int32_t &mn, int32_t &mx) {
+    mn = min(mn, xstep<STEP>(mn));
+    mx = max(mx, xstep<STEP>(mx));
+}
+__device__ __forceinline__ void wave_minmax(int32_t &mn, int32_t &mx) {
+    minmax_step<0>(mn, mx);
+    minmax_step<1>(mn, mx);
+    minmax_step<2>(mn, mx);
+    minmax_step<3>(mn, mx);
+    minmax_step<4>(mn, mx);
+    minmax_step<5>(mn, mx);
+}
+
+// Values this wave wrote earlier (f, p, t, block summaries) are re-read through L2: an
+// agent-scope relaxed load cannot hit a line the CU's L1 cached before the store.
+template <typename T>
+__device__ __forceinline__ T ld_l2(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int4 ld_l2(const int4 *p) {
+    const int32_t *q = reinterpret_cast<const int32_t *>(p);
+    return make_int4(ld_l2(q), ld_l2(q + 1), ld_l2(q + 2), ld_l2(q + 3));
+}
+
+// ---- wave prefix scans with DPP: row_shr within rows of 16, row_bcast15/31 across rows
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ int dppu(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xF, false);
+}
+// value of lane l-1 (lane 0: first)
+__device__ __forceinline__ int shr1(int v, int first) {
+    const int r = dppu<0x138>(0, v);  // wave_shr:1
+    return threadIdx.x == 0 ? first : r;
+}
+__device__ __forceinline__ int scan_max(int v) {  // inclusive prefix max
+    v = max(v, dppu<0x111>(INT32_MIN, v));
+    v = max(v, dppu<0x112>(INT32_MIN, v));
+    v = max(v, dppu<0x114>(INT32_MIN, v));
+    v = max(v, dppu<0x118>(INT32_MIN, v));
+    v = max(v, dppu<0x142, 0xA>(INT32_MIN, v));
+    v = max(v, dppu<0x143, 0xC>(INT32_MIN, v));
+    return v;
+}
+// inclusive scan of the maps f -> max(f + a, b) (left to right)
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ void mp_step(int &a, int &b) {
+    const int ao = dppu<CTRL, ROWMASK>(0, a), bo = dppu<CTRL, ROWMASK>(kNegInf, b);
+    b = max(bo + a, b);
+    a = ao + a;
+}
+__device__ __forceinline__ void scan_maxplus(int &a, int &b) {
+    mp_step<0x111>(a, b);
+    mp_step<0x112>(a, b);
+    mp_step<0x114>(a, b);
+    mp_step<0x118>(a, b);
+    mp_step<0x142, 0xA>(a, b);
+    mp_step<0x143, 0xC>(a, b);
+}
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ double min_step(double v) {
+    const double id = 1e300;
+    const int lo = dppu<CTRL, ROWMASK>(__double2loint(id), __double2loint(v));
+    const int hi = dppu<CTRL, ROWMASK>(__double2hiint(id), __double2hiint(v));
+    const double o = __hiloint2double(hi, lo);
+    return o < v ? o : v;
+}
+__device__ __forceinline__ double scan_min_d(double v) {  // inclusive prefix min
+    v = min_step<0x111>(v);
+    v = min_step<0x112>(v);
+    v = min_step<0x114>(v);
+    v = min_step<0x118>(v);
+    v = min_step<0x142, 0xA>(v);
+    v = min_step<0x143, 0xC>(v);
+    return v;
+}
+
+struct Ent {
+    int32_t x, y, f, pw;  // pw = (p_local + 1) | span << 24
+    __device__ int32_t p() const { return (pw & 0xFFFFFF) - 1; }
+    __device__ int32_t sp() const { return (int32_t)((uint32_t)pw >> 24); }
+};
+
+__device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ double rld(double v, int l) {
+    return __hiloint2double(rl(__double2hiint(v), l), rl(__double2loint(v), l));
+}
+__device__ __forceinline__ int4 pack_st(double pr, int32_t j, int32_t y) {
+    return make_int4(__double2loint(pr), __double2hiint(pr), j, y);
+}
+__device__ __forceinline__ double st_pr(const int4 &v) { return __hiloint2double(v.y, v.x); }
+
+__global__ __launch_bounds__(64) void chain_groups_kernel(ChainParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    int2 *lst = reinterpret_cast<int2 *>(smem) + wv * kInnerCap;                       // (y, local idx)
-    int32_t *stamp = reinterpret_cast<int32_t *>(smem + kWavesPerBlock * kInnerCap * sizeof(int2)) + wv * kInnerCap;
+    const int lane = threadIdx.x;
+    unsigned char *sp = smem;
+    int4 *ring = reinterpret_cast<int4 *>(sp);
+    sp += kRing * sizeof(int4);
+    int4 *ssum = reinterpret_cast<int4 *>(sp);  // kSumInts int4 per block (staircase + meta)
+    sp += kSumRing * kSumInts * sizeof(int4);
+    int4 *hc = reinterpret_cast<int4 *>(sp);
+    sp += 64 * sizeof(int4);
+    int4 *hsuf = reinterpret_cast<int4 *>(sp);  // (pr lo, pr hi, j, y): argmin of [k, 64) of block hb
+    sp += 64 * sizeof(int4);
+    int4 *bdq = reinterpret_cast<int4 *>(sp);  // 2 per element: (pr lo, pr hi, idx, y), (x, f, pw, -)
+    sp += kBdq * 2 * sizeof(int4);
+    int2 *lst = reinterpret_cast<int2 *>(sp);
+    sp += kInnerCap * sizeof(int2);
+    int2 *idq = reinterpret_cast<int2 *>(sp);  // (idx, f + span)
+    sp += kIdq * sizeof(int2);
+    int32_t *stamp = reinterpret_cast<int32_t *>(sp);
+    const double c = 0.5 * (double)P.pen_gap;
     for (;;) {
         int w = 0;
         if (lane == 0) w = atomicAdd(P.work_counter, 1);
         w = __shfl(w, 0, 64);
         if (w >= P.n_work) break;
         const int g = P.order[w];
-        const int64_t g0 = P.g_start[g], g1 = P.g_start[g + 1];
-        int ni = 0;           // entries in lst (== i0 - st_in while !overflow)
-        bool overflow = false;
-        for (int e = lane; e < kInnerCap; e += 64) stamp[e] = -1;
-        int64_t i0 = g0, st = g0, st_in = g0;
-        for (int64_t i = g0; i < g1; ++i) {
-            const uint64_t xi = P.ax[i], yi_ = P.ay[i];
-            const int32_t yi = (int32_t)yi_;
-            int32_t max_f = (int32_t)(yi_ >> 32 & 0xff);
-            int64_t max_j = -1;
-            if (i0 < i && P.ax[i0] != xi) {
-                for (int64_t j = i0; j < i; ++j) {  // insert into the inner tree
-                    if (P.max_dist_inner <= 0) break;
-                    if (!overflow && ni >= kInnerCap) overflow = true;
-                    if (overflow) continue;
-                    const int32_t yj = (int32_t)P.ay[j], jl = (int32_t)(j - g0);
-                    int c = 0;
-                    for (int e = lane; e < ni; e += 64) c += key_less(lst[e].x, lst[e].y, yj, jl);
-                    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-                    for (int top = ni - 1; top >= c; top -= 64) {  // shift [c, ni) right by one
-                        const int e = top - lane;
-                        int2 v;
-                        if (e >= c) v = lst[e];
-                        __builtin_amdgcn_wave_barrier();
-                        if (e >= c) lst[e + 1] = v;
-                        __builtin_amdgcn_wave_barrier();
+        const int64_t g0 = P.g_start[g];
+        const int32_t n = (int32_t)(P.g_start[g + 1] - g0);
+        const bool qfirst = P.g_qfirst[g] != 0;
+        int4 *gsum = P.sum + ((g0 >> 6) + g) * kSumInts;
+        int32_t hb = -1;        // block held by the head cache
+        bool hsuf_ok = false;   // hsuf holds the suffix argmins of block hb
+        int32_t i = 0;
+        CPROF_DECL
+        // anchor jl (local) as seen at iteration i: ring [i - kRing, i), head cache, else HBM
+        auto fetch = [&](int32_t jl) -> Ent {
+            Ent e;
+            int4 v;
+            if (i - jl <= kRing) {
+                v = ring[jl & kRingMask];
+            } else if ((jl >> 6) == hb) {
+                v = hc[jl & 63];
+            } else {
+                CCOUNT(0);
+                const uint64_t x = P.ax[g0 + jl], y = P.ay[g0 + jl];
+                const int64_t pp = ld_l2(P.p + g0 + jl);
+                v = make_int4((int32_t)x, (int32_t)y, ld_l2(P.f + g0 + jl),
+                              (int32_t)((pp < 0 ? 0u : (uint32_t)(pp - g0 + 1)) | (uint32_t)(y >> 32 & 0xff) << 24));
+            }
+            e.x = v.x, e.y = v.y, e.f = v.z, e.pw = v.w;
+            return e;
+        };
+        int32_t i0 = 0, st = 0, st_in = 0;
+        auto sum_at = [&](int32_t b, int k) -> int4 {  // word k of block b's summary
+            if ((i0 >> 6) - b <= kSumRing) return ssum[(b & (kSumRing - 1)) * kSumInts + k];
+            return ld_l2(gsum + (int64_t)b * kSumInts + k);
+        };
+        // best (priority, index) over window entries [st, i0) with ylo < y < yq (quirk: y == yq
+        // allowed for the query's anchor 0): per complete block the first staircase entry below
+        // yq, entries of the partial head/tail blocks, rescans where a summary cannot decide
+        auto window_best = [&](int32_t yq, int32_t ylo, bool quirk, double &bp, int32_t &bj) {
+            const int32_t fb = (st + 63) >> 6, fe = i0 >> 6;
+            auto in_q = [&](int32_t y, int32_t j) { return y > ylo && (y < yq || (quirk && y == yq && qfirst && j == 0)); };
+            bp = 0.0, bj = -1;
+            auto scan = [&](int32_t a, int32_t e) {  // entries [a, e), e - a <= 64
+                const int32_t j = a + lane;
+                if (j < e) {
+                    const Ent en = fetch(j);
+                    if (in_q(en.y, j)) {
+                        const double pr = prio(en.f, en.x, en.y, c);
+                        if (better(pr, j, bp, bj)) bp = pr, bj = j;
                     }
-                    if (lane == 0) lst[c] = make_int2(yj, jl);
-                    __builtin_amdgcn_wave_barrier();
-                    ni++;
                 }
+            };
+            if (st < (fb << 6)) scan(st, min(fb << 6, i0));             // head
+            if (fe >= fb && (fe << 6) < i0) scan(max(fe << 6, st), i0);  // tail
+            for (int32_t base = fb; base < fe; base += 64) {
+                const int32_t b = base + lane;
+                bool rescan = false;
+                if (b < fe) {
+                    const int4 meta = sum_at(b, kStair);
+                    if (quirk && qfirst && b == 0) {
+                        rescan = true;  // the index-0 quirk admits y == yq
+                    } else if (!(meta.y <= ylo || meta.x >= yq)) {
+                        const int ns = meta.z & 255;
+                        int k = 0;
+                        int4 v = make_int4(0, 0, -1, 0);
+                        for (; k < ns; ++k) {
+                            v = sum_at(b, k);
+                            if (v.w < yq) break;
+                        }
+                        if (k == ns) {
+                            rescan = (meta.z & 256) != 0;  // truncated staircase
+                        } else if (v.w > ylo) {
+                            if (better(st_pr(v), v.z, bp, bj)) bp = st_pr(v), bj = v.z;
+                        } else {
+                            rescan = true;  // the best below yq lies at or below ylo
+                        }
+                    }
+                }
+                uint64_t m = __ballot(rescan);
+                while (m) {
+                    const int l = __ffsll((unsigned long long)m) - 1;
+                    m &= m - 1;
+                    scan((base + l) << 6, ((base + l) << 6) + 64);
+                }
+            }
+            int32_t dummy = 0;
+            wave_argmin(bp, bj, dummy);
+        };
+        // inner list: ring-deque, logical k at lst[(lh + k) & (kInnerCap - 1)]; ends cached
+        int ni = 0, lh = 0;
+        int32_t lfy = 0, lfj = -1, lby = 0, lbj = -1;  // front / back keys
+        bool overflow = false;
+        auto L = [&](int k) -> int2 & { return lst[(lh + k) & (kInnerCap - 1)]; };
+        auto reload_ends = [&]() {
+            if (ni > 0) {
+                const int2 a = L(0), b = L(ni - 1);
+                lfy = a.x, lfj = a.y, lby = b.x, lbj = b.y;
+            }
+        };
+        // block deque [bh, bt) of complete blocks by their argmin, monotone (front = best)
+        int bh = 0, bt = 0;
+        bool bok = true;
+        double bf_pr = 0.0, bb_pr = 0.0;
+        int32_t bf_j = -1, bf_y = 0, bb_j = -1;
+        int4 bf_e = make_int4(0, 0, 0, 0);  // front argmin entry (x, f, pw)
+        // running argmin of the partial tail block [i0 & ~63, i0) (ignoring y)
+        double t_pr = 0.0;
+        int32_t t_j = -1, t_y = 0;
+        // inner max-deque of f_j + span_j over [st_in, i0); front/back values cached
+        int ih = 0, it = 0;
+        bool iok = true;
+        int32_t if_v = 0, ib_v = 0;
+        for (int e = lane; e < kInnerCap; e += 64) stamp[e] = -1;
+        __builtin_amdgcn_wave_barrier();
+        // double-buffered anchor chunks: lane l holds anchor (chunk base + l)
+        uint64_t nx = 0, ny = 0, cx = 0, cy = 0;
+        Ent prev{0, 0, 0, 0};  // anchor i-1
+        // block b complete: staircase summary -- S1 = argmin, S(k+1) = argmin over y < y(Sk),
+        // i.e. the entries better than every entry with y <= theirs, by y descending; the
+        // best of (block, y < Y) is the first S with y < Y -- then the argmin joins the deque
+        auto complete_block = [&](int32_t b) {
+            const int32_t jl = (b << 6) + lane;
+            const Ent e = fetch(jl);
+            const double pl = prio(e.f, e.x, e.y, c);
+            bool rec = true;
+            for (int k = 0; k < 64; ++k) {
+                const int32_t yk = rl(e.y, k);
+                const double pk = rld(pl, k);
+                if (k != lane && yk <= e.y && better(pk, (b << 6) + k, pl, jl)) rec = false;
+            }
+            const uint64_t recm = __ballot(rec);
+            int rank = 0;  // records with larger y (records have distinct y)
+            for (uint64_t m = recm; m;) {
+                const int k = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                rank += rl(e.y, k) > e.y;
+            }
+            int32_t ymn = e.y, ymx = e.y;
+            wave_minmax(ymn, ymx);
+            const int nrec = __popcll(recm);
+            const int4 meta = make_int4(ymn, ymx, min(nrec, kStair) | (nrec > kStair ? 256 : 0), 0);
+            int4 *ls = ssum + (b & (kSumRing - 1)) * kSumInts;
+            int4 *gs = gsum + (int64_t)b * kSumInts;
+            __builtin_amdgcn_wave_barrier();
+            if (rec && rank < kStair) {
+                ls[rank] = pack_st(pl, jl, e.y);
+                gs[rank] = pack_st(pl, jl, e.y);
+            }
+            if (lane == 0) ls[kStair] = meta, gs[kStair] = meta;
+            __builtin_amdgcn_wave_barrier();
+            if (!bok) return;
+            const int l0 = __ffsll((unsigned long long)__ballot(rec && rank == 0)) - 1;
+            const double apr = rld(pl, l0);
+            const int32_t aj = (b << 6) + l0, ay = rl(e.y, l0);
+            while (bt > bh && better(apr, aj, bb_pr, bb_j)) {
+                --bt;
+                if (bt > bh) {
+                    const int4 v = bdq[((bt - 1) & (kBdq - 1)) * 2];
+                    bb_pr = st_pr(v), bb_j = v.z;
+                }
+            }
+            if (bt - bh >= kBdq) {
+                bok = false;
+                return;
+            }
+            const int4 ex = make_int4(rl(e.x, l0), rl(e.f, l0), rl(e.pw, l0), 0);
+            if (lane == 0) {
+                bdq[(bt & (kBdq - 1)) * 2] = pack_st(apr, aj, ay);
+                bdq[(bt & (kBdq - 1)) * 2 + 1] = ex;
+            }
+            if (bt == bh) bf_pr = apr, bf_j = aj, bf_y = ay, bf_e = ex;
+            bb_pr = apr, bb_j = aj;
+            ++bt;
+        };
+        // entry j (now final) enters the window: inner list, inner max-deque, tail argmin
+        auto insert_one = [&](int32_t j, const Ent ej) {
+            if (P.max_dist_inner > 0) {
+                if (!overflow && ni >= kInnerCap) overflow = true;
+                if (!overflow) {
+                    if (ni == 0 || key_less(lby, lbj, ej.y, j)) {  // append (colinear)
+                        if (lane == 0) L(ni) = make_int2(ej.y, j);
+                        if (ni == 0) lfy = ej.y, lfj = j;
+                        lby = ej.y, lbj = j;
+                        ni++;
+                    } else {
+                        // position among the last <= 64 entries (entries > key form a suffix)
+                        const int m = min(ni, 64), base = ni - m;
+                        bool gt = false;
+                        if (lane < m) {
+                            const int2 v = L(base + lane);
+                            gt = key_less(ej.y, j, v.x, v.y);
+                        }
+                        const int ngt = __popcll(__ballot(gt));
+                        int pos;
+                        if (ngt < m || base == 0) {
+                            pos = ni - ngt;
+                        } else {
+                            CCOUNT(1);
+                            int cnt = 0;
+                            for (int k = lane; k < ni; k += 64) cnt += key_less(L(k).x, L(k).y, ej.y, j);
+                            for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                            pos = cnt;
+                        }
+                        for (int top = ni - 1; top >= pos; top -= 64) {  // shift [pos, ni) right by one
+                            const int k = top - lane;
+                            int2 v;
+                            if (k >= pos) v = L(k);
+                            __builtin_amdgcn_wave_barrier();
+                            if (k >= pos) L(k + 1) = v;
+                            __builtin_amdgcn_wave_barrier();
+                        }
+                        if (lane == 0) L(pos) = make_int2(ej.y, j);
+                        __builtin_amdgcn_wave_barrier();
+                        ni++;
+                        if (pos == 0) lfy = ej.y, lfj = j;
+                    }
+                }
+                if (iok) {  // max-deque push of f_j + span_j
+                    const int32_t v = ej.f + ej.sp();
+                    while (it > ih && ib_v <= v) {
+                        --it;
+                        if (it > ih) ib_v = idq[(it - 1) & (kIdq - 1)].y;
+                    }
+                    if (it - ih >= kIdq) {
+                        iok = false;
+                    } else {
+                        if (lane == 0) idq[it & (kIdq - 1)] = make_int2(j, v);
+                        if (it == ih) if_v = v;
+                        ib_v = v;
+                        ++it;
+                    }
+                }
+            }
+            // running argmin of the tail block (ties -> larger j)
+            const double pr = prio(ej.f, ej.x, ej.y, c);
+            if ((j & 63) == 0 || !(t_pr < pr)) t_pr = pr, t_j = j, t_y = ej.y;
+            if ((j & 63) == 63) complete_block(j >> 6);
+        };
+        int32_t cb = -128;  // base of the chunk in cx/cy; nx/ny hold the next one
+        int32_t spec_next = 0, spec_gap = 2;  // next batch attempt (back-off after short batches)
+        for (; i < n;) {
+            CPROF(7);
+            if ((i >> 6) != (cb >> 6)) {
+                if ((i >> 6) == (cb >> 6) + 1) {
+                    cx = nx, cy = ny;
+                } else {
+                    const int32_t b = (i & ~63) + lane;
+                    cx = b < n ? P.ax[g0 + b] : 0;
+                    cy = b < n ? P.ay[g0 + b] : 0;
+                }
+                cb = i & ~63;
+                const int32_t b = cb + 64 + lane;
+                nx = b < n ? P.ax[g0 + b] : 0;
+                ny = b < n ? P.ay[g0 + b] : 0;
+            }
+            const int32_t xi = rl((int32_t)cx, i & 63);
+            const int32_t yi = rl((int32_t)cy, i & 63);
+            const int32_t span_i = rl((int32_t)(cy >> 32 & 0xff), i & 63);
+            int32_t max_f = span_i;
+            int32_t max_j = -1;
+            // ---- 1. i0 advances: insert [i0, i) into the window structures
+            if (i0 < i && prev.x != xi) {
+                for (int32_t j = i0; j < i; ++j) insert_one(j, j == i - 1 ? prev : fetch(j));
                 i0 = i;
             }
-            while (st < i && (xi > P.ax[st] + (uint64_t)P.max_dist || (i0 > st ? i0 - st : 0) > P.cap_rmq_size)) ++st;
+            CPROF(0);
+            // ---- 2. outer window start: lane-parallel probe, one block at a time
+            for (;;) {
+                if (st >= i) break;
+                const int32_t bend = min(i, ((st >> 6) + 1) << 6);
+                const int32_t j = st + lane;
+                bool adv = false;
+                if (j < bend) {
+                    const Ent e = fetch(j);
+                    adv = (int64_t)(uint32_t)xi > (int64_t)(uint32_t)e.x + P.max_dist || i0 - j > P.cap_rmq_size;
+                }
+                const uint64_t m = __ballot(adv);
+                const int t = ~m ? __ffsll((unsigned long long)~m) - 1 : 64;  // lanes [0, t) advance
+                st += min(t, bend - st);
+                if (st < bend) break;
+                // st entered a new block: cache it if it sits beyond the ring
+                if (st < i && (st >> 6) < (i0 >> 6) && i - st > kRing && (st >> 6) != hb) {
+                    const int32_t hb2 = st >> 6;
+                    const Ent e = fetch((hb2 << 6) + lane);
+                    __builtin_amdgcn_wave_barrier();
+                    hc[lane] = make_int4(e.x, e.y, e.f, e.pw);
+                    __builtin_amdgcn_wave_barrier();
+                    hb = hb2;
+                    hsuf_ok = false;
+                }
+            }
+            const int32_t fb = (st + 63) >> 6, fe = i0 >> 6;  // complete window blocks [fb, fe)
+            while (bt > bh && (bf_j >> 6) < fb) {
+                ++bh;
+                if (bt > bh) {
+                    const int4 v = bdq[(bh & (kBdq - 1)) * 2];
+                    bf_pr = st_pr(v), bf_j = v.z, bf_y = v.w;
+                    bf_e = bdq[(bh & (kBdq - 1)) * 2 + 1];
+                }
+            }
+            if ((st & 63) && (st >> 6) < fe && ((st >> 6) != hb || !hsuf_ok)) {
+                // partial head block: cache it with its suffix argmins [lane, 64)
+                CCOUNT(5);
+                const int32_t b = st >> 6, j = (b << 6) + lane;
+                const Ent e = fetch(j);
+                double pr = prio(e.f, e.x, e.y, c);
+                int32_t pj = j, py = e.y;
+                for (int d = 1; d < 64; d <<= 1) {
+                    const double op = __shfl_down(pr, d, 64);
+                    const int32_t oj = __shfl_down(pj, d, 64), oy = __shfl_down(py, d, 64);
+                    if (lane + d < 64 && better(op, oj, pr, pj)) pr = op, pj = oj, py = oy;
+                }
+                __builtin_amdgcn_wave_barrier();
+                hc[lane] = make_int4(e.x, e.y, e.f, e.pw);
+                hsuf[lane] = pack_st(pr, pj, py);
+                __builtin_amdgcn_wave_barrier();
+                hb = b;
+                hsuf_ok = true;
+            }
+            CPROF(1);
+            // ---- 3. inner window start
             if (P.max_dist_inner > 0) {
-                while (st_in < i && (xi > P.ax[st_in] + (uint64_t)P.max_dist_inner ||
-                                     (i0 > st_in ? i0 - st_in : 0) > P.cap_rmq_size)) {
-                    if (st_in < i0 && !overflow) {  // erase from the inner list
-                        const int32_t yj = (int32_t)P.ay[st_in], jl = (int32_t)(st_in - g0);
-                        int c = 0;
-                        for (int e = lane; e < ni; e += 64) c += key_less(lst[e].x, lst[e].y, yj, jl);
-                        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-                        for (int b = c; b < ni - 1; b += 64) {  // shift (c, ni) left by one
-                            const int e = b + lane + 1;
-                            int2 v;
-                            if (e < ni) v = lst[e];
+                for (;;) {
+                    if (st_in >= i) break;
+                    const int32_t j = st_in + lane;
+                    bool adv = false;
+                    int32_t yj = 0;
+                    if (j < i) {
+                        const Ent e = fetch(j);
+                        yj = e.y;
+                        adv = (int64_t)(uint32_t)xi > (int64_t)(uint32_t)e.x + P.max_dist_inner || i0 - j > P.cap_rmq_size;
+                    }
+                    const uint64_t m = __ballot(adv);
+                    const int t = ~m ? __ffsll((unsigned long long)~m) - 1 : 64;
+                    if (t > 1 && !overflow && ni > 0) {
+                        // several entries leave: stable compaction of the list keeps j >= st_in + t
+                        const int32_t lim = st_in + t;
+                        int kept = 0;
+                        for (int base = 0; base < ni; base += 64) {
+                            const int kk = base + lane;
+                            int2 v = make_int2(0, 0);
+                            if (kk < ni) v = L(kk);
+                            const bool keep = kk < ni && v.y >= lim;
+                            const uint64_t mk = __ballot(keep);
+                            const int dst = kept + __popcll(mk & ((1ull << lane) - 1));
                             __builtin_amdgcn_wave_barrier();
-                            if (e < ni) lst[e - 1] = v;
+                            if (keep) L(dst) = v;
+                            __builtin_amdgcn_wave_barrier();
+                            kept += __popcll(mk);
+                        }
+                        ni = kept;
+                        reload_ends();
+                        st_in += t;
+                        if (t < 64) break;
+                        continue;
+                    }
+                    for (int l = 0; l < t; ++l) {  // erase the passed entries from the inner list
+                        const int32_t jj = st_in + l;
+                        if (jj >= i0 || overflow) continue;
+                        const int32_t y = rl(yj, l);
+                        if (y == lfy && jj == lfj) {  // front (colinear)
+                            lh = (lh + 1) & (kInnerCap - 1);
+                            ni--;
+                            if (ni > 0) {
+                                const int2 a = L(0);
+                                lfy = a.x, lfj = a.y;
+                            }
+                            continue;
+                        }
+                        // near the front: shift [0, pos) right by one and pop the front slot
+                        bool eq = false;
+                        if (lane < min(ni, 64)) {
+                            const int2 v = L(lane);
+                            eq = v.x == y && v.y == jj;
+                        }
+                        const uint64_t me = __ballot(eq);
+                        if (me) {
+                            const int pos = __ffsll((unsigned long long)me) - 1;
+                            int2 v;
+                            if (lane < pos) v = L(lane);
+                            __builtin_amdgcn_wave_barrier();
+                            if (lane < pos) L(lane + 1) = v;
+                            __builtin_amdgcn_wave_barrier();
+                            lh = (lh + 1) & (kInnerCap - 1);
+                            ni--;
+                            reload_ends();
+                            continue;
+                        }
+                        CCOUNT(2);
+                        int cnt = 0;
+                        for (int k = lane; k < ni; k += 64) cnt += key_less(L(k).x, L(k).y, y, jj);
+                        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                        for (int b = cnt; b < ni - 1; b += 64) {  // shift (cnt, ni) left by one
+                            const int k = b + lane + 1;
+                            int2 v;
+                            if (k < ni) v = L(k);
+                            __builtin_amdgcn_wave_barrier();
+                            if (k < ni) L(k - 1) = v;
                             __builtin_amdgcn_wave_barrier();
                         }
                         ni--;
+                        reload_ends();
                     }
-                    ++st_in;
+                    st_in += t;
+                    if (t < 64) break;
+                }
+                while (it > ih && idq[ih & (kIdq - 1)].x < st_in) {
+                    ++ih;
+                    if (it > ih) if_v = idq[ih & (kIdq - 1)].y;
                 }
             }
-            // ---- RMQ over the outer window
+            CPROF(6);
+            // ---- 3b. colinear batch: assume each of the next L anchors chains onto its
+            // predecessor (max-plus scan for f), then verify, lane-parallel, every decision the
+            // sequential DP would take: the predecessor is the window's best priority (it beats
+            // the pre-batch window best B0 and every earlier batch entry, ignoring y) and lies
+            // in the krmq range, its score passes bw, and the inner walk cannot improve max_f.
+            // The verified prefix is committed in bulk; the first failing anchor runs below.
+            // Attempts back off after short batches (non-colinear stretches).
+            if (i0 == i && i > 0 && st < i0 && i >= spec_next) {
+                const bool walk_ok = P.max_dist_inner <= 0 || (iok && !overflow);
+                int Lb = min(64, n - i);
+                // the batch's inner-list keys go into one gap: before G, the first list key above
+                // the first inserted key (entry i); all the tail [gpos, ni) shifts in one round
+                int gpos = ni;
+                int32_t gy = INT32_MAX, gj = INT32_MAX;
+                if (P.max_dist_inner > 0) Lb = min(Lb, kInnerCap - ni);
+                // B: the best pre-batch window entry with y <= Y, Y = y of the last batch anchor,
+                // a superset of every batch anchor's krmq range; the batch starts only if B is
+                // the predecessor of its first anchor
+                double b0p = 0.0;
+                int32_t b0j = -1;
+                if (walk_ok && Lb >= 2) {
+                    const int offl = (i - cb) + Lb - 1;
+                    const int32_t ymax = (int32_t)(offl < 64 ? rl((int32_t)cy, offl) : rl((int32_t)ny, offl - 64));
+                    window_best(ymax == INT32_MAX ? ymax : ymax + 1, INT32_MIN, false, b0p, b0j);
+                }
+                CCOUNT(8);
+                if (b0j != i - 1) CCOUNT(10);
+                if (!walk_ok) CCOUNT(11);
+                if (b0j == i - 1 && walk_ok && Lb >= 2) {
+                    // anchors k = i + lane from the chunk registers (cx: [cb, cb+64), nx: next 64)
+                    const int off = (i - cb) + lane;
+                    const uint64_t kx_lo = __shfl(cx, off & 63, 64), kx_hi = __shfl(nx, off & 63, 64);
+                    const uint64_t ky_lo = __shfl(cy, off & 63, 64), ky_hi = __shfl(ny, off & 63, 64);
+                    const bool inb = lane < Lb;
+                    const int32_t kx = (int32_t)(off < 64 ? kx_lo : kx_hi);
+                    const uint64_t kyy = off < 64 ? ky_lo : ky_hi;
+                    const int32_t ky = (int32_t)kyy, ksp = (int32_t)(kyy >> 32 & 0xff);
+                    const int32_t px = shr1(kx, prev.x), py = shr1(ky, prev.y), psp = shr1(ksp, prev.sp());
+                    int32_t ex = 1, wd = 0;
+                    const int32_t s = comput_sc(kx, ky, px, py, psp, P.pen_gap, P.pen_skip, &ex, &wd);
+                    bool ok = inb && kx != px && (int64_t)(uint32_t)kx <= (int64_t)(uint32_t)px + P.max_dist &&
+                              py > ky - P.max_dist && py < ky && wd <= P.bw;
+                    // f_k = max(span_k, f_{k-1} + s_k): maps f -> max(f + a, b), composed by scan
+                    int a = s, bb = ksp;
+                    scan_maxplus(a, bb);
+                    const int32_t fk = max(prev.f + a, bb);
+                    const int32_t fp = shr1(fk, prev.f);
+                    const bool linked = fp + s > ksp;  // sc > max_f = span: predecessor k-1
+                    // priorities of batch entries; the candidate of lane l is entry l-1
+                    const double pk = prio(fk, kx, ky, c);
+                    const double ipm = scan_min_d(inb ? pk : 1e300);
+                    const bool best_here = pk == ipm && !(b0p < pk);  // beats B0 and earlier entries
+                    // (cross-lane operations run with every lane active: DPP reads of an
+                    // inactive lane return the fallback value)
+                    const bool cand_ok = shr1(best_here ? 1 : 0, 1) != 0;
+                    // inner walk: max(f_j + span_j) over the inner window must not exceed f_k
+                    const int vex = shr1(scan_max(inb ? fk + ksp : INT32_MIN), INT32_MIN);  // entries before k
+                    bool wok = true;
+                    if (P.max_dist_inner > 0 && !ex && ky > 0) wok = max(vex, it > ih ? if_v : INT32_MIN) <= fk;
+                    // inner-list keys (y, idx) of entries i.. strictly increase (py < ky); they must
+                    // all fall into the gap of the list before G
+                    if (P.max_dist_inner > 0 && ni > 0) {
+                        const int32_t e0y = rl(ky, 0);
+                        if (!key_less(lby, lbj, e0y, i)) {
+                            const int m = min(ni, 64), base = ni - m;
+                            bool gt = false;
+                            int2 v = make_int2(0, 0);
+                            if (lane < m) {
+                                v = L(base + lane);
+                                gt = key_less(e0y, i, v.x, v.y);
+                            }
+                            const uint64_t mg = __ballot(gt);
+                            const int ngt = __popcll(mg);
+                            if (ngt == m && base > 0) {
+                                gy = INT32_MIN;  // gap beyond the last 64 entries: no batch
+                            } else {
+                                gpos = ni - ngt;
+                                const int lg = __ffsll((unsigned long long)mg) - 1;
+                                gy = rl(v.x, lg), gj = rl(v.y, lg);
+                            }
+                        }
+                        // entry k-1 (k = i + lane, lane >= 1) is inserted at anchor k
+                        if (lane >= 1 && !key_less(py, i + lane - 1, gy, gj)) ok = false;
+                    }
+                    const bool ok_geom = ok;
+                    ok = ok && cand_ok && wok;
+                    const uint64_t bad = __ballot(!ok);
+                    const int acc = bad ? __ffsll((unsigned long long)bad) - 1 : 64;
+#ifdef HYMET_CHAIN_PROF
+                    if (acc < Lb) {
+                        const int fl = acc;
+                        const bool g_ = rl(ok_geom ? 1 : 0, fl), c_ = rl(cand_ok ? 1 : 0, fl), w_ = rl(wok ? 1 : 0, fl);
+                        const bool xs = rl(kx != px ? 1 : 0, fl), yr = rl((py > ky - P.max_dist && py < ky) ? 1 : 0, fl);
+                        if (!xs) CCOUNT(12);
+                        else if (!yr) CCOUNT(13);
+                        else if (!g_) CCOUNT(14);
+                        else if (!c_) CCOUNT(15);
+                        else if (!w_) CCOUNT(16);
+                        else CCOUNT(17);  // list gap
+                    }
+                    _pcnt[18] += acc;
+#endif
+                    if (acc < 4) {
+                        spec_next = i + spec_gap;
+                        spec_gap = min(spec_gap * 2, 64);
+                    } else {
+                        spec_gap = 2;
+                    }
+                    if (acc > 0) {
+                        // commit anchors [i, i + acc): f, p, ring; insert entries [i, i + acc - 1)
+                        const int32_t k = i + lane;
+                        const int32_t pk_local = linked ? k - 1 : -1;
+                        const int32_t pw = (int32_t)((uint32_t)(pk_local + 1) | (uint32_t)ksp << 24);
+                        if (lane < acc) {
+                            P.f[g0 + k] = fk;
+                            P.p[g0 + k] = pk_local < 0 ? -1 : g0 + pk_local;
+                            ring[k & kRingMask] = make_int4(kx, ky, fk, pw);
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        CCOUNT(7);
+                        const int nins = acc - 1;
+                        if (nins > 0) {
+                            if (P.max_dist_inner > 0) {
+                                // list: shift [gpos, ni) right by nins, batch keys into [gpos, gpos + nins)
+                                {
+                                    const int kk = gpos + lane;
+                                    int2 v;
+                                    if (kk < ni) v = L(kk);
+                                    __builtin_amdgcn_wave_barrier();
+                                    if (kk < ni) L(kk + nins) = v;
+                                    if (lane < nins) L(gpos + lane) = make_int2(ky, k);
+                                    __builtin_amdgcn_wave_barrier();
+                                }
+                                if (gpos == 0) lfy = rl(ky, 0), lfj = i;
+                                if (gpos == ni) lby = rl(ky, nins - 1), lbj = i + nins - 1;
+                                ni += nins;
+                                // max-deque: pop the back while <= the batch maximum, then append
+                                // the batch's suffix records (values greater than all later ones)
+                                const int v = fk + ksp;
+                                int run = lane < nins ? v : INT32_MIN;
+                                for (int d = 1; d < 64; d <<= 1) {
+                                    const int o = __shfl_down(run, d, 64);
+                                    if (lane + d < 64) run = max(run, o);
+                                }
+                                int sfx = __shfl_down(run, 1, 64);
+                                if (lane == 63) sfx = INT32_MIN;
+                                const int vmax = rl(run, 0);
+                                while (it > ih && ib_v <= vmax) {
+                                    --it;
+                                    if (it > ih) ib_v = idq[(it - 1) & (kIdq - 1)].y;
+                                }
+                                const bool recd = lane < nins && v > sfx;
+                                const uint64_t rm = __ballot(recd);
+                                const int nr = __popcll(rm);
+                                if (it - ih + nr > kIdq) {
+                                    iok = false;
+                                } else {
+                                    const int rank = __popcll(rm & ((1ull << lane) - 1));
+                                    if (recd) idq[(it + rank) & (kIdq - 1)] = make_int2(k, v);
+                                    __builtin_amdgcn_wave_barrier();
+                                    if (it == ih) if_v = rl(v, __ffsll((unsigned long long)rm) - 1);
+                                    ib_v = rl(v, 63 - __clzll((long long)rm));
+                                    it += nr;
+                                }
+                            }
+                            // tail-block argmin, and blocks completed by the insertions
+                            const int32_t nb0 = i >> 6, nb1 = (i + nins) >> 6;
+                            for (int32_t b = nb0; b < nb1; ++b) complete_block(b);
+                            {
+                                const int32_t tb = (i + nins) & ~63, j = tb + lane;
+                                double tp = 0.0;
+                                int32_t tj = -1, ty = 0;
+                                if (j < i + nins) {
+                                    const Ent e = fetch(j);
+                                    tp = prio(e.f, e.x, e.y, c), tj = j, ty = e.y;
+                                }
+                                wave_argmin(tp, tj, ty);
+                                t_pr = tp, t_j = tj, t_y = ty;
+                            }
+                            i0 = i + nins;
+                        }
+                        const int l = acc - 1;
+                        prev.x = rl(kx, l), prev.y = rl(ky, l), prev.f = rl(fk, l), prev.pw = rl(pw, l);
+                        i += acc;
+                        continue;
+                    }
+                }
+            }
+            CPROF(2);
+            // ---- 4. RMQ over the outer window [st, i0)
             double bp = 0.0;
-            int64_t bj = -1;
-            for (int64_t j = st + lane; j < i0; j += 64) {
-                const int32_t yj = (int32_t)P.ay[j];
-                const bool in = (yj > yi - P.max_dist) && (yj < yi || (yj == yi && j == 0));
-                if (!in) continue;
-                const double pr = prio(P.f[j], P.ax[j], P.ay[j], P.pen_gap);
-                if (bj < 0 || pr < bp || (pr == bp && j > bj)) bp = pr, bj = j;
+            int32_t bj = -1;
+            Ent eb;  // the winner's entry
+            bool have_eb = false;
+            const int32_t ylo = yi - P.max_dist;
+            auto in_range = [&](int32_t y, int32_t j) { return y > ylo && (y < yi || (y == yi && qfirst && j == 0)); };
+            if (st < i0) {
+                // best of the whole window ignoring y: head suffix, best complete block, tail block
+                bool cert = st <= (fe << 6);  // else the window lies inside the partial tail block
+                int32_t wy = 0, src = -1;
+                if (cert) {
+                    if (st < (fb << 6)) {  // partial head block (complete, cached with suffix argmins)
+                        const int4 v = hsuf[st & 63];
+                        bp = st_pr(v), bj = v.z, wy = v.w, src = 0;
+                    }
+                    if (fb < fe) {
+                        if (!bok) cert = false;
+                        else if (better(bf_pr, bf_j, bp, bj)) bp = bf_pr, bj = bf_j, wy = bf_y, src = 1;
+                    }
+                    if ((fe << 6) < i0 && better(t_pr, t_j, bp, bj)) bp = t_pr, bj = t_j, wy = t_y, src = 2;
+                }
+                if (cert && bj >= 0 && in_range(wy, bj)) {
+                    if (src == 1) eb.x = bf_e.x, eb.y = bf_y, eb.f = bf_e.y, eb.pw = bf_e.z, have_eb = true;
+                } else {
+                    CCOUNT(3);
+                    if (cert && bj >= 0) CCOUNT(6);
+                    window_best(yi, ylo, true, bp, bj);
+                }
             }
-            for (int o = 32; o > 0; o >>= 1) {
-                const double op = __shfl_xor(bp, o, 64);
-                const int64_t oj = __shfl_xor(bj, o, 64);
-                if (oj >= 0 && (bj < 0 || op < bp || (op == bp && oj > bj))) bp = op, bj = oj;
-            }
+            CPROF(3);
             if (bj >= 0) {
                 int32_t exact, width;
-                const int32_t sc = P.f[bj] + comput_sc(xi, yi_, P.ax[bj], P.ay[bj], P.pen_gap, P.pen_skip, &exact, &width);
+                if (!have_eb) eb = bj == i - 1 ? prev : fetch(bj);
+                const int32_t sc = eb.f + comput_sc(xi, yi, eb.x, eb.y, eb.sp(), P.pen_gap, P.pen_skip, &exact, &width);
                 if (width <= P.bw && sc > max_f) max_f = sc, max_j = bj;
-                const int64_t n_inner = i0 > st_in ? i0 - st_in : 0;
-                if (!exact && n_inner > 0 && yi > 0) {
-                    int n_skip = 0;
-                    bool done = false;
-                    const int32_t ylo = yi - P.max_dist_inner;
+                const int32_t n_inner = i0 > st_in ? i0 - st_in : 0;
+                bool walk = !exact && n_inner > 0 && yi > 0 && P.max_dist_inner > 0;
+                if (walk && iok && it > ih && if_v <= max_f) walk = false;  // no candidate can beat max_f
+                CPROF(5);
+                if (walk) {
+                    CCOUNT(4);
+                    const int32_t ylo_in = yi - P.max_dist_inner;
                     if (!overflow) {
-                        // last list position with y <= yi - 1
-                        int c = 0;
-                        for (int e = lane; e < ni; e += 64) c += lst[e].x < yi;
-                        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-                        for (int pos = c - 1; pos >= 0 && !done; pos -= 64) {
-                            const int e = pos - lane;
-                            int32_t yj = INT32_MIN, jl = 0, sc_l = 0, w_l = INT32_MAX;
-                            int64_t pj = -1;
+                        // walk the list downwards from the last entry with y <= yi - 1
+                        int cnt = 0;
+                        for (int e = lane; e < ni; e += 64) cnt += L(e).x < yi;
+                        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                        int nsk = 0;
+                        for (int top = cnt - 1; top >= 0; top -= 64) {
+                            const int e = top - lane;
+                            const int nl = min(64, top + 1);
+                            int32_t yj = 0, jl = -1, sc_l = 0, w_l = INT32_MAX, pj = -1;
                             if (e >= 0) {
-                                const int2 v = lst[e];
+                                const int2 v = L(e);
                                 yj = v.x, jl = v.y;
-                                const int64_t j = g0 + jl;
+                                const Ent ej = fetch(jl);
                                 int32_t ex;
-                                sc_l = P.f[j] + comput_sc(xi, yi_, P.ax[j], P.ay[j], P.pen_gap, P.pen_skip, &ex, &w_l);
-                                pj = P.p[j];
+                                sc_l = ej.f + comput_sc(xi, yi, ej.x, ej.y, ej.sp(), P.pen_gap, P.pen_skip, &ex, &w_l);
+                                pj = ej.p();
                             }
-                            const int nl = min(64, pos + 1);
-                            for (int l = 0; l < nl; ++l) {
-                                const int32_t yl = __shfl(yj, l, 64);
-                                if (yl < ylo) {
-                                    done = true;
-                                    break;
-                                }
-                                const int32_t wl = __shfl(w_l, l, 64);
-                                if (wl > P.bw) continue;
-                                const int32_t sl = __shfl(sc_l, l, 64);
-                                const int32_t jll = __shfl(jl, l, 64);
-                                const int64_t pl = __shfl(pj, l, 64);
-                                const int64_t j = g0 + jll;
-                                if (sl > max_f) {
-                                    max_f = sl, max_j = j;
-                                    if (n_skip > 0) --n_skip;
-                                } else if (stamp[(int)((j - g0) % kInnerCap)] == (int32_t)i && j >= st_in && j < i0) {
-                                    if (++n_skip > P.max_chn_skip) {
-                                        done = true;
-                                        break;
-                                    }
-                                }
-                                if (pl >= 0 && pl >= st_in && pl < i0) {
-                                    __builtin_amdgcn_wave_barrier();
-                                    if (lane == 0) stamp[(int)((pl - g0) % kInnerCap)] = (int32_t)i;
-                                    __builtin_amdgcn_wave_barrier();
+                            const uint64_t mA = __ballot(e >= 0 && yj < ylo_in);
+                            const int LA = mA ? __ffsll((unsigned long long)mA) - 1 : nl;  // y-bound break
+                            const bool valid = lane < LA && w_l <= P.bw;
+                            // t[p[j]] = i marks (a mark always points later in walk order)
+                            if (valid && pj >= st_in && pj < i0) stamp[pj % kInnerCap] = i;
+                            __builtin_amdgcn_wave_barrier();
+                            const bool stamped = valid && stamp[jl % kInnerCap] == i;
+                            // running max_f before each candidate: exclusive prefix max
+                            int incl = valid ? sc_l : INT32_MIN;
+                            for (int d = 1; d < 64; d <<= 1) {
+                                const int o = __shfl_up(incl, d, 64);
+                                if (lane >= d) incl = max(incl, o);
+                            }
+                            int excl = __shfl_up(incl, 1, 64);
+                            if (lane == 0) excl = INT32_MIN;
+                            excl = max(excl, max_f);
+                            const bool imp = valid && sc_l > excl;
+                            // n_skip: improve -> max(s-1, 0); stamped -> s+1; as max-plus maps s -> max(s+a, b)
+                            int a = imp ? -1 : (valid && stamped ? 1 : 0);
+                            int bb = imp ? 0 : kNegInf;
+                            for (int d = 1; d < 64; d <<= 1) {
+                                const int ao = __shfl_up(a, d, 64), bo = __shfl_up(bb, d, 64);
+                                if (lane >= d) {
+                                    bb = max(bo + a, bb);
+                                    a = ao + a;
                                 }
                             }
+                            const int s = max(nsk + a, bb);
+                            const uint64_t mB = __ballot(valid && !imp && stamped && s > P.max_chn_skip);
+                            const int LB = mB ? __ffsll((unsigned long long)mB) - 1 : 64;
+                            const int lim = min(LA, LB + 1);  // candidates the sequential loop reaches
+                            const uint64_t mI = __ballot(imp && lane < lim);
+                            if (mI) {
+                                const int Lh = 63 - __clzll((long long)mI);
+                                max_f = rl(sc_l, Lh);
+                                max_j = rl(jl, Lh);
+                            }
+                            if (mB || LA < nl) break;
+                            nsk = rl(s, 63);
+                            __builtin_amdgcn_wave_barrier();
                         }
                     } else {
                         // overflow path: next candidate = largest (y, idx) below the previous one
-                        int32_t cy = yi, cj = INT32_MIN;  // exclusive upper bound (yi - 1, +inf) == (yi, -inf)
+                        int n_skip = 0;
+                        int32_t cy_ = yi, cj = INT32_MIN;
                         bool first = true;
                         for (;;) {
                             int32_t by = INT32_MIN, bjl = INT32_MIN;
-                            for (int64_t j = st_in + lane; j < i0; j += 64) {
-                                const int32_t yj = (int32_t)P.ay[j];
-                                const int32_t jl = (int32_t)(j - g0);
-                                const bool below = first ? (yj <= yi - 1) : key_less(yj, jl, cy, cj);
-                                if (below && (bjl == INT32_MIN || key_less(by, bjl, yj, jl))) by = yj, bjl = jl;
+                            for (int32_t j = st_in + lane; j < i0; j += 64) {
+                                const int32_t yj = fetch(j).y;
+                                const bool below = first ? (yj <= yi - 1) : key_less(yj, j, cy_, cj);
+                                if (below && (bjl == INT32_MIN || key_less(by, bjl, yj, j))) by = yj, bjl = j;
                             }
                             for (int o = 32; o > 0; o >>= 1) {
                                 const int32_t oy = __shfl_xor(by, o, 64), oj = __shfl_xor(bjl, o, 64);
@@ -240,28 +1021,34 @@ __global__ __launch_bounds__(256) void chain_groups_kernel(ChainParams P) {
                             }
                             if (bjl == INT32_MIN) break;
                             first = false;
-                            cy = by, cj = bjl;
-                            if (by < ylo) break;
-                            const int64_t j = g0 + bjl;
+                            cy_ = by, cj = bjl;
+                            if (by < ylo_in) break;
+                            const Ent ej = fetch(bjl);
                             int32_t ex, wl;
-                            const int32_t sl = P.f[j] + comput_sc(xi, yi_, P.ax[j], P.ay[j], P.pen_gap, P.pen_skip, &ex, &wl);
+                            const int32_t sl = ej.f + comput_sc(xi, yi, ej.x, ej.y, ej.sp(), P.pen_gap, P.pen_skip, &ex, &wl);
                             if (wl <= P.bw) {
                                 if (sl > max_f) {
-                                    max_f = sl, max_j = j;
+                                    max_f = sl, max_j = bjl;
                                     if (n_skip > 0) --n_skip;
-                                } else if (P.t_global[j] == (int32_t)i) {
+                                } else if (ld_l2(P.t_global + g0 + bjl) == i) {
                                     if (++n_skip > P.max_chn_skip) break;
                                 }
-                                const int64_t pl = P.p[j];
-                                if (pl >= 0) P.t_global[pl] = (int32_t)i;  // every lane writes: program order
+                                if (ej.p() >= 0) P.t_global[g0 + ej.p()] = i;  // every lane writes: program order
                             }
                         }
                     }
                 }
             }
-            P.f[i] = max_f;  // every lane stores: later loads by any lane follow its own store
-            P.p[i] = max_j;
+            CPROF(4);
+            // every lane stores the same values: later global loads by any lane see them
+            P.f[g0 + i] = max_f;
+            P.p[g0 + i] = max_j < 0 ? -1 : g0 + max_j;
+            prev.x = xi, prev.y = yi, prev.f = max_f, prev.pw = (int32_t)((uint32_t)(max_j + 1) | (uint32_t)span_i << 24);
+            if (lane == 0) ring[i & kRingMask] = make_int4(prev.x, prev.y, prev.f, prev.pw);
+            __builtin_amdgcn_wave_barrier();
+            ++i;
         }
+        CPROF_FLUSH;
     }
 }
 
@@ -334,23 +1121,25 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
 
 }  // namespace
 
-int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *g_start, const int32_t *order,
-                 int32_t n_work, int32_t *f, int64_t *p, int32_t *t_global, int max_dist, int max_dist_inner, int bw,
-                 int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip, int64_t n_anchors) {
+int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *g_start, const uint8_t *g_qfirst,
+                 const int32_t *order, int32_t n_work, int32_t *f, int64_t *p, int32_t *t_global, int max_dist,
+                 int max_dist_inner, int bw, int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip,
+                 int64_t n_anchors, int64_t n_groups) {
     if (n_work <= 0) return HYMET_OK;
-    DevBuf cnt;
+    DevBuf cnt, sum;
+    const size_t n_sum = (size_t)(n_anchors >> 6) + (size_t)n_groups + 2;
+    HY_HIP(sum.alloc(16 * kSumInts * n_sum, ctx->stream));
     HY_HIP(cnt.alloc(4, ctx->stream));
     HY_HIP(hipMemsetAsync(cnt.p, 0, 4, ctx->stream));
     if (max_dist < bw) max_dist = bw;
     if (max_dist_inner <= 0 || max_dist_inner >= max_dist) max_dist_inner = 0;
-    ChainParams P{ax, ay, g_start, order, n_work, cnt.as<int32_t>(), f, p, t_global, max_dist, max_dist_inner, bw,
-                  max_chn_skip, cap_rmq_size, pen_gap, pen_skip};
-    const size_t lds = kWavesPerBlock * kInnerCap * (sizeof(int2) + sizeof(int32_t));
-    int64_t blocks = cdiv(n_work, kWavesPerBlock);
-    const int64_t cap = (int64_t)ctx->n_cu * 6;
+    ChainParams P{ax, ay, g_start, g_qfirst, order, n_work, cnt.as<int32_t>(), f, p, t_global, sum.as<int4>(), max_dist, max_dist_inner, bw, max_chn_skip, cap_rmq_size, pen_gap, pen_skip};
+    // one wave per block; LDS (kChainLds ~20 KB) allows 8 resident waves per CU
+    int64_t blocks = n_work;
+    const int64_t cap = (int64_t)ctx->n_cu * 8;
     if (blocks > cap) blocks = cap;
-    ProfScope _ps(ctx, "mm_chain", 28.0 * (double)n_anchors);  // x,y read + f,p write per anchor
-    hipLaunchKernelGGL(chain_groups_kernel, dim3((unsigned)blocks), dim3(64 * kWavesPerBlock), lds, ctx->stream, P);
+    ProfScope _ps(ctx, max_dist > 10000 ? "mm_chain_long" : "mm_chain", 28.0 * (double)n_anchors);  // x,y read + f,p write per anchor
+    hipLaunchKernelGGL(chain_groups_kernel, dim3((unsigned)blocks), dim3(64), kChainLds, ctx->stream, P);
     HY_CHECK_LAUNCH("chain_groups_kernel");
     return HYMET_OK;
 }

@@ -28,9 +28,10 @@ struct hymet_mm_result {
 namespace hymet {
 namespace mm {
 
-int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *g_start, const int32_t *order,
-                 int32_t n_work, int32_t *f, int64_t *p, int32_t *t_global, int max_dist, int max_dist_inner, int bw,
-                 int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip, int64_t n_anchors);
+int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *g_start, const uint8_t *g_qfirst,
+                 const int32_t *order, int32_t n_work, int32_t *f, int64_t *p, int32_t *t_global, int max_dist,
+                 int max_dist_inner, int bw, int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip,
+                 int64_t n_anchors, int64_t n_groups);
 int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, const int64_t *p, int32_t *t,
                      const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, int min_cnt, int min_sc,
                      int max_drop, int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first, int32_t *n_chains);
@@ -279,12 +280,23 @@ __global__ void group_flag_kernel(const uint64_t *k1, int64_t n, uint32_t *flag)
     if (i < n) flag[i] = (i == 0 || k1[i] != k1[i - 1]) ? 1u : 0u;
 }
 
+__global__ void group_flag_x_kernel(const uint64_t *x, int64_t n, uint32_t *flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = (i == 0 || (x[i] >> 32) != (x[i - 1] >> 32)) ? 1u : 0u;
+}
+
 __global__ void group_start_kernel(const uint32_t *flag, const int64_t *gpos, int64_t n, int64_t *g_start, int32_t *gid) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t g = gpos[i] + flag[i] - 1;
     gid[i] = (int32_t)g;
     if (flag[i]) g_start[g] = i;
+}
+
+// groups that start their query's anchor array (lchain.c's krmq index-0 quirk is per query)
+__global__ void group_qfirst_kernel(const int64_t *qoff, int n_q, const int32_t *gid, uint8_t *out) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n_q && qoff[q] < qoff[q + 1]) out[gid[qoff[q]]] = 1;
 }
 
 __global__ void group_size_kernel(const int64_t *g_start, int32_t G, int min_cnt, uint32_t *key, uint32_t *gidx,
@@ -493,6 +505,12 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         uint32_t *kp = skey.as<uint32_t>(), *ka = skey2.as<uint32_t>(), *vp = sidx.as<uint32_t>(), *va = sidx2.as<uint32_t>();
         rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 32);
         if (rc) return rc;
+        {  // the chaining kernel packs local predecessor indices in 24 bits
+            uint32_t k0 = 0;
+            HY_HIP(hipMemcpyAsync(&k0, kp, 4, hipMemcpyDeviceToHost, ctx->stream));
+            HY_HIP(hipStreamSynchronize(ctx->stream));
+            HY_ARG(~k0 < (1u << 24) - 1, "hymet_mm_map: an anchor group exceeds 2^24 anchors");
+        }
         DevBuf f, p, t;
         HY_HIP(f.alloc(4 * (size_t)n, ctx->stream));
         HY_HIP(p.alloc(8 * (size_t)n, ctx->stream));
@@ -500,9 +518,14 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(hipMemsetAsync(f.p, 0, 4 * (size_t)n, ctx->stream));
         HY_HIP(hipMemsetAsync(p.p, 0xFF, 8 * (size_t)n, ctx->stream));
         HY_HIP(hipMemsetAsync(t.p, 0xFF, 4 * (size_t)n, ctx->stream));
-        rc = launch_chain(ctx, A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), g_start.as<int64_t>(), (const int32_t *)vp,
+        DevBuf qfirst;
+        HY_HIP(qfirst.alloc((size_t)G, ctx->stream));
+        HY_HIP(hipMemsetAsync(qfirst.p, 0, (size_t)G, ctx->stream));
+        LAUNCH1(group_qfirst_kernel, n_q, A.d_off.as<int64_t>(), n_q, gid.as<int32_t>(), qfirst.as<uint8_t>());
+        rc = launch_chain(ctx, A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
+                          (const int32_t *)vp,
                           (int32_t)n_work, f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(), opt->max_gap,
-                          opt->rmq_inner_dist, bw, opt->max_chain_skip, opt->rmq_size_cap, pen_gap, pen_skip, n);
+                          opt->rmq_inner_dist, bw, opt->max_chain_skip, opt->rmq_size_cap, pen_gap, pen_skip, n, G);
         if (rc) return rc;
         // z = anchors with f >= min_sc ordered by (group, f, idx)
         DevBuf zflag, zpos;
@@ -620,7 +643,8 @@ namespace mm {
 int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const uint64_t *cu, const int64_t *cboff,
                    const int64_t *qc, const int64_t *qb, const uint64_t *mini_pos, const int64_t *mp_off, const int64_t *qlen,
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
-                   int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs);
+                   int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
+                   int64_t NB, int64_t NC, int64_t NM);
 
 namespace {
 __global__ void rechain_flag_kernel(const uint64_t *by, const uint64_t *cu, const int64_t *qc, const int64_t *qb,
@@ -863,7 +887,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
                                 C.d_qc.as<int64_t>(), C.d_qb.as<int64_t>(), mini_pos.as<uint64_t>(), mp_off.as<int64_t>(),
                                 d_qlen.as<int64_t>(), d_hash.as<uint32_t>(), rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
                                 z.p, rg.as<hymet_mm_reg>(), wv.as<int32_t>(), cov.as<uint64_t>(), tmp.as<int32_t>(),
-                                nr.as<int32_t>());
+                                nr.as<int32_t>(), C.n_anchor, NC, NM);
         if (r2) return r2;
         regs.resize(NC);
         nreg.resize(n_q);
@@ -890,6 +914,59 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
         for (int i = 0; i < nr; i++) res->regs.push_back(src[c0 + i]);
         res->reg_off[q + 1] = (int64_t)res->regs.size();
     }
+    return HYMET_OK;
+}
+
+int hymet_mm_chain_dp(hymet_ctx *ctx, const uint64_t *h_x, const uint64_t *h_y, int64_t n, int max_dist,
+                      int max_dist_inner, int bw, int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip,
+                      int32_t *h_f, int64_t *h_p) {
+    HY_ARG(ctx && (n == 0 || (h_x && h_y && h_f && h_p)), "hymet_mm_chain_dp: null argument");
+    HY_ARG(n >= 0 && n < INT32_MAX, "hymet_mm_chain_dp: n out of range");
+    if (n == 0) return HYMET_OK;
+    HY_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    DevBuf x, y, flag, gpos, gid, g_start, qfirst, skey, sidx, swork, skey2, sidx2, f, p, t;
+    HY_HIP(x.alloc(8 * (size_t)n, st));
+    HY_HIP(y.alloc(8 * (size_t)n, st));
+    HY_HIP(hipMemcpyAsync(x.p, h_x, 8 * (size_t)n, hipMemcpyHostToDevice, st));
+    HY_HIP(hipMemcpyAsync(y.p, h_y, 8 * (size_t)n, hipMemcpyHostToDevice, st));
+    HY_HIP(flag.alloc(4 * (size_t)n, st));
+    LAUNCH1(group_flag_x_kernel, n, x.as<uint64_t>(), n, flag.as<uint32_t>());
+    int64_t G = 0;
+    int rc = scan_flags(ctx, flag.as<uint32_t>(), n, gpos, &G);
+    if (rc) return rc;
+    HY_HIP(g_start.alloc(8 * (size_t)(G + 1), st));
+    HY_HIP(gid.alloc(4 * (size_t)n, st));
+    LAUNCH1(group_start_kernel, n, flag.as<uint32_t>(), gpos.as<int64_t>(), n, g_start.as<int64_t>(), gid.as<int32_t>());
+    HY_HIP(hipMemcpyAsync(g_start.as<int64_t>() + G, &n, 8, hipMemcpyHostToDevice, st));
+    HY_HIP(qfirst.alloc((size_t)G, st));
+    HY_HIP(hipMemsetAsync(qfirst.p, 0, (size_t)G, st));
+    HY_HIP(hipMemsetAsync(qfirst.p, 1, 1, st));  // one query: group 0 holds anchor 0
+    for (DevBuf *b : {&skey, &sidx, &swork, &skey2, &sidx2}) HY_HIP(b->alloc(4 * (size_t)G, st));
+    LAUNCH1(group_size_kernel, G, g_start.as<int64_t>(), (int32_t)G, 1, skey.as<uint32_t>(), sidx.as<uint32_t>(),
+            swork.as<uint32_t>());
+    uint32_t *kp = skey.as<uint32_t>(), *ka = skey2.as<uint32_t>(), *vp = sidx.as<uint32_t>(), *va = sidx2.as<uint32_t>();
+    rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 32);
+    if (rc) return rc;
+    {  // the chaining kernel packs local predecessor indices in 24 bits
+        uint32_t k0 = 0;
+        HY_HIP(hipMemcpyAsync(&k0, kp, 4, hipMemcpyDeviceToHost, st));
+        HY_HIP(hipStreamSynchronize(st));
+        HY_ARG(~k0 < (1u << 24) - 1, "hymet_mm_chain_dp: an anchor group exceeds 2^24 anchors");
+    }
+    HY_HIP(f.alloc(4 * (size_t)n, st));
+    HY_HIP(p.alloc(8 * (size_t)n, st));
+    HY_HIP(t.alloc(4 * (size_t)n, st));
+    HY_HIP(hipMemsetAsync(f.p, 0, 4 * (size_t)n, st));
+    HY_HIP(hipMemsetAsync(p.p, 0xFF, 8 * (size_t)n, st));
+    HY_HIP(hipMemsetAsync(t.p, 0xFF, 4 * (size_t)n, st));
+    rc = launch_chain(ctx, x.as<uint64_t>(), y.as<uint64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
+                      (const int32_t *)vp, (int32_t)G, f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(), max_dist,
+                      max_dist_inner, bw, max_chn_skip, cap_rmq_size, pen_gap, pen_skip, n, G);
+    if (rc) return rc;
+    HY_HIP(hipMemcpyAsync(h_f, f.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+    HY_HIP(hipMemcpyAsync(h_p, p.p, 8 * (size_t)n, hipMemcpyDeviceToHost, st));
+    HY_HIP(hipStreamSynchronize(st));
     return HYMET_OK;
 }
 

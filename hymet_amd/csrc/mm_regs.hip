@@ -1,10 +1,17 @@
 // Per-query region selection (minimap2 hit.c / map.c after chaining):
 // mm_gen_regs (score + hash order), mm_reg_set_coor / mm_cal_fuzzy_len, mm_set_parent,
 // mm_select_sub (+ mm_sync_regs), mm_est_err, mm_filter_strand_retained, mm_set_mapq.
-// One thread per query: a query has few chains (tens) and every step is an O(n^2)-at-most
-// scan over them; the queries are independent, so the launch is wide.  Scratch lives in
-// global memory at the query's chain range.  Float/double arithmetic is written in the
-// order of hit.c (-ffp-contract=off).
+// Everything that walks a chain's anchors is anchor-parallel and runs first:
+//   chain_anchor_kernel  one thread per chained anchor: its mlen/blen contribution
+//                        (mm_reg_set_coor), its index among the query minimizers (mm_est_err's
+//                        get_mini_idx binary search);
+//   chain_viol_kernel    one thread per anchor: the first anchor, in est_err's walking order,
+//                        whose minimizer index does not increase -- est_err's sequential
+//                        two-pointer walk matches exactly the prefix before it;
+//   query_sumk_kernel    per-query sum of minimizer spans (avg_k).
+// regions_kernel then runs one thread per query: a query has few chains (tens) and every step
+// left is an O(n^2)-at-most scan over them.  Scratch lives in global memory at the query's
+// chain range.  Float/double arithmetic is written in the order of hit.c (-ffp-contract=off).
 #include "mm_common.hpp"
 
 namespace hymet {
@@ -49,6 +56,16 @@ __device__ void heap_sort(T *a, int64_t n, Less less) {
     }
 }
 
+__device__ __forceinline__ int64_t upper_idx(const int64_t *off, int64_t n, int64_t v) {  // last s with off[s] <= v
+    int64_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= v) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
 struct RegParams {
     const uint64_t *bx, *by;       // chained anchors, chain by chain
     const uint64_t *cu;            // score<<32 | count per chain
@@ -71,9 +88,13 @@ struct RegParams {
     uint64_t *cov;
     int32_t *tmp;
     int32_t *n_regs;
+    // per-chain anchor statistics (chain_anchor_kernel / chain_viol_kernel)
+    const int32_t *c_mlen, *c_blen, *c_st, *c_last, *c_fv;
+    const uint64_t *q_sumk;
 };
 
-__device__ void set_coor(hymet_mm_reg *r, int32_t qlen, const uint64_t *ax, const uint64_t *ay) {
+__device__ void set_coor(hymet_mm_reg *r, int32_t qlen, const uint64_t *ax, const uint64_t *ay, int32_t mlen,
+                         int32_t blen) {
     const int32_t k = r->as, q_span = (int32_t)(ay[k] >> 32 & 0xff);
     r->rev = (int32_t)(ax[k] >> 63);
     r->rid = (int32_t)(ax[k] << 1 >> 33);
@@ -86,14 +107,19 @@ __device__ void set_coor(hymet_mm_reg *r, int32_t qlen, const uint64_t *ax, cons
         r->qs = qlen - ((int32_t)ay[k + r->cnt - 1] + 1);
         r->qe = qlen - ((int32_t)ay[k] + 1 - q_span);
     }
-    r->mlen = r->blen = (int32_t)(ay[r->as] >> 32 & 0xff);
-    for (int i = r->as + 1; i < r->as + r->cnt; ++i) {
-        const int span = (int)(ay[i] >> 32 & 0xff);
-        const int tl = (int32_t)ax[i] - (int32_t)ax[i - 1];
-        const int ql = (int32_t)ay[i] - (int32_t)ay[i - 1];
-        r->blen += tl > ql ? tl : ql;
-        r->mlen += tl > span && ql > span ? span : tl < ql ? tl : ql;
+    r->mlen = mlen;  // span(first) + sum over consecutive anchors (chain_anchor_kernel)
+    r->blen = blen;
+}
+
+// chain index of a region: its anchors start at b0 + as (chains of the query: [c0, c1))
+__device__ __forceinline__ int64_t chain_of(const int64_t *cboff, int64_t c0, int64_t c1, int64_t a) {
+    int64_t lo = c0, hi = c1 - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (cboff[mid] <= a) lo = mid;
+        else hi = mid - 1;
     }
+    return lo;
 }
 
 __device__ int get_mini_idx(int qlen, uint64_t ax, uint64_t ay, int32_t n, const uint64_t *mini_pos) {
@@ -107,6 +133,70 @@ __device__ int get_mini_idx(int qlen, uint64_t ax, uint64_t ay, int32_t n, const
         else return m;
     }
     return -1;
+}
+
+struct AnchorStatParams {
+    const uint64_t *bx, *by, *cu;
+    const int64_t *cboff, *qb, *qlen, *mp_off;
+    const uint64_t *mini_pos;
+    int64_t NB, NC;
+    int n_q;
+    int32_t *a_idx, *a_chain, *c_mlen, *c_blen, *c_st, *c_last;
+};
+
+__global__ void chain_anchor_kernel(AnchorStatParams P) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P.NB) return;
+    const int64_t c = upper_idx(P.cboff, P.NC, b);
+    const int64_t q = upper_idx(P.qb, P.n_q, b);
+    const int32_t cnt = (int32_t)P.cu[c];
+    const int32_t pos = (int32_t)(b - P.cboff[c]);
+    const uint64_t x = P.bx[b], y = P.by[b];
+    const int32_t span = (int32_t)(y >> 32 & 0xff);
+    int32_t dm, db;
+    if (pos == 0) {
+        dm = db = span;
+    } else {  // hit.c mm_reg_set_coor
+        const int32_t tl = (int32_t)x - (int32_t)P.bx[b - 1];
+        const int32_t ql = (int32_t)y - (int32_t)P.by[b - 1];
+        db = tl > ql ? tl : ql;
+        dm = tl > span && ql > span ? span : tl < ql ? tl : ql;
+    }
+    atomicAdd(&P.c_mlen[c], dm);
+    atomicAdd(&P.c_blen[c], db);
+    const int64_t m0 = P.mp_off[q];
+    const int32_t nm = (int32_t)(P.mp_off[q + 1] - m0);
+    const int32_t idx = nm > 0 ? get_mini_idx((int)P.qlen[q], x, y, nm, P.mini_pos + m0) : -1;
+    P.a_idx[b] = idx;
+    P.a_chain[b] = (int32_t)c;
+    const int32_t kk = (x >> 63) ? cnt - 1 - pos : pos;  // est_err walking order
+    if (kk == 0) P.c_st[c] = idx;
+    if (kk == cnt - 1) P.c_last[c] = idx;
+}
+
+// est_err's loop `for (k=1, j=st+1; j<nm && k<cnt; ++j) if (idx(k) == j) ++k, ++n_match;`
+// matches anchor k iff idx(1..k) strictly increase from st; the first anchor that does not
+// (or has no minimizer) stalls it to the end.
+__global__ void chain_viol_kernel(const uint64_t *bx, const uint64_t *cu, const int64_t *cboff, const int32_t *a_idx,
+                                  const int32_t *a_chain, int64_t NB, int32_t *c_fv) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= NB) return;
+    const int32_t c = a_chain[b];
+    const int32_t cnt = (int32_t)cu[c];
+    const int32_t pos = (int32_t)(b - cboff[c]);
+    const bool rev = bx[b] >> 63;
+    const int32_t kk = rev ? cnt - 1 - pos : pos;
+    if (kk == 0) return;
+    const int32_t cur = a_idx[b], prev = a_idx[rev ? b + 1 : b - 1];
+    if (cur < 0 || cur <= prev) atomicMin(&c_fv[c], kk);
+}
+
+__global__ void query_sumk_kernel(const uint64_t *mini_pos, const int64_t *mp_off, int n_q, int64_t NM,
+                                  unsigned long long *sumk) {
+    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= NM) return;
+    const int64_t q = upper_idx(mp_off, n_q, m);
+    atomicAdd(&sumk[q], (unsigned long long)(mini_pos[m] >> 32 & 0xff));
 }
 
 __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
@@ -154,7 +244,8 @@ __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
         ri->strand_retained = 0;
         ri->mapq = 0;
         ri->pad = 0;
-        set_coor(ri, qlen, ax, ay);
+        const int64_t c = chain_of(P.cboff, c0, c1, b0 + ri->as);
+        set_coor(ri, qlen, ax, ay, P.c_mlen[c], P.c_blen[c]);
     }
     // ---- mm_set_parent (mask_level, mask_len; no alignment: no dp_max branch)
     {
@@ -238,30 +329,24 @@ __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
         }
         n = k;
     }
-    // ---- mm_est_err
+    // ---- mm_est_err (the per-anchor walk was done by chain_anchor_kernel / chain_viol_kernel)
     {
         const int64_t m0 = P.mp_off[q];
         const int32_t nm = (int32_t)(P.mp_off[q + 1] - m0);
-        const uint64_t *mp = P.mini_pos + m0;
         if (nm > 0) {
-            uint64_t sum_k = 0;
-            for (int i = 0; i < nm; ++i) sum_k += mp[i] >> 32 & 0xff;
+            const uint64_t sum_k = P.q_sumk[q];
             const float avg_k = __fdiv_rn((float)sum_k, (float)nm);
             for (int i = 0; i < n; ++i) {
                 hymet_mm_reg *ri = &r[i];
                 ri->div = -1.0f;
                 if (ri->cnt == 0) continue;
-                const int a0 = ri->rev ? ri->as + ri->cnt - 1 : ri->as;
-                int32_t st = get_mini_idx(qlen, ax[a0], ay[a0], nm, mp), en = st;
+                const int64_t c = chain_of(P.cboff, c0, c1, b0 + ri->as);
+                const int32_t st = P.c_st[c];
                 if (st < 0) continue;
+                const int32_t fv = P.c_fv[c] < ri->cnt ? P.c_fv[c] : ri->cnt;
+                const int32_t n_match = fv;
+                const int32_t en = fv == ri->cnt ? P.c_last[c] : nm - 1;
                 const int32_t l_ref = (int32_t)P.ref_len[ri->rid];
-                int32_t j, kk, n_match;
-                for (kk = 1, j = st + 1, n_match = 1; j < nm && kk < ri->cnt; ++j) {
-                    const int aa = ri->rev ? ri->as + ri->cnt - 1 - kk : ri->as + kk;
-                    const int32_t x = get_mini_idx(qlen, ax[aa], ay[aa], nm, mp);
-                    if (x == j) ++kk, ++n_match;
-                    en = j;
-                }
                 int32_t n_tot = en - st + 1;
                 if ((float)ri->qs > avg_k && (float)ri->rs > avg_k) ++n_tot;
                 if ((float)(qlen - ri->qe) > avg_k && (float)(l_ref - ri->re) > avg_k) ++n_tot;
@@ -312,13 +397,42 @@ __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
 int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const uint64_t *cu, const int64_t *cboff,
                    const int64_t *qc, const int64_t *qb, const uint64_t *mini_pos, const int64_t *mp_off, const int64_t *qlen,
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
-                   int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs) {
+                   int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
+                   int64_t NB, int64_t NC, int64_t NM) {
     if (n_q <= 0) return HYMET_OK;
+    hipStream_t st = ctx->stream;
+    DevBuf a_idx, a_chain, cst, sumk;
+    HY_HIP(a_idx.alloc(4 * (size_t)(NB + 1), st));
+    HY_HIP(a_chain.alloc(4 * (size_t)(NB + 1), st));
+    HY_HIP(cst.alloc(4 * 5 * (size_t)(NC + 1), st));
+    HY_HIP(sumk.alloc(8 * (size_t)n_q, st));
+    int32_t *c_mlen = cst.as<int32_t>(), *c_blen = c_mlen + (NC + 1), *c_st = c_blen + (NC + 1), *c_last = c_st + (NC + 1),
+            *c_fv = c_last + (NC + 1);
+    HY_HIP(hipMemsetAsync(c_mlen, 0, 8 * (size_t)(NC + 1), st));
+    HY_HIP(hipMemsetAsync(c_fv, 0x7f, 4 * (size_t)(NC + 1), st));
+    HY_HIP(hipMemsetAsync(sumk.p, 0, 8 * (size_t)n_q, st));
+    {
+        ProfScope _ps(ctx, "mm_chain_stats", (double)NB * (16.0 + 16.0 + 8.0) + (double)NM * 8.0);
+        if (NB > 0) {
+            AnchorStatParams A{bx, by, cu, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, a_idx.as<int32_t>(),
+                               a_chain.as<int32_t>(), c_mlen, c_blen, c_st, c_last};
+            hipLaunchKernelGGL(chain_anchor_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A);
+            HY_CHECK_LAUNCH("chain_anchor_kernel");
+            hipLaunchKernelGGL(chain_viol_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, bx, cu, cboff,
+                               a_idx.as<int32_t>(), a_chain.as<int32_t>(), NB, c_fv);
+            HY_CHECK_LAUNCH("chain_viol_kernel");
+        }
+        if (NM > 0) {
+            hipLaunchKernelGGL(query_sumk_kernel, dim3((unsigned)cdiv(NM, 256)), dim3(256), 0, st, mini_pos, mp_off, n_q, NM,
+                               sumk.as<unsigned long long>());
+            HY_CHECK_LAUNCH("query_sumk_kernel");
+        }
+    }
     RegParams P{bx, by, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
-                tmp, n_regs};
+                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk.as<uint64_t>()};
     ProfScope _ps(ctx, "mm_regions");
-    hipLaunchKernelGGL(regions_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, ctx->stream, P);
+    hipLaunchKernelGGL(regions_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P);
     HY_CHECK_LAUNCH("regions_kernel");
     return HYMET_OK;
 }

@@ -146,6 +146,14 @@ int hymet_mm_result_size(const hymet_mm_result *res, int64_t *n_regs);
 int hymet_mm_result_copy(const hymet_mm_result *res, int64_t *h_off, int32_t *h_rep_len,
                          hymet_mm_reg *h_regs);
 int hymet_mm_result_destroy(hymet_mm_result *res);
+/* Chaining DP alone (lchain.c mg_lchain_rmq's f[]/p[], the stage inside hymet_mm_map), for
+ * parity tests and kernel timing: n anchors (x, y as minimap2 packs them) of ONE query,
+ * sorted by x; groups are runs of equal x>>32.  max_dist/bw are given as mg_lchain_rmq
+ * receives them (first pass: max_gap, bw; long join: max_gap, bw_long).  Host arrays,
+ * synchronous; h_p holds anchor indices or -1. */
+int hymet_mm_chain_dp(hymet_ctx *ctx, const uint64_t *h_x, const uint64_t *h_y, int64_t n, int max_dist,
+                      int max_dist_inner, int bw, int max_chn_skip, int cap_rmq_size, float pen_gap,
+                      float pen_skip, int32_t *h_f, int64_t *h_p);
 
 /* --------------------------------------------------- weighted LCA (classify)
  * Replaces the per-query loop of scripts/classification_cami.py:290-308 (+ _weighted_lca

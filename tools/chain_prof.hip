@@ -1,0 +1,115 @@
+// Section-level cycle profile of chain_groups_kernel (s_memtime around each stage of the
+// per-anchor loop) on ONE group.  Build (tools/chain_prof.sh):
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -DHYMET_CHAIN_PROF -I include \
+//         tools/chain_prof.hip -o tools/chain_prof
+// Input: raw n x (x, y) uint64 anchors (tools/bench_chain.py --dump FILE).
+#include "../hymet_amd/csrc/mm_chain.hip"
+
+#include <cstdio>
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+using namespace hymet::mm;
+
+#define CK(x)                                                               \
+    do {                                                                    \
+        hipError_t e_ = (x);                                                \
+        if (e_ != hipSuccess) {                                             \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));         \
+            return 1;                                                       \
+        }                                                                   \
+    } while (0)
+
+int main(int argc, char **argv) {
+    if (argc < 3) {
+        fprintf(stderr, "usage: chain_prof anchors.bin bw\n");
+        return 2;
+    }
+    FILE *fp = fopen(argv[1], "rb");
+    if (!fp) return 2;
+    std::vector<uint64_t> a;
+    uint64_t v[2];
+    while (fread(v, 8, 2, fp) == 2) a.push_back(v[0]), a.push_back(v[1]);
+    fclose(fp);
+    const int64_t n = (int64_t)a.size() / 2;
+    const int bw = atoi(argv[2]);
+    std::vector<uint64_t> hx(n), hy(n);
+    for (int64_t i = 0; i < n; i++) hx[i] = a[2 * i], hy[i] = a[2 * i + 1];
+    uint64_t *dx, *dy;
+    int64_t *gs, *dp;
+    int32_t *order, *cnt, *df, *dt;
+    uint8_t *qf;
+    int4 *sum;
+    const size_t ns = (size_t)(n >> 6) + (size_t)n / 2 + 4;
+    CK(hipMalloc(&dx, 8 * n));
+    CK(hipMalloc(&dy, 8 * n));
+    CK(hipMalloc(&gs, 16));
+    CK(hipMalloc(&dp, 8 * n));
+    CK(hipMalloc(&order, 4));
+    CK(hipMalloc(&cnt, 4));
+    CK(hipMalloc(&df, 4 * n));
+    CK(hipMalloc(&dt, 4 * n));
+    CK(hipMalloc(&qf, 1));
+    CK(hipMalloc(&sum, 16 * kSumInts * ns));
+    CK(hipMemcpy(dx, hx.data(), 8 * n, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dy, hy.data(), 8 * n, hipMemcpyHostToDevice));
+    // groups = runs of equal x >> 32, work list by size descending, group 0 holds anchor 0
+    std::vector<int64_t> h_gs;
+    for (int64_t i = 0; i < n; i++)
+        if (i == 0 || (hx[i] >> 32) != (hx[i - 1] >> 32)) h_gs.push_back(i);
+    const int G = (int)h_gs.size();
+    h_gs.push_back(n);
+    std::vector<int32_t> h_order(G);
+    for (int g = 0; g < G; g++) h_order[g] = g;
+    std::sort(h_order.begin(), h_order.end(), [&](int a, int b) { return h_gs[a + 1] - h_gs[a] > h_gs[b + 1] - h_gs[b]; });
+    std::vector<uint8_t> h_qf(G, 0);
+    h_qf[0] = 1;
+    CK(hipFree(gs));
+    CK(hipFree(order));
+    CK(hipFree(qf));
+    CK(hipMalloc(&gs, 8 * (G + 1)));
+    CK(hipMalloc(&order, 4 * G));
+    CK(hipMalloc(&qf, G));
+    CK(hipMemcpy(gs, h_gs.data(), 8 * (G + 1), hipMemcpyHostToDevice));
+    CK(hipMemcpy(order, h_order.data(), 4 * G, hipMemcpyHostToDevice));
+    CK(hipMemcpy(qf, h_qf.data(), G, hipMemcpyHostToDevice));
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int nblk = std::min(G, prop.multiProcessorCount * 8);
+    int max_dist = 10000 < bw ? bw : 10000;
+    for (int rep = 0; rep < 2; rep++) {
+        unsigned long long z[32] = {0};
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_prof), z, sizeof(z)));
+        CK(hipMemset(cnt, 0, 4));
+        CK(hipMemset(df, 0, 4 * n));
+        CK(hipMemset(dp, 0xFF, 8 * n));
+        CK(hipMemset(dt, 0xFF, 4 * n));
+        ChainParams P{dx, dy, gs, qf, order, G, cnt, df, dp, dt, sum, max_dist, 1000, bw, 25, 100000, 0.12f, 0.0f};
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        CK(hipEventRecord(e0, 0));
+        hipLaunchKernelGGL(chain_groups_kernel, dim3(nblk), dim3(64), kChainLds, 0, P);
+        CK(hipGetLastError());
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(g_chain_prof), sizeof(z)));
+        const char *names[8] = {"i0-advance", "st+head", "st_in", "rmq", "walk", "winner+cert", "st_in-probe", "loop/batch"};
+        double tot = 0;
+        for (int k = 0; k < 8; k++) tot += (double)z[k];
+        printf("n=%lld groups=%d bw=%d kernel %.2f ms = %.0f ns/anchor; %.0f cycles/anchor\n", (long long)n, G, bw, ms, ms * 1e6 / n,
+               tot / n);
+        for (int k = 0; k < 8; k++)
+            if (z[k]) printf("  %-12s %8.0f cyc/anchor  %5.1f%%\n", names[k], (double)z[k] / n, 100.0 * z[k] / tot);
+        const char *cn[8] = {"global fetch", "list ins general", "list erase general", "rmq full path", "walk",
+                             "head suffix", "cert y-fail", "batches"};
+        for (int k = 0; k < 8; k++) printf("  %-20s %8.4f per anchor\n", cn[k], (double)z[8 + k] / n);
+        const char *cn2[11] = {"batch attempts", "pre: cert", "pre: b0 != prev", "pre: walk", "fail: x same", "fail: y range",
+                               "fail: gap/width", "fail: cand", "fail: walk", "fail: list", "accepted"};
+        for (int k = 0; k < 11; k++) printf("  %-20s %8.4f per anchor\n", cn2[k], (double)z[16 + k] / n);
+    }
+    return 0;
+}
