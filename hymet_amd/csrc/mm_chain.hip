@@ -42,6 +42,9 @@
 // anchors ordered by (f, idx) descending (canonical T3).
 #include "mm_common.hpp"
 
+#include <cstdlib>
+#include <string>
+
 namespace hymet {
 namespace mm {
 namespace {
@@ -1056,39 +1059,26 @@ struct BacktrackParams {
     const int64_t *g_start;
     const int32_t *f;
     const int64_t *p;
-    int32_t *t;
-    const int64_t *z_off;   // per group: start of its (f, idx)-ascending z list
-    const int32_t *z_idx;   // anchor indices ordered by (group, f, idx) ascending
+    int32_t *t;                // zeroed by the caller
+    const int64_t *z_off;      // per group: start of its (f, idx)-ascending z list
+    const int32_t *z_idx;      // anchor indices ordered by (group, f, idx) ascending
     int32_t n_groups;
     int min_cnt, min_sc, max_drop;
     // outputs (per group region = its anchor range)
-    int64_t *chain_ids;     // anchor ids of each chain, start -> end, packed in the group's range
-    uint64_t *chain_u;      // score<<32 | count, packed at the group's range start
-    int64_t *chain_first;   // offset in chain_ids of each chain
-    int32_t *n_chains;      // per group
+    int64_t *chain_ids;        // anchor ids of each chain, start -> end, packed in the group's range
+    uint64_t *chain_u;         // score<<32 | count, packed at the group's range start
+    int64_t *chain_first;      // offset in chain_ids of each chain
+    int32_t *n_chains;         // per group
 };
 
-__device__ int64_t bk_end(int32_t max_drop, int64_t zi, int32_t zf, const int32_t *f, const int64_t *p, int32_t *t) {
-    int64_t i = zi, end_i = -1, max_i = i;
-    int32_t max_s = 0;
-    if (i < 0 || t[i] != 0) return i;
-    do {
-        int32_t s;
-        t[i] = 2;
-        end_i = i = p[i];
-        s = i < 0 ? zf : zf - f[i];
-        if (s > max_s) max_s = s, max_i = i;
-        else if (max_s - s > max_drop) break;
-    } while (i >= 0 && t[i] == 0);
-    for (i = zi; i >= 0 && i != end_i; i = p[i]) t[i] = 0;
-    return max_i;
-}
-
+// mg_chain_backtrack, one thread per group.  The walk from a start anchor follows p[] once:
+// its path is recorded in chain_ids (this thread's own scratch), so mg_chain_bk_end's t = 2
+// marks and its reset walk are not needed (p[i] < i: a path never revisits itself), and the
+// chain is path[0, best end).  Each step issues the next node's p, f and t loads together.
 __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= P.n_groups) return;
-    const int64_t g0 = P.g_start[g], g1 = P.g_start[g + 1];
-    for (int64_t i = g0; i < g1; i++) P.t[i] = 0;
+    const int64_t g0 = P.g_start[g];
     int64_t wpos = g0;  // next free slot in chain_ids
     int nc = 0;
     const int64_t z0 = P.z_off[g], z1 = P.z_off[g + 1];
@@ -1096,19 +1086,33 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
         const int64_t zi = P.z_idx[k];
         if (P.t[zi] != 0) continue;
         const int32_t zf = P.f[zi];
-        const int64_t end_i = bk_end(P.max_drop, zi, zf, P.f, P.p, P.t);
-        int64_t i = zi, nv = 0;
-        for (; i != end_i; i = P.p[i]) {
-            P.chain_ids[wpos + nv] = i;  // end -> start for now
-            P.t[i] = 1;
-            nv++;
+        int64_t *buf = P.chain_ids + wpos;
+        int64_t len = 0, nv = 0;
+        int32_t max_s = 0;
+        int64_t i = zi, nxt = P.p[zi];
+        for (;;) {
+            buf[len++] = i;
+            int32_t fn = 0, tn = 1;
+            int64_t pn = -1;
+            if (nxt >= 0) fn = P.f[nxt], tn = P.t[nxt], pn = P.p[nxt];
+            const int32_t s = nxt < 0 ? zf : zf - fn;
+            if (s > max_s) {
+                max_s = s;
+                nv = len;
+            } else if (max_s - s > P.max_drop) {
+                break;
+            }
+            if (nxt < 0 || tn != 0) break;
+            i = nxt;
+            nxt = pn;
         }
-        const int32_t sc = i < 0 ? zf : zf - P.f[i];
+        const int32_t sc = nv == 0 ? 0 : max_s;  // zf - f[best end] (zf if the chain reaches -1)
+        for (int64_t a = 0; a < nv; a++) P.t[buf[a]] = 1;
         if (sc >= P.min_sc && nv > 0 && nv >= P.min_cnt) {
             for (int64_t a = 0, b = nv - 1; a < b; a++, b--) {  // start -> end
-                const int64_t tmp = P.chain_ids[wpos + a];
-                P.chain_ids[wpos + a] = P.chain_ids[wpos + b];
-                P.chain_ids[wpos + b] = tmp;
+                const int64_t tmp = buf[a];
+                buf[a] = buf[b];
+                buf[b] = tmp;
             }
             P.chain_u[g0 + nc] = (uint64_t)(uint32_t)sc << 32 | (uint32_t)nv;
             P.chain_first[g0 + nc] = wpos;
@@ -1145,9 +1149,10 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
 }
 
 int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, const int64_t *p, int32_t *t,
-                     const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, int min_cnt, int min_sc,
-                     int max_drop, int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first, int32_t *n_chains) {
+                     const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, int min_cnt, int min_sc, int max_drop,
+                     int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first, int32_t *n_chains, int64_t n_anchors) {
     if (n_groups <= 0) return HYMET_OK;
+    HY_HIP(hipMemsetAsync(t, 0, 4 * (size_t)n_anchors, ctx->stream));
     BacktrackParams P{g_start, f, p, t, z_off, z_idx, n_groups, min_cnt, min_sc, max_drop, chain_ids, chain_u, chain_first,
                       n_chains};
     ProfScope _ps(ctx, "mm_backtrack");

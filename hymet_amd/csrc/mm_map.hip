@@ -33,8 +33,8 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
                  int max_dist_inner, int bw, int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip,
                  int64_t n_anchors, int64_t n_groups);
 int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, const int64_t *p, int32_t *t,
-                     const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, int min_cnt, int min_sc,
-                     int max_drop, int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first, int32_t *n_chains);
+                     const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, int min_cnt, int min_sc, int max_drop,
+                     int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first, int32_t *n_chains, int64_t n_anchors);
 
 namespace {
 
@@ -108,22 +108,37 @@ struct SeedParams {
     int64_t n_buckets;
     int n_q;
     int max_occ, max_max_occ, dist;
-    uint32_t *seed_n;    // out: occurrences of every minimizer (0 = not a seed or filtered)
+    uint32_t *seed_n;    // occurrences of every minimizer (seed_count_kernel); out: 0 = not a seed or filtered
     int32_t *rep_len;    // out per query
+    const uint32_t *q_high;  // query holds a seed above max_occ
 };
+
+// occurrences of every minimizer (one thread each); flags the queries holding a seed above
+// max_occ -- only those need the sequential streak selection below
+__global__ void seed_count_kernel(const uint64_t *mx, const uint32_t *qid, int64_t n, const uint32_t *koff,
+                                  int64_t n_buckets, int max_occ, uint32_t *seed_n, uint32_t *q_high) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t h = mx[i] >> 8;
+    uint32_t c = 0;
+    if ((int64_t)h < n_buckets) c = koff[h + 1] - koff[h];
+    seed_n[i] = c;
+    if ((int)c > max_occ) q_high[qid[i]] = 1;
+}
 
 // one thread per query: mm_seed_collect_all + mm_seed_select + mm_collect_matches
 __global__ __launch_bounds__(64) void seed_select_kernel(SeedParams P) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= P.n_q) return;
+    if (!P.q_high[q]) {  // no seed above max_occ: nothing is filtered, rep_len = 0
+        P.rep_len[q] = 0;
+        return;
+    }
     const int64_t m0 = P.qm_off[q], m1 = P.qm_off[q + 1];
     const int len = (int)P.qlen[q];
     int n_seed = 0, n_high = 0;
     for (int64_t i = m0; i < m1; i++) {
-        const uint64_t h = P.mx[i] >> 8;
-        uint32_t n = 0;
-        if ((int64_t)h < P.n_buckets) n = P.koff[h + 1] - P.koff[h];
-        P.seed_n[i] = n;
+        const uint32_t n = P.seed_n[i];
         if (n) {
             n_seed++;
             if ((int)n > P.max_occ) n_high++;
@@ -354,16 +369,19 @@ __global__ void chain_cnt_kernel(const uint64_t *cu, int64_t n, uint32_t *cnt) {
     if (i < n) cnt[i] = (uint32_t)cu[i];
 }
 
-__global__ void chain_copy_kernel(const uint64_t *cu, const int64_t *cfirst, const int64_t *bpos, const int64_t *chain_ids,
-                                  const uint64_t *ax, const uint64_t *ay, int64_t n, uint64_t *bx, uint64_t *by) {
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) return;
-    const int32_t m = (int32_t)cu[c];
-    const int64_t f = cfirst[c], o = bpos[c];
-    for (int32_t j = 0; j < m; j++) {
-        const int64_t a = chain_ids[f + j];
-        bx[o + j] = ax[a];
-        by[o + j] = ay[a];
+// one wave per chain (grid-stride): anchors of chain c in start -> end order, and c per anchor
+__global__ __launch_bounds__(64) void chain_copy_kernel(const uint64_t *cu, const int64_t *cfirst, const int64_t *bpos,
+                                                        const int64_t *chain_ids, const uint64_t *ax, const uint64_t *ay,
+                                                        int64_t n, uint64_t *bx, uint64_t *by, int32_t *bchain) {
+    for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
+        const int32_t m = (int32_t)cu[c];
+        const int64_t f = cfirst[c], o = bpos[c];
+        for (int32_t j = threadIdx.x; j < m; j += 64) {
+            const int64_t a = chain_ids[f + j];
+            bx[o + j] = ax[a];
+            by[o + j] = ay[a];
+            bchain[o + j] = (int32_t)c;
+        }
     }
 }
 
@@ -430,6 +448,7 @@ struct AnchorSet {
 // anchor) + chain scores/counts + per-query chain offsets.
 struct ChainSet {
     DevBuf bx, by, cu, cboff;  // cboff: offset of each chain's anchors in bx/by
+    DevBuf bchain, cq;         // chain of each compacted anchor; query of each chain
     int64_t n_anchor = 0, n_chain = 0;
     std::vector<int64_t> h_qc;   // n_q + 1 chain offsets per query
     std::vector<int64_t> h_qb;   // n_q + 1 anchor offsets per query
@@ -570,7 +589,7 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         rc = launch_backtrack(ctx, g_start.as<int64_t>(), f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(),
                               z_off.as<int64_t>(), (const int32_t *)vi, (int32_t)G, opt->min_cnt, opt->min_chain_score, bw,
                               chain_ids.as<int64_t>(), chain_u.as<uint64_t>(), chain_first.as<int64_t>(),
-                              n_chains.as<int32_t>());
+                              n_chains.as<int32_t>(), n);
         if (rc) return rc;
         // chain list sorted by first anchor index (compact_a order)
         DevBuf cpos;
@@ -611,11 +630,16 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         C.n_anchor = NB;
         HY_HIP(C.bx.alloc(8 * (size_t)(NB + 1), ctx->stream));
         HY_HIP(C.by.alloc(8 * (size_t)(NB + 1), ctx->stream));
-        LAUNCH1(chain_copy_kernel, NC, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), C.cboff.as<int64_t>(),
-                chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, C.bx.as<uint64_t>(),
-                C.by.as<uint64_t>());
+        HY_HIP(C.bchain.alloc(4 * (size_t)(NB + 1), ctx->stream));
+        if (NC > 0) {
+            const int64_t nb = NC < (int64_t)ctx->n_cu * 64 ? NC : (int64_t)ctx->n_cu * 64;
+            hipLaunchKernelGGL(chain_copy_kernel, dim3((unsigned)nb), dim3(64), 0, ctx->stream, C.cu.as<uint64_t>(),
+                               cf_s.as<int64_t>(), C.cboff.as<int64_t>(), chain_ids.as<int64_t>(), A.ax.as<uint64_t>(),
+                               A.ay.as<uint64_t>(), NC, C.bx.as<uint64_t>(), C.by.as<uint64_t>(), C.bchain.as<int32_t>());
+            HY_CHECK_LAUNCH("chain_copy_kernel");
+        }
         // per-query chain offsets
-        DevBuf cq;
+        DevBuf &cq = C.cq;
         HY_HIP(cq.alloc(4 * (size_t)(NC + 1), ctx->stream));
         LAUNCH1(chain_query_kernel, NC, ck, NC, A.d_off.as<int64_t>(), n_q, cq.as<uint32_t>());
         HY_HIP(C.d_qc.alloc(8 * (size_t)(n_q + 1), ctx->stream));
@@ -644,7 +668,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
                    const int64_t *qc, const int64_t *qb, const uint64_t *mini_pos, const int64_t *mp_off, const int64_t *qlen,
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
-                   int64_t NB, int64_t NC, int64_t NM);
+                   int64_t NB, int64_t NC, int64_t NM, const int32_t *bchain, const uint32_t *cq);
 
 namespace {
 __global__ void rechain_flag_kernel(const uint64_t *by, const uint64_t *cu, const int64_t *qc, const int64_t *qb,
@@ -776,19 +800,28 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
         HY_HIP(hipStreamSynchronize(st));
     }
     // ------------------------------------------------------------- 3 seeds
-    DevBuf seed_n, rep_len;
+    DevBuf seed_n, rep_len, qid, q_high;
     HY_HIP(seed_n.alloc(4 * (size_t)(M + 1), st));
     HY_HIP(rep_len.alloc(4 * (size_t)n_q, st));
+    HY_HIP(qid.alloc(4 * (size_t)(M + 1), st));
+    HY_HIP(q_high.alloc(4 * (size_t)n_q, st));
+    HY_HIP(hipMemsetAsync(q_high.p, 0, 4 * (size_t)n_q, st));
+    LAUNCH1(fill_qid_kernel, M, qm_off.as<int64_t>(), n_q, M, qid.as<uint32_t>());
+    {
+        ProfScope _ps(ctx, "mm_seed_count", (double)M * (8.0 + 8.0 + 4.0));  // minimizer, 2 offsets, count
+        LAUNCH1(seed_count_kernel, M, mx.as<uint64_t>(), qid.as<uint32_t>(), M, idx->d_koff, idx->n_buckets, opt->mid_occ,
+                seed_n.as<uint32_t>(), q_high.as<uint32_t>());
+    }
     {
         SeedParams P{mx.as<uint64_t>(), my.as<uint64_t>(), qm_off.as<int64_t>(), d_qlen.as<int64_t>(), idx->d_koff,
                      idx->n_buckets, n_q, opt->mid_occ, opt->max_max_occ, opt->occ_dist, seed_n.as<uint32_t>(),
-                     rep_len.as<int32_t>()};
+                     rep_len.as<int32_t>(), q_high.as<uint32_t>()};
         ProfScope _ps(ctx, "mm_seed_select");
         hipLaunchKernelGGL(seed_select_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P);
         HY_CHECK_LAUNCH("seed_select_kernel");
     }
     // ------------------------------------------------------------ 4 anchors
-    DevBuf a_pos, mflag, mp_pos, qid, mini_pos, mp_off;
+    DevBuf a_pos, mflag, mp_pos, mini_pos, mp_off;
     int64_t A = 0, NM = 0;
     rc = scan_flags(ctx, seed_n.as<uint32_t>(), M, a_pos, &A);
     if (rc) return rc;
@@ -798,8 +831,6 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
     if (rc) return rc;
     HY_HIP(hipMemcpyAsync(a_pos.as<int64_t>() + M, &A, 8, hipMemcpyHostToDevice, st));
     HY_HIP(hipMemcpyAsync(mp_pos.as<int64_t>() + M, &NM, 8, hipMemcpyHostToDevice, st));
-    HY_HIP(qid.alloc(4 * (size_t)(M + 1), st));
-    LAUNCH1(fill_qid_kernel, M, qm_off.as<int64_t>(), n_q, M, qid.as<uint32_t>());
     HY_HIP(mini_pos.alloc(8 * (size_t)(NM + 1), st));
     HY_HIP(mp_off.alloc(8 * (size_t)(n_q + 1), st));
     hipLaunchKernelGGL(sample_off_kernel, dim3((unsigned)cdiv(n_q + 1, 256)), dim3(256), 0, st, mp_pos.as<int64_t>(),
@@ -887,7 +918,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
                                 C.d_qc.as<int64_t>(), C.d_qb.as<int64_t>(), mini_pos.as<uint64_t>(), mp_off.as<int64_t>(),
                                 d_qlen.as<int64_t>(), d_hash.as<uint32_t>(), rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
                                 z.p, rg.as<hymet_mm_reg>(), wv.as<int32_t>(), cov.as<uint64_t>(), tmp.as<int32_t>(),
-                                nr.as<int32_t>(), C.n_anchor, NC, NM);
+                                nr.as<int32_t>(), C.n_anchor, NC, NM, C.bchain.as<int32_t>(), C.cq.as<uint32_t>());
         if (r2) return r2;
         regs.resize(NC);
         nreg.resize(n_q);

@@ -141,14 +141,16 @@ struct AnchorStatParams {
     const uint64_t *mini_pos;
     int64_t NB, NC;
     int n_q;
-    int32_t *a_idx, *a_chain, *c_mlen, *c_blen, *c_st, *c_last;
+    const int32_t *bchain;   // chain of each anchor (chain_copy_kernel)
+    const uint32_t *cq;      // query of each chain
+    int32_t *a_idx, *c_mlen, *c_blen, *c_st, *c_last;
 };
 
 __global__ void chain_anchor_kernel(AnchorStatParams P) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= P.NB) return;
-    const int64_t c = upper_idx(P.cboff, P.NC, b);
-    const int64_t q = upper_idx(P.qb, P.n_q, b);
+    const int64_t c = P.bchain[b];
+    const int64_t q = P.cq[c];
     const int32_t cnt = (int32_t)P.cu[c];
     const int32_t pos = (int32_t)(b - P.cboff[c]);
     const uint64_t x = P.bx[b], y = P.by[b];
@@ -168,7 +170,6 @@ __global__ void chain_anchor_kernel(AnchorStatParams P) {
     const int32_t nm = (int32_t)(P.mp_off[q + 1] - m0);
     const int32_t idx = nm > 0 ? get_mini_idx((int)P.qlen[q], x, y, nm, P.mini_pos + m0) : -1;
     P.a_idx[b] = idx;
-    P.a_chain[b] = (int32_t)c;
     const int32_t kk = (x >> 63) ? cnt - 1 - pos : pos;  // est_err walking order
     if (kk == 0) P.c_st[c] = idx;
     if (kk == cnt - 1) P.c_last[c] = idx;
@@ -398,12 +399,11 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
                    const int64_t *qc, const int64_t *qb, const uint64_t *mini_pos, const int64_t *mp_off, const int64_t *qlen,
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
-                   int64_t NB, int64_t NC, int64_t NM) {
+                   int64_t NB, int64_t NC, int64_t NM, const int32_t *bchain, const uint32_t *cq) {
     if (n_q <= 0) return HYMET_OK;
     hipStream_t st = ctx->stream;
-    DevBuf a_idx, a_chain, cst, sumk;
+    DevBuf a_idx, cst, sumk;
     HY_HIP(a_idx.alloc(4 * (size_t)(NB + 1), st));
-    HY_HIP(a_chain.alloc(4 * (size_t)(NB + 1), st));
     HY_HIP(cst.alloc(4 * 5 * (size_t)(NC + 1), st));
     HY_HIP(sumk.alloc(8 * (size_t)n_q, st));
     int32_t *c_mlen = cst.as<int32_t>(), *c_blen = c_mlen + (NC + 1), *c_st = c_blen + (NC + 1), *c_last = c_st + (NC + 1),
@@ -414,12 +414,12 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
     {
         ProfScope _ps(ctx, "mm_chain_stats", (double)NB * (16.0 + 16.0 + 8.0) + (double)NM * 8.0);
         if (NB > 0) {
-            AnchorStatParams A{bx, by, cu, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, a_idx.as<int32_t>(),
-                               a_chain.as<int32_t>(), c_mlen, c_blen, c_st, c_last};
+            AnchorStatParams A{bx, by, cu, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, bchain, cq, a_idx.as<int32_t>(),
+                               c_mlen, c_blen, c_st, c_last};
             hipLaunchKernelGGL(chain_anchor_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A);
             HY_CHECK_LAUNCH("chain_anchor_kernel");
             hipLaunchKernelGGL(chain_viol_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, bx, cu, cboff,
-                               a_idx.as<int32_t>(), a_chain.as<int32_t>(), NB, c_fv);
+                               a_idx.as<int32_t>(), bchain, NB, c_fv);
             HY_CHECK_LAUNCH("chain_viol_kernel");
         }
         if (NM > 0) {

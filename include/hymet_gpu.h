@@ -33,6 +33,7 @@ extern "C" {
 #define HYMET_E_HIP (-1)       /* a HIP runtime call failed */
 #define HYMET_E_ARG (-2)       /* invalid argument / unsupported parameter */
 #define HYMET_E_CAPACITY (-3)  /* caller-provided buffer too small; retry with the size reported */
+#define HYMET_E_INTERNAL (-4)  /* a device-side consistency check failed (no out-of-range access was made) */
 
 typedef struct hymet_ctx hymet_ctx;
 
