@@ -113,9 +113,21 @@ def bench_cami(args, comm, gpu, torch):
     torch.cuda.synchronize()
     comm.barrier()
     t0 = time.perf_counter()
+    prof_host = os.environ.get("HYMET_BENCH_PYPROF") and comm.rank == 0
+    if prof_host:
+        import cProfile
+        cp = cProfile.Profile()
+        cp.enable()
     for _ in range(args.steps):
         res = pipe.run(pq)
     torch.cuda.synchronize()
+    if prof_host:
+        import io
+        import pstats
+        cp.disable()
+        sio = io.StringIO()
+        pstats.Stats(cp, stream=sio).sort_stats("cumulative").print_stats(30)
+        print(sio.getvalue(), file=sys.stderr)
     comm.barrier()
     dt = comm.max_float(time.perf_counter() - t0)
     gpu.prof(False)

@@ -358,14 +358,20 @@ class Classifier:
     # ----------------------------------------------------------------- output
     def rows(self, res: LcaResult):
         out = []
+        lin_cache = {}  # (depth, name ids) -> lineage string: few distinct lineages, many queries
+        depth, names, conf = res.depth, res.names, res.conf
         for q, name in enumerate(res.queries):
-            d = int(res.depth[q])
+            d = int(depth[q])
             if self.variant == CAMI:
                 if d <= 0:
                     out.append((name, "Unknown", "root", 0.0))
                 else:
-                    lin = "; ".join(f"{RANKS[i]}:{self.labels[res.names[q, i]]}" for i in range(d))
-                    out.append((name, lin, RANKS[d - 1], float(res.conf[q])))
+                    key = (d,) + tuple(names[q, :d].tolist())
+                    lin = lin_cache.get(key)
+                    if lin is None:
+                        lin = "; ".join(f"{RANKS[i]}:{self.labels[names[q, i]]}" for i in range(d))
+                        lin_cache[key] = lin
+                    out.append((name, lin, RANKS[d - 1], float(conf[q])))
             else:
                 if d == -1:
                     lin = self.hier.rows[self.taxids[int(res.tax[q])]]
@@ -373,16 +379,20 @@ class Classifier:
                 elif d == 0:
                     out.append((name, "Unknown", "root", 0.0))
                 else:
-                    full = ";".join(self.labels[res.names[q, i]] for i in range(d))
-                    out.append((name, full, legacy_level(full), float(res.conf[q])))
+                    key = (d,) + tuple(names[q, :d].tolist())
+                    hit = lin_cache.get(key)
+                    if hit is None:
+                        full = ";".join(self.labels[names[q, i]] for i in range(d))
+                        hit = (full, legacy_level(full))
+                        lin_cache[key] = hit
+                    out.append((name, hit[0], hit[1], float(conf[q])))
         return out
 
-    def tsv_bytes(self, res: LcaResult) -> bytes:
+    def tsv_bytes(self, res: LcaResult, rows=None) -> bytes:
         buf = io.StringIO(newline="")
         w = csv.writer(buf, delimiter="\t")
         w.writerow(["Query", "Lineage", "Taxonomic Level", "Confidence"])
-        for q, lin, lvl, conf in self.rows(res):
-            w.writerow([q, lin, lvl, f"{conf:.4f}"])
+        w.writerows([q, lin, lvl, f"{conf:.4f}"] for q, lin, lvl, conf in (rows if rows is not None else self.rows(res)))
         return buf.getvalue().encode()
 
 

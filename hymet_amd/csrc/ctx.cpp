@@ -2,6 +2,9 @@
 #include "common.hpp"
 
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
 
 namespace hymet {
 static thread_local std::string g_err;
@@ -13,6 +16,52 @@ int fail(int code, const std::string &msg) {
 int hip_fail(hipError_t e, const char *what) {
     g_err = std::string(what) + ": " + hipGetErrorString(e);
     return HYMET_E_HIP;
+}
+
+static std::mutex g_cache_mu;
+static std::map<std::pair<int, size_t>, std::vector<void *>> g_cache;  // (device, class) -> free blocks
+
+static size_t size_class(size_t b) {
+    if (b <= 4096) return 4096;
+    int e = 63 - __builtin_clzll((unsigned long long)b);
+    const size_t q = ((size_t)1 << e) / 4;
+    return (b + q - 1) / q * q;
+}
+
+hipError_t scratch_alloc(size_t bytes, void **p, size_t *cls) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    *cls = size_class(bytes);
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        auto it = g_cache.find({dev, *cls});
+        if (it != g_cache.end() && !it->second.empty()) {
+            *p = it->second.back();
+            it->second.pop_back();
+            return hipSuccess;
+        }
+    }
+    e = hipMalloc(p, *cls);
+    if (e == hipErrorOutOfMemory) {  // give the cached blocks of this device back and retry once
+        (void)hipGetLastError();
+        (void)hipDeviceSynchronize();
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        for (auto &kv : g_cache)
+            if (kv.first.first == dev) {
+                for (void *q : kv.second) (void)hipFree(q);
+                kv.second.clear();
+            }
+        e = hipMalloc(p, *cls);
+    }
+    return e;
+}
+
+void scratch_free(void *p, size_t cls) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    g_cache[{dev, cls}].push_back(p);
 }
 }  // namespace hymet
 
@@ -38,6 +87,7 @@ int hymet_init(int device, hymet_ctx **out) {
     c->n_cu = prop.multiProcessorCount;
     HY_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->own_stream = true;
+
     *out = c;
     return HYMET_OK;
 }

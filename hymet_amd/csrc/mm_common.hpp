@@ -36,24 +36,24 @@ __host__ __device__ __forceinline__ uint64_t hash64(uint64_t key) {
     return key;
 }
 
-// Stream-ordered device scratch, freed at scope exit.
+// Device scratch from the library's caching allocator (hymet::scratch_alloc), returned to the
+// cache at scope exit.  All work of a context runs on its one stream, so a block handed back
+// while kernels that use it are still queued can be reissued at once: the next user is queued
+// behind them.
 struct DevBuf {
     void *p = nullptr;
-    size_t n = 0;
-    hipStream_t s = nullptr;
+    size_t n = 0, cls = 0;
     DevBuf() = default;
     DevBuf(const DevBuf &) = delete;
     DevBuf &operator=(const DevBuf &) = delete;
     ~DevBuf() { release(); }
-    hipError_t alloc(size_t bytes, hipStream_t st) {
+    hipError_t alloc(size_t bytes, hipStream_t) {
         release();
-        s = st;
         n = bytes;
-        if (bytes == 0) bytes = 16;
-        return hipMallocAsync(&p, bytes, st);
+        return scratch_alloc(bytes == 0 ? 16 : bytes, &p, &cls);
     }
     void release() {
-        if (p) (void)hipFreeAsync(p, s);
+        if (p) scratch_free(p, cls);
         p = nullptr;
         n = 0;
     }

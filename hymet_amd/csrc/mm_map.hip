@@ -17,6 +17,9 @@
 #include "mm_common.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 
 struct hymet_mm_result {
     int n_q = 0;
@@ -403,6 +406,31 @@ __global__ void count_per_query_kernel(const uint32_t *cq, int64_t n, int n_q, i
 }  // namespace
 
 // ---------------------------------------------------------------- host helpers
+// HYMET_TRACE=1: whole-call wall time of hymet_mm_map, destructors included
+struct CallTrace {
+    bool on = getenv("HYMET_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    ~CallTrace() {
+        if (on)
+            fprintf(stderr, "[hymet_mm_map] %-22s %9.2f ms\n", "TOTAL (with frees)",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count());
+    }
+};
+// HYMET_TRACE=1: per-phase wall times of hymet_mm_map (stream synchronised at each mark)
+struct PhaseTrace {
+    hymet_ctx *ctx;
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    explicit PhaseTrace(hymet_ctx *c) : ctx(c), on(getenv("HYMET_TRACE") != nullptr), t(std::chrono::steady_clock::now()) {}
+    void mark(const char *what) {
+        if (!on) return;
+        (void)hipStreamSynchronize(ctx->stream);
+        const auto n = std::chrono::steady_clock::now();
+        fprintf(stderr, "[hymet_mm_map] %-22s %9.2f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
+
 template <typename K, typename V>
 static int sort_pairs(hymet_ctx *ctx, K *&keys, K *&keys_alt, V *&vals, V *&vals_alt, int64_t n, int begin_bit, int end_bit) {
     if (n <= 1) return HYMET_OK;
@@ -720,6 +748,7 @@ extern "C" {
 int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *opt, const uint32_t *d_2b,
                  const uint32_t *d_mask, const int64_t *h_starts, const int64_t *h_lens, const uint32_t *h_name_hash,
                  int32_t n_q, hymet_mm_result **out) {
+    CallTrace call_trace;
     HY_ARG(ctx && idx && opt && d_2b && d_mask && out, "hymet_mm_map: null argument");
     HY_ARG(n_q >= 0, "hymet_mm_map: n_q < 0");
     HY_ARG(opt->mid_occ > 0, "hymet_mm_map: opt->mid_occ must be resolved (hymet_mm_index_max_occ + clamps)");
@@ -735,6 +764,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
     const float pen_gap = (float)(opt->chain_gap_scale * 0.01 * k);
     const float pen_skip = (float)(opt->chain_skip_scale * 0.01 * k);
     int rc;
+    PhaseTrace tr(ctx);
     // ---------------------------------------------------------------- 1 sketch
     DevBuf mx, my, qm_off;
     int64_t M = 0;
@@ -748,6 +778,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
     std::vector<int64_t> h_qm(n_q + 1);
     HY_HIP(hipMemcpyAsync(h_qm.data(), qm_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, st));
     HY_HIP(hipStreamSynchronize(st));
+    tr.mark("sketch");
     // ------------------------------------------------------- 2 mm_seed_mz_flt
     bool need_flt = false;
     if (opt->q_occ_frac > 0.0f)
@@ -799,6 +830,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
         HY_HIP(hipMemcpyAsync(h_qm.data(), qm_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, st));
         HY_HIP(hipStreamSynchronize(st));
     }
+    tr.mark("mz_flt");
     // ------------------------------------------------------------- 3 seeds
     DevBuf seed_n, rep_len, qid, q_high;
     HY_HIP(seed_n.alloc(4 * (size_t)(M + 1), st));
@@ -820,6 +852,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
         hipLaunchKernelGGL(seed_select_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P);
         HY_CHECK_LAUNCH("seed_select_kernel");
     }
+    tr.mark("seeds");
     // ------------------------------------------------------------ 4 anchors
     DevBuf a_pos, mflag, mp_pos, mini_pos, mp_off;
     int64_t A = 0, NM = 0;
@@ -860,10 +893,12 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
         rc = sort_anchor_set(ctx, x, y, k1, k2, val, A, key1_bits, S1);
         if (rc) return rc;
     }
+    tr.mark("anchors+sort");
     // ------------------------------------------------ 6 chain (+ 7 long join)
     ChainSet C1;
     rc = chain_set(ctx, opt, pen_gap, pen_skip, opt->bw, S1, n_q, C1);
     if (rc) return rc;
+    tr.mark("chain_set 1");
     ChainSet *CF = &C1;
     ChainSet C2;
     std::vector<uint32_t> h_flag(n_q, 0);
@@ -904,6 +939,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
             CF = nullptr;
         }
     }
+    tr.mark("long join");
     // -------------------------------------------------------------- 8 regions
     auto run_regions = [&](ChainSet &C, std::vector<hymet_mm_reg> &regs, std::vector<int32_t> &nreg) -> int {
         const int64_t NC = C.n_chain;
@@ -937,6 +973,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
     }
     HY_HIP(hipMemcpyAsync(res->rep_len.data(), rep_len.p, 4 * (size_t)n_q, hipMemcpyDeviceToHost, st));
     HY_HIP(hipStreamSynchronize(st));
+    tr.mark("regions");
     for (int q = 0; q < n_q; q++) {
         const bool use2 = !CF && h_flag[q];
         const int nr = use2 ? n2[q] : n1[q];
@@ -945,6 +982,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
         for (int i = 0; i < nr; i++) res->regs.push_back(src[c0 + i]);
         res->reg_off[q + 1] = (int64_t)res->regs.size();
     }
+    tr.mark("assemble");
     return HYMET_OK;
 }
 

@@ -2,13 +2,13 @@
 // mm_gen_regs (score + hash order), mm_reg_set_coor / mm_cal_fuzzy_len, mm_set_parent,
 // mm_select_sub (+ mm_sync_regs), mm_est_err, mm_filter_strand_retained, mm_set_mapq.
 // Everything that walks a chain's anchors is anchor-parallel and runs first:
-//   chain_anchor_kernel  one thread per chained anchor: its mlen/blen contribution
-//                        (mm_reg_set_coor), its index among the query minimizers (mm_est_err's
-//                        get_mini_idx binary search);
-//   chain_viol_kernel    one thread per anchor: the first anchor, in est_err's walking order,
-//                        whose minimizer index does not increase -- est_err's sequential
-//                        two-pointer walk matches exactly the prefix before it;
-//   query_sumk_kernel    per-query sum of minimizer spans (avg_k).
+//   anchor_mini_idx_kernel  one thread per chained anchor: its index among the query
+//                           minimizers (mm_est_err's get_mini_idx binary search);
+//   chain_stats_kernel      one wave per chain: mlen/blen sums (mm_reg_set_coor) and the first
+//                           anchor, in est_err's walking order, whose minimizer index does not
+//                           increase -- est_err's sequential two-pointer walk matches exactly
+//                           the prefix before it;
+//   query_sumk_kernel       one wave per query: sum of minimizer spans (avg_k).
 // regions_kernel then runs one thread per query: a query has few chains (tens) and every step
 // left is an O(n^2)-at-most scan over them.  Scratch lives in global memory at the query's
 // chain range.  Float/double arithmetic is written in the order of hit.c (-ffp-contract=off).
@@ -88,7 +88,7 @@ struct RegParams {
     uint64_t *cov;
     int32_t *tmp;
     int32_t *n_regs;
-    // per-chain anchor statistics (chain_anchor_kernel / chain_viol_kernel)
+    // per-chain anchor statistics (chain_stats_kernel)
     const int32_t *c_mlen, *c_blen, *c_st, *c_last, *c_fv;
     const uint64_t *q_sumk;
 };
@@ -107,7 +107,7 @@ __device__ void set_coor(hymet_mm_reg *r, int32_t qlen, const uint64_t *ax, cons
         r->qs = qlen - ((int32_t)ay[k + r->cnt - 1] + 1);
         r->qe = qlen - ((int32_t)ay[k] + 1 - q_span);
     }
-    r->mlen = mlen;  // span(first) + sum over consecutive anchors (chain_anchor_kernel)
+    r->mlen = mlen;  // span(first) + sum over consecutive anchors (chain_stats_kernel)
     r->blen = blen;
 }
 
@@ -146,58 +146,79 @@ struct AnchorStatParams {
     int32_t *a_idx, *c_mlen, *c_blen, *c_st, *c_last;
 };
 
-__global__ void chain_anchor_kernel(AnchorStatParams P) {
+// per chained anchor: its index among the query minimizers (mm_est_err's get_mini_idx)
+__global__ void anchor_mini_idx_kernel(AnchorStatParams P) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= P.NB) return;
-    const int64_t c = P.bchain[b];
-    const int64_t q = P.cq[c];
-    const int32_t cnt = (int32_t)P.cu[c];
-    const int32_t pos = (int32_t)(b - P.cboff[c]);
-    const uint64_t x = P.bx[b], y = P.by[b];
-    const int32_t span = (int32_t)(y >> 32 & 0xff);
-    int32_t dm, db;
-    if (pos == 0) {
-        dm = db = span;
-    } else {  // hit.c mm_reg_set_coor
-        const int32_t tl = (int32_t)x - (int32_t)P.bx[b - 1];
-        const int32_t ql = (int32_t)y - (int32_t)P.by[b - 1];
-        db = tl > ql ? tl : ql;
-        dm = tl > span && ql > span ? span : tl < ql ? tl : ql;
-    }
-    atomicAdd(&P.c_mlen[c], dm);
-    atomicAdd(&P.c_blen[c], db);
+    const int64_t q = P.cq[P.bchain[b]];
     const int64_t m0 = P.mp_off[q];
     const int32_t nm = (int32_t)(P.mp_off[q + 1] - m0);
-    const int32_t idx = nm > 0 ? get_mini_idx((int)P.qlen[q], x, y, nm, P.mini_pos + m0) : -1;
-    P.a_idx[b] = idx;
-    const int32_t kk = (x >> 63) ? cnt - 1 - pos : pos;  // est_err walking order
-    if (kk == 0) P.c_st[c] = idx;
-    if (kk == cnt - 1) P.c_last[c] = idx;
+    P.a_idx[b] = nm > 0 ? get_mini_idx((int)P.qlen[q], P.bx[b], P.by[b], nm, P.mini_pos + m0) : -1;
 }
 
+__device__ __forceinline__ int wsum(int v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ int wmin(int v) {
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// one wave per chain (grid-stride): mm_reg_set_coor's mlen/blen sums, and for mm_est_err the
+// walk-order first/last minimizer index and the first anchor whose index does not increase:
 // est_err's loop `for (k=1, j=st+1; j<nm && k<cnt; ++j) if (idx(k) == j) ++k, ++n_match;`
-// matches anchor k iff idx(1..k) strictly increase from st; the first anchor that does not
-// (or has no minimizer) stalls it to the end.
-__global__ void chain_viol_kernel(const uint64_t *bx, const uint64_t *cu, const int64_t *cboff, const int32_t *a_idx,
-                                  const int32_t *a_chain, int64_t NB, int32_t *c_fv) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= NB) return;
-    const int32_t c = a_chain[b];
-    const int32_t cnt = (int32_t)cu[c];
-    const int32_t pos = (int32_t)(b - cboff[c]);
-    const bool rev = bx[b] >> 63;
-    const int32_t kk = rev ? cnt - 1 - pos : pos;
-    if (kk == 0) return;
-    const int32_t cur = a_idx[b], prev = a_idx[rev ? b + 1 : b - 1];
-    if (cur < 0 || cur <= prev) atomicMin(&c_fv[c], kk);
+// matches anchor k iff idx(1..k) strictly increase from st; the first that does not (or has no
+// minimizer) stalls it to the end
+__global__ __launch_bounds__(64) void chain_stats_kernel(AnchorStatParams P, const int32_t *a_idx, int32_t *c_fv) {
+    const int lane = threadIdx.x;
+    for (int64_t c = blockIdx.x; c < P.NC; c += gridDim.x) {
+        const int32_t cnt = (int32_t)P.cu[c];
+        const int64_t o = P.cboff[c];
+        const bool rev = P.bx[o] >> 63;
+        int dm_sum = 0, db_sum = 0, fv = cnt;
+        for (int32_t j0 = 0; j0 < cnt; j0 += 64) {
+            const int32_t j = j0 + lane;
+            if (j >= cnt) continue;
+            const int64_t b = o + j;
+            const uint64_t x = P.bx[b], y = P.by[b];
+            const int32_t span = (int32_t)(y >> 32 & 0xff);
+            if (j == 0) {
+                dm_sum += span, db_sum += span;
+            } else {  // hit.c mm_reg_set_coor
+                const int32_t tl = (int32_t)x - (int32_t)P.bx[b - 1];
+                const int32_t ql = (int32_t)y - (int32_t)P.by[b - 1];
+                db_sum += tl > ql ? tl : ql;
+                dm_sum += tl > span && ql > span ? span : tl < ql ? tl : ql;
+            }
+            const int32_t kk = rev ? cnt - 1 - j : j;  // est_err walking order
+            if (kk >= 1) {
+                const int32_t cur = a_idx[b], prev = a_idx[rev ? b + 1 : b - 1];
+                if (cur < 0 || cur <= prev) fv = min(fv, kk);
+            }
+        }
+        dm_sum = wsum(dm_sum);
+        db_sum = wsum(db_sum);
+        fv = wmin(fv);
+        if (lane == 0) {
+            P.c_mlen[c] = dm_sum;
+            P.c_blen[c] = db_sum;
+            c_fv[c] = fv;
+            P.c_st[c] = a_idx[rev ? o + cnt - 1 : o];
+            P.c_last[c] = a_idx[rev ? o : o + cnt - 1];
+        }
+    }
 }
 
-__global__ void query_sumk_kernel(const uint64_t *mini_pos, const int64_t *mp_off, int n_q, int64_t NM,
-                                  unsigned long long *sumk) {
-    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= NM) return;
-    const int64_t q = upper_idx(mp_off, n_q, m);
-    atomicAdd(&sumk[q], (unsigned long long)(mini_pos[m] >> 32 & 0xff));
+// one wave per query: sum of minimizer spans (avg_k)
+__global__ __launch_bounds__(64) void query_sumk_kernel(const uint64_t *mini_pos, const int64_t *mp_off, int n_q,
+                                                        unsigned long long *sumk) {
+    for (int q = blockIdx.x; q < n_q; q += gridDim.x) {
+        unsigned long long sk = 0;
+        for (int64_t m = mp_off[q] + threadIdx.x; m < mp_off[q + 1]; m += 64) sk += mini_pos[m] >> 32 & 0xff;
+        for (int o = 32; o > 0; o >>= 1) sk += __shfl_xor(sk, o, 64);
+        if (threadIdx.x == 0) sumk[q] = sk;
+    }
 }
 
 __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
@@ -330,7 +351,7 @@ __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
         }
         n = k;
     }
-    // ---- mm_est_err (the per-anchor walk was done by chain_anchor_kernel / chain_viol_kernel)
+    // ---- mm_est_err (the per-anchor walk was done by chain_stats_kernel)
     {
         const int64_t m0 = P.mp_off[q];
         const int32_t nm = (int32_t)(P.mp_off[q + 1] - m0);
@@ -408,25 +429,21 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
     HY_HIP(sumk.alloc(8 * (size_t)n_q, st));
     int32_t *c_mlen = cst.as<int32_t>(), *c_blen = c_mlen + (NC + 1), *c_st = c_blen + (NC + 1), *c_last = c_st + (NC + 1),
             *c_fv = c_last + (NC + 1);
-    HY_HIP(hipMemsetAsync(c_mlen, 0, 8 * (size_t)(NC + 1), st));
-    HY_HIP(hipMemsetAsync(c_fv, 0x7f, 4 * (size_t)(NC + 1), st));
-    HY_HIP(hipMemsetAsync(sumk.p, 0, 8 * (size_t)n_q, st));
     {
         ProfScope _ps(ctx, "mm_chain_stats", (double)NB * (16.0 + 16.0 + 8.0) + (double)NM * 8.0);
+        AnchorStatParams A{bx, by, cu, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, bchain, cq, a_idx.as<int32_t>(),
+                           c_mlen, c_blen, c_st, c_last};
         if (NB > 0) {
-            AnchorStatParams A{bx, by, cu, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, bchain, cq, a_idx.as<int32_t>(),
-                               c_mlen, c_blen, c_st, c_last};
-            hipLaunchKernelGGL(chain_anchor_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A);
-            HY_CHECK_LAUNCH("chain_anchor_kernel");
-            hipLaunchKernelGGL(chain_viol_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, bx, cu, cboff,
-                               a_idx.as<int32_t>(), bchain, NB, c_fv);
-            HY_CHECK_LAUNCH("chain_viol_kernel");
+            hipLaunchKernelGGL(anchor_mini_idx_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A);
+            HY_CHECK_LAUNCH("anchor_mini_idx_kernel");
+            const int64_t nb = NC < (int64_t)ctx->n_cu * 64 ? NC : (int64_t)ctx->n_cu * 64;
+            hipLaunchKernelGGL(chain_stats_kernel, dim3((unsigned)nb), dim3(64), 0, st, A, a_idx.as<int32_t>(), c_fv);
+            HY_CHECK_LAUNCH("chain_stats_kernel");
         }
-        if (NM > 0) {
-            hipLaunchKernelGGL(query_sumk_kernel, dim3((unsigned)cdiv(NM, 256)), dim3(256), 0, st, mini_pos, mp_off, n_q, NM,
-                               sumk.as<unsigned long long>());
-            HY_CHECK_LAUNCH("query_sumk_kernel");
-        }
+        const int nqb = n_q < ctx->n_cu * 64 ? n_q : ctx->n_cu * 64;
+        hipLaunchKernelGGL(query_sumk_kernel, dim3((unsigned)nqb), dim3(64), 0, st, mini_pos, mp_off, n_q,
+                           sumk.as<unsigned long long>());
+        HY_CHECK_LAUNCH("query_sumk_kernel");
     }
     RegParams P{bx, by, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,

@@ -2,7 +2,7 @@
 //
 // Kernels
 //   table_insert   : distinct sketch hashes -> open-addressing uint64 table in HBM
-//                    (linear probing, slot = top bits of the hash), one atomicCAS per hash.
+//                    (linear probing from a multiplicative-hash home slot), one atomicCAS per hash.
 //   screen_count<K>: one thread = one 64-position tile of the pooled, packed query bases.
 //                    Rolling 2-bit forward / reverse-complement words decide the canonical
 //                    strand by integer compare (== Mash's memcmp on ASCII, since A<C<G<T);
@@ -20,6 +20,11 @@
 namespace {
 
 constexpr uint64_t kEmpty = ~0ull;
+
+// Home slot of a hash: multiplicative (Fibonacci) hashing of the full 64 bits.  The top bits
+// alone would crowd every real sketch into the bottom of the table: a bottom-s MinHash sketch
+// holds the s SMALLEST hashes of its genome, so their top bits are all zero.
+__device__ __forceinline__ uint64_t home_slot(uint64_t h, int shift) { return (h * 0x9E3779B97F4A7C15ull) >> shift; }
 constexpr int kTile = 64;  // k-mer start positions per thread (multiple of 32: lanes stay in phase)
 constexpr int kMaxDb = 4;
 
@@ -134,7 +139,7 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
                     continue;
                 }
                 const uint64_t *keys = P.keys[d];
-                uint64_t s = h >> P.shift[d];
+                uint64_t s = home_slot(h, P.shift[d]);
                 for (;;) {
                     const uint64_t key = keys[s];
                     if (key == h) {
@@ -164,7 +169,7 @@ __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t *__res
         slot_of[i] = nslots;
         return;
     }
-    uint64_t s = h >> shift;
+    uint64_t s = home_slot(h, shift);
     for (;;) {
         unsigned long long prev = atomicCAS(&keys[s], (unsigned long long)kEmpty, (unsigned long long)h);
         if (prev == kEmpty || prev == h) break;

@@ -126,36 +126,41 @@ class Pipeline:
     def paf_table(self, ix: IndexSet, queries: SeqSet, results, with_text=False):
         """PAF lines in minimap2's output order (part-major, query order) as classifier arrays."""
         qnames = queries.names
-        qidx: Dict[int, int] = {}
-        order_q: List[int] = []
-        lq, lt, lb, ll, le = [], [], [], [], []
-        text = [] if with_text else None
+        lq, lt, lb, text = [], [], [], ([] if with_text else None)
         for pi, b0, res in results:
             first = ix.part_first[pi]
             regs = res.regs
             if len(regs) == 0:
                 continue
             nper = np.diff(res.off)
-            qs = np.repeat(np.arange(len(nper)) + b0, nper)
-            for q in np.flatnonzero(nper) + b0:
-                if int(q) not in qidx:
-                    qidx[int(q)] = len(order_q)
-                    order_q.append(int(q))
-            lq.append(np.array([qidx[int(q)] for q in qs], np.int32))
-            lt.append((regs["rid"] + first).astype(np.int32))
+            lq.append(np.repeat(np.arange(len(nper), dtype=np.int64) + b0, nper))
+            lt.append(regs["rid"].astype(np.int32) + np.int32(first))
             lb.append(regs["blen"].astype(np.int64))
-            ll.append(queries.lengths[qs].astype(np.int64))
-            le.append(np.zeros(len(regs), np.uint8))
             if with_text:
-                for q in range(len(nper)):
-                    rr = res.query(q)
-                    if len(rr):
-                        g = q + b0
-                        text.extend(mp.paf_lines(qnames[g], int(queries.lengths[g]), rr, int(res.rep_len[q]),
-                                                 ix.names[first:], ix.lens[first:]))
-        cat = (lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt))
-        table = cls.PafTable([qnames[q] for q in order_q], cat(lq, np.int32), list(ix.names), cat(lt, np.int32),
-                             cat(lb, np.int64), cat(ll, np.int64), cat(le, np.uint8))
+                for q in np.flatnonzero(nper):
+                    g = int(q) + b0
+                    text.extend(mp.paf_lines(qnames[g], int(queries.lengths[g]), res.query(int(q)), int(res.rep_len[q]),
+                                             ix.names[first:], ix.lens[first:]))
+        if lq:
+            all_q = np.concatenate(lq)
+            uq, first_pos = np.unique(all_q, return_index=True)
+            order_q = uq[np.argsort(first_pos, kind="stable")]      # queries by first appearance
+            pos = np.empty(int(all_q.max()) + 1, np.int64)
+            pos[order_q] = np.arange(len(order_q))
+            line_q = pos[all_q].astype(np.int32)
+            line_t, line_b = np.concatenate(lt), np.concatenate(lb)
+            line_l = np.asarray(queries.lengths, np.int64)[all_q]
+        else:
+            order_q = np.zeros(0, np.int64)
+            line_q, line_t = np.zeros(0, np.int32), np.zeros(0, np.int32)
+            line_b, line_l = np.zeros(0, np.int64), np.zeros(0, np.int64)
+        exact = np.zeros(len(line_q), np.uint8)
+        if self.classifier.variant == cls.LEGACY and len(line_q):
+            # classification.py:141-151: query == target and coverage >= 0.99
+            same = np.asarray(qnames, dtype=object)[all_q] == np.asarray(ix.names, dtype=object)[line_t]
+            cov = np.where(line_l > 0, line_b / np.maximum(line_l, 1), 0.0)
+            exact = (same & (cov >= 0.99)).astype(np.uint8)
+        table = cls.PafTable([qnames[q] for q in order_q], line_q, list(ix.names), line_t, line_b, line_l, exact)
         return table, text
 
     # ------------------------------------------------------------------- run
@@ -171,7 +176,7 @@ class Pipeline:
         table, text = self.paf_table(ix, queries, results, with_paf)
         res = self.classifier.run(table, comm=self.comm)
         rws = self.classifier.rows(res)
-        tsv = self.classifier.tsv_bytes(res)
+        tsv = self.classifier.tsv_bytes(res, rws)
         return RunResult(selected, rows, thr, tsv, len(rws), sum(1 for r in rws if r[1] != "Unknown"), table.n_lines, text)
 
 
