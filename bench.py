@@ -38,8 +38,8 @@ def log(*a):
 
 
 def roofline_from_prof(prof, prefer=None):
-    """Dominant kernel = the largest summed device time among kernels with a byte model."""
-    cand = {k: v for k, v in prof.items() if v[2] > 0}
+    """Dominant kernel = the largest summed device time (every hot kernel has a byte model)."""
+    cand = dict(prof)
     if not cand:
         return None
     name = prefer if prefer in cand else max(cand, key=lambda k: cand[k][0])

@@ -1064,8 +1064,9 @@ struct BacktrackParams {
     const int32_t *z_idx;      // anchor indices ordered by (group, f, idx) ascending
     int32_t n_groups;
     int min_cnt, min_sc, max_drop;
+    int64_t long_min;          // groups above this size go to backtrack_long_kernel
     // outputs (per group region = its anchor range)
-    int64_t *chain_ids;        // anchor ids of each chain, start -> end, packed in the group's range
+    int64_t *chain_ids;        // anchor ids of each chain, end -> start, packed in the group's range
     uint64_t *chain_u;         // score<<32 | count, packed at the group's range start
     int64_t *chain_first;      // offset in chain_ids of each chain
     int32_t *n_chains;         // per group
@@ -1074,27 +1075,184 @@ struct BacktrackParams {
 // mg_chain_backtrack, one thread per group.  The walk from a start anchor follows p[] once:
 // its path is recorded in chain_ids (this thread's own scratch), so mg_chain_bk_end's t = 2
 // marks and its reset walk are not needed (p[i] < i: a path never revisits itself), and the
-// chain is path[0, best end).  Each step issues the next node's p, f and t loads together.
+// chain is path[0, best end), left in walk order (end -> start; chain_list / chain_copy read it
+// reversed).  Path nodes are marked as the walk passes them and the few past the best end
+// unmarked afterwards, so no pass re-reads the path.  Paths run mostly down consecutive anchors, so the walk keeps a
+// window of kBtWin (p, f, t) triples below the current node, loaded together (one memory
+// round trip per window instead of one per step); the z scan batches its t probes the same
+// way.  Windows are refilled after every walk, since a walk's t marks make them stale.
+constexpr int kBtWin = 8;
+
+// Groups larger than kBtLong anchors (HYMET_BT_LONG overrides it, for tests) (a long contig against a close strain: tens of thousands
+// of anchors, nearly all in one chain) would leave a single lane walking them while the rest
+// of the grid idles.  They get a whole wave each (work list + atomic counter): the z scan
+// probes 64 entries per step (ballot), and the walk - whose state is wave-uniform, kept in
+// SGPRs via readfirstlane - refills a 64-node (p, f, t) window with one coalesced load and
+// reads each step's node from it with readlane.  Lane 0 does the path / t stores; a fence
+// after each walk and L2 loads of t make its marks visible to the other lanes' probes.
+constexpr int64_t kBtLong = 1024;
+
+__device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+    return (int64_t)((uint64_t)(uint32_t)uni((int32_t)(v >> 32)) << 32 | (uint32_t)uni((int32_t)v));
+}
+__device__ __forceinline__ int64_t rlane64(int64_t v, int l) {
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int32_t)(v >> 32), l);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int32_t)v, l);
+    return (int64_t)((uint64_t)hi << 32 | lo);
+}
+
+__global__ void bt_long_list_kernel(const int64_t *g_start, int32_t n_groups, int64_t long_min, int32_t *list,
+                                    int32_t *cnt) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < n_groups && g_start[g + 1] - g_start[g] > long_min) list[atomicAdd(cnt, 1)] = g;
+}
+
+__global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, const int32_t *list, const int32_t *cnt,
+                                                            int32_t *counter) {
+    const int lane = threadIdx.x;
+    const int32_t n_long = uni(ld_l2(cnt));
+    for (;;) {
+        int32_t w = 0;
+        if (lane == 0) w = atomicAdd(counter, 1);
+        w = uni(w);  // lane 0 is the first active lane
+        if (w >= n_long) break;
+        const int32_t g = uni(list[w]);
+        const int64_t g0 = uni64(P.g_start[g]);
+        const int64_t z0 = uni64(P.z_off[g]), z1 = uni64(P.z_off[g + 1]);
+        int64_t wpos = g0;
+        int nc = 0;
+        int64_t k = z1 - 1;
+        while (k >= z0) {
+            const int64_t kk = k - lane;
+            const int32_t zc = kk >= z0 ? P.z_idx[kk] : 0;
+            const int32_t tv = kk >= z0 ? ld_l2(P.t + zc) : 1;
+            const uint64_t m = __ballot(tv == 0);
+            if (m == 0) {
+                k -= 64;
+                continue;
+            }
+            const int hit = uni(__ffsll((unsigned long long)m) - 1);
+            const int64_t zi = (int64_t)__builtin_amdgcn_readlane(zc, hit);
+            k -= hit + 1;
+            const int32_t zf = uni(P.f[zi]);
+            int64_t *buf = P.chain_ids + wpos;
+            int64_t len = 0, nv = 0;
+            int32_t max_s = 0;
+            int64_t i = zi, nxt = uni64(P.p[zi]);
+            int64_t whi = -1;  // window: lane l holds anchor whi - l
+            int64_t wp = -1;
+            int32_t wf = 0, wt = 1;
+            for (;;) {
+                if (lane == 0) {
+                    buf[len] = i;
+                    P.t[i] = 1;
+                }
+                len++;
+                int32_t fn = 0, tn = 1;
+                int64_t pn = -1;
+                if (nxt >= 0) {
+                    if (nxt > whi || nxt <= whi - 64) {
+                        whi = nxt;
+                        const int64_t j = nxt - lane;
+                        const bool ok = j >= g0;
+                        wp = ok ? P.p[j] : -1;
+                        wf = ok ? P.f[j] : 0;
+                        wt = ok ? ld_l2(P.t + j) : 1;
+                    }
+                    const int o = (int)(whi - nxt);
+                    fn = __builtin_amdgcn_readlane(wf, o);
+                    tn = __builtin_amdgcn_readlane(wt, o);
+                    pn = rlane64(wp, o);
+                }
+                const int32_t s = nxt < 0 ? zf : zf - fn;
+                if (s > max_s) {
+                    max_s = s;
+                    nv = len;
+                } else if (max_s - s > P.max_drop) {
+                    break;
+                }
+                if (nxt < 0 || tn != 0) break;
+                i = nxt;
+                nxt = pn;
+            }
+            const int32_t sc = nv == 0 ? 0 : max_s;
+            if (lane == 0) {
+                for (int64_t a = nv; a < len; a++) P.t[buf[a]] = 0;
+                if (sc >= P.min_sc && nv > 0 && nv >= P.min_cnt) {
+                    P.chain_u[g0 + nc] = (uint64_t)(uint32_t)sc << 32 | (uint32_t)nv;
+                    P.chain_first[g0 + nc] = wpos;
+                }
+            }
+            if (sc >= P.min_sc && nv > 0 && nv >= P.min_cnt) {
+                nc++;
+                wpos += nv;
+            }
+            __threadfence();
+        }
+        if (lane == 0) P.n_chains[g] = nc;
+    }
+}
+
+
 __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= P.n_groups) return;
     const int64_t g0 = P.g_start[g];
+    if (P.g_start[g + 1] - g0 > P.long_min) return;  // backtrack_long_kernel
     int64_t wpos = g0;  // next free slot in chain_ids
     int nc = 0;
     const int64_t z0 = P.z_off[g], z1 = P.z_off[g + 1];
-    for (int64_t k = z1 - 1; k >= z0; --k) {
-        const int64_t zi = P.z_idx[k];
-        if (P.t[zi] != 0) continue;
+    int64_t k = z1 - 1;
+    while (k >= z0) {
+        // next z entry (descending) whose anchor is unmarked
+        int32_t zc[kBtWin], tc[kBtWin];
+#pragma unroll
+        for (int u = 0; u < kBtWin; u++) zc[u] = k - u >= z0 ? P.z_idx[k - u] : 0;
+#pragma unroll
+        for (int u = 0; u < kBtWin; u++) tc[u] = k - u >= z0 ? P.t[zc[u]] : 1;
+        int hit = -1;
+#pragma unroll
+        for (int u = kBtWin - 1; u >= 0; u--)
+            if (tc[u] == 0) hit = u;
+        if (hit < 0) {
+            k -= kBtWin;
+            continue;
+        }
+        int64_t zi = 0;
+#pragma unroll
+        for (int u = 0; u < kBtWin; u++)
+            if (u == hit) zi = zc[u];
+        k -= hit + 1;
         const int32_t zf = P.f[zi];
         int64_t *buf = P.chain_ids + wpos;
         int64_t len = 0, nv = 0;
         int32_t max_s = 0;
         int64_t i = zi, nxt = P.p[zi];
+        int64_t whi = -1;  // window covers anchors (whi - kBtWin, whi]
+        int64_t wp[kBtWin];
+        int32_t wf[kBtWin], wt[kBtWin];
         for (;;) {
             buf[len++] = i;
+            P.t[i] = 1;  // no revisits: marking as we go cannot change this walk's reads
             int32_t fn = 0, tn = 1;
             int64_t pn = -1;
-            if (nxt >= 0) fn = P.f[nxt], tn = P.t[nxt], pn = P.p[nxt];
+            if (nxt >= 0) {
+                if (nxt > whi || nxt <= whi - kBtWin) {
+                    whi = nxt;
+#pragma unroll
+                    for (int u = 0; u < kBtWin; u++) {
+                        const bool ok = nxt - u >= g0;
+                        wp[u] = ok ? P.p[nxt - u] : -1;
+                        wf[u] = ok ? P.f[nxt - u] : 0;
+                        wt[u] = ok ? P.t[nxt - u] : 1;
+                    }
+                }
+                const int64_t o = whi - nxt;
+#pragma unroll
+                for (int u = 0; u < kBtWin; u++)
+                    if (o == u) fn = wf[u], tn = wt[u], pn = wp[u];
+            }
             const int32_t s = nxt < 0 ? zf : zf - fn;
             if (s > max_s) {
                 max_s = s;
@@ -1107,13 +1265,8 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
             nxt = pn;
         }
         const int32_t sc = nv == 0 ? 0 : max_s;  // zf - f[best end] (zf if the chain reaches -1)
-        for (int64_t a = 0; a < nv; a++) P.t[buf[a]] = 1;
-        if (sc >= P.min_sc && nv > 0 && nv >= P.min_cnt) {
-            for (int64_t a = 0, b = nv - 1; a < b; a++, b--) {  // start -> end
-                const int64_t tmp = buf[a];
-                buf[a] = buf[b];
-                buf[b] = tmp;
-            }
+        for (int64_t a = nv; a < len; a++) P.t[buf[a]] = 0;  // past the best end: stays unmarked
+        if (sc >= P.min_sc && nv > 0 && nv >= P.min_cnt) {  // kept end -> start (readers reverse)
             P.chain_u[g0 + nc] = (uint64_t)(uint32_t)sc << 32 | (uint32_t)nv;
             P.chain_first[g0 + nc] = wpos;
             nc++;
@@ -1153,11 +1306,24 @@ int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, c
                      int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first, int32_t *n_chains, int64_t n_anchors) {
     if (n_groups <= 0) return HYMET_OK;
     HY_HIP(hipMemsetAsync(t, 0, 4 * (size_t)n_anchors, ctx->stream));
-    BacktrackParams P{g_start, f, p, t, z_off, z_idx, n_groups, min_cnt, min_sc, max_drop, chain_ids, chain_u, chain_first,
-                      n_chains};
-    ProfScope _ps(ctx, "mm_backtrack");
+    const char *ev = getenv("HYMET_BT_LONG");
+    const int64_t long_min = ev ? atoll(ev) : kBtLong;
+    BacktrackParams P{g_start,  f,       p,        t,           z_off,   z_idx, n_groups, min_cnt, min_sc, max_drop,
+                      long_min, chain_ids, chain_u, chain_first, n_chains};
+    DevBuf list, cnt;
+    HY_HIP(list.alloc(4 * (size_t)n_groups, ctx->stream));
+    HY_HIP(cnt.alloc(8, ctx->stream));
+    HY_HIP(hipMemsetAsync(cnt.p, 0, 8, ctx->stream));
+    // z index + t probe + walked (p, f) + t mark + chain id write, per anchor
+    ProfScope _ps(ctx, "mm_backtrack", 32.0 * (double)n_anchors);
+    hipLaunchKernelGGL(bt_long_list_kernel, dim3((unsigned)cdiv(n_groups, 256)), dim3(256), 0, ctx->stream, g_start,
+                       n_groups, long_min, list.as<int32_t>(), cnt.as<int32_t>());
+    HY_CHECK_LAUNCH("bt_long_list_kernel");
     hipLaunchKernelGGL(backtrack_groups_kernel, dim3((unsigned)cdiv(n_groups, 64)), dim3(64), 0, ctx->stream, P);
     HY_CHECK_LAUNCH("backtrack_groups_kernel");
+    hipLaunchKernelGGL(backtrack_long_kernel, dim3((unsigned)ctx->n_cu * 4), dim3(64), 0, ctx->stream, P,
+                       list.as<int32_t>(), cnt.as<int32_t>(), cnt.as<int32_t>() + 1);
+    HY_CHECK_LAUNCH("backtrack_long_kernel");
     return HYMET_OK;
 }
 

@@ -361,7 +361,7 @@ __global__ void chain_list_kernel(const int64_t *g_start, const int32_t *n_chain
     int64_t o = c_pos[g];
     for (int c = 0; c < n_chains[g]; c++, o++) {
         const int64_t fo = chain_first[g0 + c];
-        ckey[o] = (uint64_t)chain_ids[fo];
+        ckey[o] = (uint64_t)chain_ids[fo + (uint32_t)chain_u[g0 + c] - 1];  // stored end -> start
         cu[o] = chain_u[g0 + c];
         cfirst[o] = fo;
     }
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(64) void chain_copy_kernel(const uint64_t *cu, cons
         const int32_t m = (int32_t)cu[c];
         const int64_t f = cfirst[c], o = bpos[c];
         for (int32_t j = threadIdx.x; j < m; j += 64) {
-            const int64_t a = chain_ids[f + j];
+            const int64_t a = chain_ids[f + m - 1 - j];  // backtrack stores end -> start
             bx[o + j] = ax[a];
             by[o + j] = ay[a];
             bchain[o + j] = (int32_t)c;
@@ -614,11 +614,31 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(chain_u.alloc(8 * (size_t)n, ctx->stream));
         HY_HIP(chain_first.alloc(8 * (size_t)n, ctx->stream));
         HY_HIP(n_chains.alloc(4 * (size_t)G, ctx->stream));
+        if (getenv("HYMET_TRACE_BT")) {  // diagnostic: backtrack time vs the largest groups
+            std::vector<int64_t> gs(G + 1), zo(G + 1);
+            HY_HIP(hipMemcpyAsync(gs.data(), g_start.p, 8 * (size_t)(G + 1), hipMemcpyDeviceToHost, ctx->stream));
+            HY_HIP(hipMemcpyAsync(zo.data(), z_off.p, 8 * (size_t)(G + 1), hipMemcpyDeviceToHost, ctx->stream));
+            HY_HIP(hipStreamSynchronize(ctx->stream));
+            int64_t mg = 0, mz = 0, big = 0;
+            for (int64_t g = 0; g < G; g++) {
+                mg = std::max(mg, gs[g + 1] - gs[g]);
+                mz = std::max(mz, zo[g + 1] - zo[g]);
+                big += gs[g + 1] - gs[g] > 10000;
+            }
+            fprintf(stderr, "[bt] G=%lld n=%lld nz=%lld max_group=%lld max_z=%lld groups>10k=%lld", (long long)G,
+                    (long long)n, (long long)nz, (long long)mg, (long long)mz, (long long)big);
+        }
+        const auto bt0 = std::chrono::steady_clock::now();
         rc = launch_backtrack(ctx, g_start.as<int64_t>(), f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(),
                               z_off.as<int64_t>(), (const int32_t *)vi, (int32_t)G, opt->min_cnt, opt->min_chain_score, bw,
                               chain_ids.as<int64_t>(), chain_u.as<uint64_t>(), chain_first.as<int64_t>(),
                               n_chains.as<int32_t>(), n);
         if (rc) return rc;
+        if (getenv("HYMET_TRACE_BT")) {
+            HY_HIP(hipStreamSynchronize(ctx->stream));
+            fprintf(stderr, " bt=%.2f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - bt0).count());
+        }
         // chain list sorted by first anchor index (compact_a order)
         DevBuf cpos;
         int64_t NC = 0;
@@ -848,7 +868,7 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
         SeedParams P{mx.as<uint64_t>(), my.as<uint64_t>(), qm_off.as<int64_t>(), d_qlen.as<int64_t>(), idx->d_koff,
                      idx->n_buckets, n_q, opt->mid_occ, opt->max_max_occ, opt->occ_dist, seed_n.as<uint32_t>(),
                      rep_len.as<int32_t>(), q_high.as<uint32_t>()};
-        ProfScope _ps(ctx, "mm_seed_select");
+        ProfScope _ps(ctx, "mm_seed_select", (double)M * (8.0 + 8.0 + 4.0 + 4.0));  // minimizer x/y, count, seed flag
         hipLaunchKernelGGL(seed_select_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P);
         HY_CHECK_LAUNCH("seed_select_kernel");
     }

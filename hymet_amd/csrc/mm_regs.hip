@@ -448,7 +448,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
     RegParams P{bx, by, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
                 tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk.as<uint64_t>()};
-    ProfScope _ps(ctx, "mm_regions");
+    ProfScope _ps(ctx, "mm_regions", (double)NC * (8.0 + 8.0 + 4.0 * 5) + (double)n_q * 64.0);  // chain + stats reads, reg writes
     hipLaunchKernelGGL(regions_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P);
     HY_CHECK_LAUNCH("regions_kernel");
     return HYMET_OK;

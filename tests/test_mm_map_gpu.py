@@ -49,7 +49,11 @@ def _queries(rng, refs):
     return qs
 
 
-def test_map_matches_oracle(gpu):
+@pytest.mark.parametrize("bt_long", [None, "4"])
+def test_map_matches_oracle(gpu, monkeypatch, bt_long):
+    """bt_long = "4": nearly every chain group takes the wave-per-group backtrack path."""
+    if bt_long is not None:
+        monkeypatch.setenv("HYMET_BT_LONG", bt_long)
     from hymet_amd import mapper
     from hymet_amd.seqio import DevicePool, from_records
     from oracle import oracle_lib as ol
