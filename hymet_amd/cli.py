@@ -1,0 +1,237 @@
+"""Stage drop-ins with the reference scripts' argv / file / exit-code contracts.
+
+    python -m hymet_amd.cli screen  INPUT_DIR DB.msh SCREEN_TAB FILTERED SORTED TOP_HITS SELECTED THRESH
+        == scripts/mash.sh:4-55 (mash screen -p 8 -v 0.9, sort -u -k5,5, sort -gr, threshold walk)
+    python -m hymet_amd.cli limit --selected F --output F [--score-file F]... [--max N] [--dedupe] ...
+        == scripts/limit_candidates.py:47-89,249-289
+    python -m hymet_amd.cli map     INPUT_DIR REFERENCE_FASTA INDEX_PATH PAF_OUT
+        == scripts/minimap2.sh:4-33 (minimap2 -I2g -d, minimap2 -x asm10)
+    python -m hymet_amd.cli classify        --paf P --taxonomy T --hierarchy H --output O [--processes N]
+        == scripts/classification_cami.py:345-354
+    python -m hymet_amd.cli classify-legacy (same flags)
+        == scripts/classification.py:184-200
+
+The thin wrappers under scripts/ call these, so run_hymet_cami.sh / main.pl can use them
+in place of the reference stage scripts unchanged.  All device work goes through
+libhymet_gpu.so; without it (or without a GPU) every GPU subcommand fails loudly.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import logging
+import os
+import sys
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+
+def _fna_files(input_dir: str) -> List[str]:
+    # bash expands "$INPUT_DIR"/*.fna in collation order; LC_ALL=C byte order here
+    return sorted(glob.glob(os.path.join(input_dir, "*.fna")), key=lambda p: p.encode())
+
+
+def _write_lines(path: str, lines: Sequence[str]):
+    with open(path, "w", encoding="utf-8", newline="") as f:
+        for l in lines:
+            f.write(l + "\n")
+
+
+# ------------------------------------------------------------------ screen (mash.sh)
+def cmd_screen(argv: Sequence[str]) -> int:
+    if len(argv) != 8:
+        print("usage: screen INPUT_DIR DB.msh SCREEN_TAB FILTERED SORTED TOP_HITS SELECTED THRESH", file=sys.stderr)
+        return 2
+    input_dir, msh_path, screen_tab, filtered, sorted_p, top_hits, selected, thresh = argv
+    from . import screen as scr
+    from . import select as sel
+    from ._lib import Gpu
+    from .msh import load_db
+    from .seqio import DevicePool, read_fasta
+    files = _fna_files(input_dir)
+    db = load_db(msh_path)
+    gpu = Gpu(int(os.environ.get("HYMET_DEVICE", "0")))
+    rows: List[str] = []
+    if files:
+        ss = read_fasta(files)
+        res = scr.screen(gpu, DevicePool(gpu, ss, DevicePool.ALPHA_MASH), [db])[0]
+        rows = res.lines(v_max=0.9)
+    _write_lines(screen_tab, rows)
+    f_rows = sel.sort_unique_k5(rows)
+    _write_lines(filtered, f_rows)
+    s_rows = sel.sort_gr(f_rows)
+    _write_lines(sorted_p, s_rows)
+    n_files = len(files)
+    need = sel.min_candidates(n_files)
+    print("====================================")
+    print(f"Number of input sequences: {n_files}")
+    print(f"Minimum expected candidates: {need}")
+    print("====================================")
+    best, top, names = sel.select_threshold(s_rows, thresh, n_files)
+    _write_lines(top_hits, top)
+    _write_lines(selected, names)
+    print("====================================")
+    print(f"Final threshold used: {best}")
+    print(f"Candidates found: {len(top)}")
+    print("====================================")
+    return 0
+
+
+# ------------------------------------------------------------ limit (limit_candidates.py)
+def cmd_limit(argv: Sequence[str]) -> int:
+    from . import select as sel
+    p = argparse.ArgumentParser(prog="limit", description="Limit Mash candidate genomes (limit_candidates.py).")
+    p.add_argument("--selected", required=True)
+    p.add_argument("--output", required=True)
+    p.add_argument("--score-file", action="append", default=[], dest="score_files")
+    p.add_argument("--assembly-dir", default=None)
+    p.add_argument("--max", type=int, default=5000)
+    p.add_argument("--dedupe", action="store_true")
+    p.add_argument("--log", default=None)
+    p.add_argument("--no-download", action="store_true")
+    a = p.parse_args(argv)
+    if a.max <= 0:
+        raise SystemExit("The --max value must be greater than zero.")
+    with open(a.selected, "r", encoding="utf-8") as f:
+        cands = [l.strip() for l in f if l.strip()]
+    if not cands:
+        raise SystemExit(f"No candidates found in {a.selected}")
+    scores = sel.read_scores([s for s in a.score_files if os.path.exists(s)])
+    # never downloads: without local assembly summaries the species key is the accession
+    smap = sel.species_map(a.assembly_dir) if a.dedupe else {}
+    chosen = sel.limit(cands, scores, a.max, a.dedupe, smap)
+    tmp = a.output + ".tmp"
+    _write_lines(tmp, chosen)
+    os.replace(tmp, a.output)
+    kept = len(chosen)
+    summary = (f"[limit_candidates] kept {kept} / {len(cands)} candidates ({kept} unique keys) "
+               f"{'(species dedupe)' if a.dedupe else ''}")
+    print(summary)
+    if a.log:
+        os.makedirs(os.path.dirname(os.path.abspath(a.log)), exist_ok=True)
+        with open(a.log, "a", encoding="utf-8") as f:
+            f.write(summary.rstrip("\n") + "\n")
+    return 0
+
+
+# ------------------------------------------------------------------ map (minimap2.sh)
+INDEX_MAGIC = "hymet-amd-mm-index/1"
+
+
+def map_paf(gpu, refs, queries, split_idx: str = "2g", mini_batch: float = 50e6, batch_bases: int = 40_000_000,
+            w: int = 10, k: int = 15) -> List[str]:
+    """minimap2 -I<split_idx> index of `refs` + `-x asm10` mapping of `queries` -> PAF lines
+    in minimap2's order (index part by part; queries in input order within a part)."""
+    from . import mapper as mp
+    from .pipeline import _batches
+    from .seqio import DevicePool
+    parts = mp.split_parts(refs.lengths, float(mp.parse_num(split_idx)), mini_batch)
+    batches = []
+    for b0, b1 in _batches(queries.lengths, batch_bases):
+        sub = queries if (b0 == 0 and b1 == queries.n) else queries.subset(range(b0, b1))
+        batches.append((b0, sub, DevicePool(gpu, sub, DevicePool.ALPHA_MINIMAP2)))
+    out: List[str] = []
+    opt = None
+    for p in parts:
+        sub = refs.subset(p) if len(parts) > 1 else refs
+        part = mp.IndexPart(gpu, sub, w, k)
+        if opt is None:
+            opt = mp.MapOpt.asm10()
+            opt.resolve_mid_occ(part)          # mm_mapopt_update on the first part
+        for b0, qs, qp in batches:
+            res = mp.map_part(gpu, part, qp, opt)
+            for q in np.flatnonzero(np.diff(res.off)):
+                q = int(q)
+                out.extend(mp.paf_lines(qs.names[q], int(qs.lengths[q]), res.query(q), int(res.rep_len[q]),
+                                        part.names, part.lens))
+        part.close()
+    return out
+
+
+def cmd_map(argv: Sequence[str]) -> int:
+    if len(argv) != 4:
+        print("usage: map INPUT_DIR REFERENCE_FASTA INDEX_PATH PAF_OUT", file=sys.stderr)
+        return 2
+    input_dir, ref_fasta, index_path, paf_out = argv
+    from ._lib import Gpu
+    from .seqio import read_fasta
+    split = os.environ.get("SPLIT_IDX", "2g")
+    try:
+        if not (os.path.exists(index_path) and os.path.getsize(index_path) > 0):
+            print("Creating index with minimap2...")
+            # The device index is rebuilt from the reference FASTA on every run (seconds
+            # on the GPU); the file records what it was built from, so the reference's
+            # "[ -s reference.mmi ]" cache test keeps its meaning.
+            st = os.stat(ref_fasta)
+            with open(index_path, "w") as f:
+                json.dump({"format": INDEX_MAGIC, "reference": os.path.abspath(ref_fasta), "size": st.st_size,
+                           "split_idx": split, "k": 15, "w": 10}, f)
+                f.write("\n")
+        else:
+            print(f"Using cached minimap2 index: {index_path}")
+        print("Running alignment with minimap2...")
+        gpu = Gpu(int(os.environ.get("HYMET_DEVICE", "0")))
+        refs = read_fasta([ref_fasta])
+        queries = read_fasta(_fna_files(input_dir))
+        lines = map_paf(gpu, refs, queries, split)
+        _write_lines(paf_out, lines)
+    except Exception as e:  # minimap2.sh:25-29
+        print(f"Error running alignment with minimap2. ({e})")
+        return 1
+    print(f"Alignment completed successfully! Results saved to {paf_out}.")
+    return 0
+
+
+# --------------------------------------------------- classify (classification*.py)
+def cmd_classify(argv: Sequence[str], legacy: bool = False) -> int:
+    from . import classify as cls
+    from ._lib import Gpu
+    p = argparse.ArgumentParser(prog="classify")
+    p.add_argument("--paf", required=True)
+    p.add_argument("--taxonomy", required=True)
+    p.add_argument("--hierarchy", required=True)
+    p.add_argument("--output", required=True)
+    p.add_argument("--processes", type=int, default=4)   # accepted; the GPU does the fan-out
+    a = p.parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
+    gpu = Gpu(int(os.environ.get("HYMET_DEVICE", "0")))
+    variant = cls.LEGACY if legacy else cls.CAMI
+    c = cls.Classifier(gpu, a.taxonomy, a.hierarchy, variant)
+    paf = cls.read_paf(a.paf, variant)
+    if legacy and len(paf.queries) == 0:
+        raise ZeroDivisionError("division by zero")  # classification.py:182 on an empty PAF
+    res = c.run(paf)
+    rows = c.rows(res)
+    with open(a.output, "wb") as f:
+        f.write(c.tsv_bytes(res, rows))
+    n = len(rows)
+    k = sum(1 for r in rows if r[1] != "Unknown")
+    logging.info(f"Classification complete. Results saved to {a.output}")
+    logging.info(f"Classified: {k}/{n} ({(k / n if n else 0):.1%})")
+    return 0
+
+
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv:
+        print(__doc__, file=sys.stderr)
+        return 2
+    cmd, rest = argv[0], argv[1:]
+    if cmd == "screen":
+        return cmd_screen(rest)
+    if cmd == "limit":
+        return cmd_limit(rest)
+    if cmd == "map":
+        return cmd_map(rest)
+    if cmd == "classify":
+        return cmd_classify(rest)
+    if cmd == "classify-legacy":
+        return cmd_classify(rest, legacy=True)
+    print(f"unknown subcommand {cmd!r}", file=sys.stderr)
+    return 2
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -432,9 +432,10 @@ struct PhaseTrace {
 };
 
 template <typename K, typename V>
-static int sort_pairs(hymet_ctx *ctx, K *&keys, K *&keys_alt, V *&vals, V *&vals_alt, int64_t n, int begin_bit, int end_bit) {
+static int sort_pairs(hymet_ctx *ctx, K *&keys, K *&keys_alt, V *&vals, V *&vals_alt, int64_t n, int begin_bit, int end_bit,
+                      const char *tag = "radix_sort") {
     if (n <= 1) return HYMET_OK;
-    ProfScope _ps(ctx, "radix_sort", 2.0 * (double)n * (sizeof(K) + sizeof(V)) * (double)((end_bit - begin_bit + 7) / 8));
+    ProfScope _ps(ctx, tag, 2.0 * (double)n * (sizeof(K) + sizeof(V)) * (double)((end_bit - begin_bit + 7) / 8));
     size_t tmp = 0;
     HY_HIP(rocprim::radix_sort_pairs(nullptr, tmp, keys, keys_alt, vals, vals_alt, (size_t)n, begin_bit, end_bit, ctx->stream));
     DevBuf t;
@@ -491,13 +492,13 @@ static int sort_anchor_set(hymet_ctx *ctx, DevBuf &x, DevBuf &y, DevBuf &k1, Dev
     HY_HIP(valb.alloc(4 * (size_t)n, ctx->stream));
     uint64_t *kk = k2.as<uint64_t>(), *kka = k2b.as<uint64_t>();
     uint32_t *vv = val.as<uint32_t>(), *vva = valb.as<uint32_t>();
-    int rc = sort_pairs(ctx, kk, kka, vv, vva, n, 0, 64);
+    int rc = sort_pairs(ctx, kk, kka, vv, vva, n, 0, 64, "radix_sort_anchor_pos");
     if (rc) return rc;
     HY_HIP(k1g.alloc(8 * (size_t)n, ctx->stream));
     HY_HIP(k1b.alloc(8 * (size_t)n, ctx->stream));
     LAUNCH1(gather_kernel<uint64_t>, n, k1.as<uint64_t>(), vv, k1g.as<uint64_t>(), n);
     uint64_t *k1p = k1g.as<uint64_t>(), *k1a = k1b.as<uint64_t>();
-    rc = sort_pairs(ctx, k1p, k1a, vv, vva, n, 0, key1_bits);
+    rc = sort_pairs(ctx, k1p, k1a, vv, vva, n, 0, key1_bits, "radix_sort_anchor_group");
     if (rc) return rc;
     HY_HIP(out.ax.alloc(8 * (size_t)n, ctx->stream));
     HY_HIP(out.ay.alloc(8 * (size_t)n, ctx->stream));
@@ -550,7 +551,7 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         rc = scan_flags(ctx, swork.as<uint32_t>(), G, wpos, &n_work);
         if (rc) return rc;
         uint32_t *kp = skey.as<uint32_t>(), *ka = skey2.as<uint32_t>(), *vp = sidx.as<uint32_t>(), *va = sidx2.as<uint32_t>();
-        rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 32);
+        rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 32, "radix_sort_groups");
         if (rc) return rc;
         {  // the chaining kernel packs local predecessor indices in 24 bits
             uint32_t k0 = 0;
@@ -592,13 +593,13 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         LAUNCH1(zfill_kernel, n, f.as<int32_t>(), zflag.as<uint32_t>(), zpos.as<int64_t>(), gid.as<int32_t>(), n,
                 zf.as<uint32_t>(), zi.as<uint32_t>(), zg.as<uint32_t>());
         uint32_t *kf = zf.as<uint32_t>(), *kfa = zf2.as<uint32_t>(), *vi = zi.as<uint32_t>(), *via = zi2.as<uint32_t>();
-        rc = sort_pairs(ctx, kf, kfa, vi, via, nz, 0, 32);
+        rc = sort_pairs(ctx, kf, kfa, vi, via, nz, 0, 32, "radix_sort_z_f");
         if (rc) return rc;
         DevBuf zgg;
         HY_HIP(zgg.alloc(zb, ctx->stream));
         LAUNCH1(gather_kernel<uint32_t>, nz, gid.as<uint32_t>(), vi, zgg.as<uint32_t>(), nz);
         uint32_t *kg = zgg.as<uint32_t>(), *kga = zg2.as<uint32_t>();
-        rc = sort_pairs(ctx, kg, kga, vi, via, nz, 0, bits_for(G));
+        rc = sort_pairs(ctx, kg, kga, vi, via, nz, 0, bits_for(G), "radix_sort_z_group");
         if (rc) return rc;
         DevBuf z_off;
         HY_HIP(z_off.alloc(8 * (size_t)(G + 1), ctx->stream));
@@ -660,7 +661,7 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         LAUNCH1(iota_u32_kernel, NC, perm.as<uint32_t>(), NC);
         uint64_t *ck = ckey.as<uint64_t>(), *cka = ckeyb.as<uint64_t>();
         uint32_t *pp = perm.as<uint32_t>(), *ppa = perm2.as<uint32_t>();
-        rc = sort_pairs(ctx, ck, cka, pp, ppa, NC, 0, bits_for(n));
+        rc = sort_pairs(ctx, ck, cka, pp, ppa, NC, 0, bits_for(n), "radix_sort_chains");
         if (rc) return rc;
         DevBuf cu_s, cf_s;
         HY_HIP(cu_s.alloc(8 * (size_t)(NC + 1), ctx->stream));
@@ -816,13 +817,13 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
         LAUNCH1(iota_u32_kernel, M, sidx.as<uint32_t>(), M);
         uint64_t *kx = sx.as<uint64_t>(), *kxa = sx2.as<uint64_t>();
         uint32_t *vi = sidx.as<uint32_t>(), *via = sidx2.as<uint32_t>();
-        rc = sort_pairs(ctx, kx, kxa, vi, via, M, 0, 2 * k + 8);
+        rc = sort_pairs(ctx, kx, kxa, vi, via, M, 0, 2 * k + 8, "radix_sort_mz");
         if (rc) return rc;
         HY_HIP(sq.alloc(4 * (size_t)M, st));
         HY_HIP(sq2.alloc(4 * (size_t)M, st));
         LAUNCH1(gather_kernel<uint32_t>, M, qid.as<uint32_t>(), vi, sq.as<uint32_t>(), M);
         uint32_t *kq = sq.as<uint32_t>(), *kqa = sq2.as<uint32_t>();
-        rc = sort_pairs(ctx, kq, kqa, vi, via, M, 0, bits_for(n_q));
+        rc = sort_pairs(ctx, kq, kqa, vi, via, M, 0, bits_for(n_q), "radix_sort_mz");
         if (rc) return rc;
         LAUNCH1(gather_kernel<uint64_t>, M, mx.as<uint64_t>(), vi, kxa, M);  // x in (q, x) order
         HY_HIP(drop.alloc((size_t)M, st));
@@ -1035,7 +1036,7 @@ int hymet_mm_chain_dp(hymet_ctx *ctx, const uint64_t *h_x, const uint64_t *h_y, 
     LAUNCH1(group_size_kernel, G, g_start.as<int64_t>(), (int32_t)G, 1, skey.as<uint32_t>(), sidx.as<uint32_t>(),
             swork.as<uint32_t>());
     uint32_t *kp = skey.as<uint32_t>(), *ka = skey2.as<uint32_t>(), *vp = sidx.as<uint32_t>(), *va = sidx2.as<uint32_t>();
-    rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 32);
+    rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 32, "radix_sort_groups");
     if (rc) return rc;
     {  // the chaining kernel packs local predecessor indices in 24 bits
         uint32_t k0 = 0;

@@ -14,8 +14,11 @@ import numpy as np
 
 
 class Comm:
-    def __init__(self, rank: int = 0, world: int = 1):
+    def __init__(self, rank: int = 0, world: int = 1, replicated_pool: bool = False):
+        """replicated_pool: every rank holds the same contig pool (the screen then splits
+        k-mer positions); otherwise (default) each rank's pool is its own contig shard."""
         self.rank, self.world = rank, world
+        self.replicated_pool = replicated_pool
         self.dist = None
         self.device = None
 

@@ -126,7 +126,7 @@ class Pipeline:
     def paf_table(self, ix: IndexSet, queries: SeqSet, results, with_text=False):
         """PAF lines in minimap2's output order (part-major, query order) as classifier arrays."""
         qnames = queries.names
-        lq, lt, lb, text = [], [], [], ([] if with_text else None)
+        lq, lt, lb, lp, text = [], [], [], [], ([] if with_text else None)
         for pi, b0, res in results:
             first = ix.part_first[pi]
             regs = res.regs
@@ -136,6 +136,7 @@ class Pipeline:
             lq.append(np.repeat(np.arange(len(nper), dtype=np.int64) + b0, nper))
             lt.append(regs["rid"].astype(np.int32) + np.int32(first))
             lb.append(regs["blen"].astype(np.int64))
+            lp.append(np.full(len(regs), pi, np.int32))
             if with_text:
                 for q in np.flatnonzero(nper):
                     g = int(q) + b0
@@ -150,7 +151,10 @@ class Pipeline:
             line_q = pos[all_q].astype(np.int32)
             line_t, line_b = np.concatenate(lt), np.concatenate(lb)
             line_l = np.asarray(queries.lengths, np.int64)[all_q]
+            fp = np.sort(first_pos)
+            self.last_qkey = (np.concatenate(lp)[fp], order_q.astype(np.int64))  # (part of first line, query)
         else:
+            self.last_qkey = (np.zeros(0, np.int32), np.zeros(0, np.int64))
             order_q = np.zeros(0, np.int64)
             line_q, line_t = np.zeros(0, np.int32), np.zeros(0, np.int32)
             line_b, line_l = np.zeros(0, np.int64), np.zeros(0, np.int64)
@@ -164,8 +168,10 @@ class Pipeline:
         return table, text
 
     # ------------------------------------------------------------------- run
-    def run(self, queries, with_paf=False) -> RunResult:
-        """queries: a SeqSet, or a Prepared (already resident in HBM)."""
+    def run(self, queries, with_paf=False, query_ids=None) -> RunResult:
+        """queries: a SeqSet, or a Prepared (already resident in HBM).  With several ranks,
+        query_ids gives each local query's index in the whole input (default: the shards
+        are consecutive slices in rank order); rank 0's RunResult.tsv is the whole TSV."""
         pq = queries if isinstance(queries, Prepared) else self.prepare(queries)
         queries = pq.queries
         selected, rows, thr = self.screen_select(pq.mash_pool)
@@ -176,8 +182,31 @@ class Pipeline:
         table, text = self.paf_table(ix, queries, results, with_paf)
         res = self.classifier.run(table, comm=self.comm)
         rws = self.classifier.rows(res)
+        if self.comm is not None and self.comm.world > 1:
+            part, q = self.last_qkey
+            gid = (np.asarray(query_ids, np.int64)[q] if query_ids is not None
+                   else (np.int64(self.comm.rank) << np.int64(32)) + q)
+            rws = gather_rows(self.comm, rws, part, gid)
         tsv = self.classifier.tsv_bytes(res, rws)
         return RunResult(selected, rows, thr, tsv, len(rws), sum(1 for r in rws if r[1] != "Unknown"), table.n_lines, text)
+
+
+def gather_rows(comm, rows, part: np.ndarray, qid: np.ndarray, dst: int = 0):
+    """Rank `dst` assembles the classified_sequences.tsv rows of every contig shard
+    (SURVEY.md §8e step 7).  minimap2 prints the pooled input's PAF index part by part, and
+    within a part query by query in input order; the reference writes one row per query in
+    order of first PAF appearance.  So rows sort by (part of the query's first line, the
+    query's index in the whole input).  Other ranks get []."""
+    got = comm.gather_obj((rows, np.asarray(part, np.int64), np.asarray(qid, np.int64)), dst)
+    if comm.rank != dst:
+        return []
+    all_rows = [r for rw, _, _ in got for r in rw]
+    if not all_rows:
+        return []
+    kp = np.concatenate([p for _, p, _ in got])
+    kq = np.concatenate([q for _, _, q in got])
+    order = np.lexsort((kq, kp))
+    return [all_rows[i] for i in order]
 
 
 @dataclass

@@ -106,6 +106,19 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
     return counts, bottom, n_kmers
 
 
+def reduce_partials(comm, counts, bottom: np.ndarray, nk: int, s: int):
+    """Combine the ranks' partial screens of one pool: hit counts are
+    summed (all-reduce, RCCL on the device tensors), the pool bottom-s sketch is the bottom
+    s of the union of the ranks' candidates, and the k-mer totals add up."""
+    if comm is None or comm.world <= 1:
+        return counts, bottom, nk
+    for c in counts:
+        comm.allreduce_sum_(c)
+    bottom = _bottom_s(np.concatenate(comm.allgather_np(np.asarray(bottom, np.uint64))), s)
+    nk = int(sum(int(x[0]) for x in comm.allgather_np(np.array([nk], dtype=np.int64))))
+    return counts, bottom, nk
+
+
 def set_size_from_bottom(bottom: np.ndarray) -> int:
     """MinHashHeap::estimateSetSize: 2^64 * |heap| / max(heap), truncated to uint64."""
     if len(bottom) == 0:
@@ -139,16 +152,12 @@ def screen(gpu, pool, dbs: Sequence[SketchDB], tables: Optional[Sequence[ScreenT
             chunk = idx[j:j + 4]
             s = max(dbs[i].sketch_size for i in chunk)
             n_pos = max(0, pool.n_bases - k + 1)
-            if comm is not None and comm.world > 1:
-                b, e = comm.shard_range(n_pos)
+            if comm is not None and comm.world > 1 and comm.replicated_pool:
+                b, e = comm.shard_range(n_pos)   # every rank holds the whole pool: split positions
             else:
-                b, e = 0, n_pos
+                b, e = 0, n_pos                  # the pool is this rank's contig shard
             counts, bottom, nk = count_pool(gpu, pool, [tables[i] for i in chunk], k, seed, s, b, e)
-            if comm is not None and comm.world > 1:
-                for c in counts:
-                    comm.allreduce_sum_(c)
-                bottom = _bottom_s(np.concatenate(comm.allgather_np(bottom)), s)
-                nk = int(sum(comm.allgather_np(np.array([nk], dtype=np.int64)))[0])
+            counts, bottom, nk = reduce_partials(comm, counts, bottom, nk, s)
             for ci, i in enumerate(chunk):
                 sh, md = table_stats(gpu, tables[i], counts[ci])
                 b_i = bottom[:dbs[i].sketch_size]

@@ -1,0 +1,149 @@
+"""Multi-rank host logic of the sharded path on CPU: world_size 2, gloo.
+
+  * hymet_amd.screen.reduce_partials  -- screen hit counts summed, pool bottom-s merged,
+    k-mer totals added (the exchange after each rank screens its own contig shard)
+  * hymet_amd.pipeline.gather_rows    -- rank 0 assembles classified_sequences.tsv rows in
+    the reference's first-PAF-appearance order from shards of any partition
+  * hymet_amd.dist.Comm collectives used by bench.py (barrier, max over ranks, gathers)
+"""
+import multiprocessing as mp
+import os
+import socket
+import traceback
+
+import numpy as np
+import pytest
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, fn_name, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        from hymet_amd.dist import Comm
+        comm = Comm(rank, world).init_backend(None, "gloo")
+        try:
+            out = globals()[fn_name](comm)
+        finally:
+            comm.close()
+        q.put((rank, "ok", out))
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def _run_ranks(fn_name, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, status, out = q.get(timeout=240)
+        assert status == "ok", out
+        res[rank] = out
+    for p in ps:
+        p.join(timeout=60)
+    return res
+
+
+# ------------------------------------------------------------------ screen exchange
+def _screen_data():
+    rng = np.random.default_rng(3)
+    counts = [rng.integers(0, 5, size=(2, 1001)).astype(np.int32) for _ in range(2)]   # [rank][db]
+    cands = [np.unique(rng.integers(1, 2 ** 62, size=n, dtype=np.int64).astype(np.uint64)) for n in (700, 900)]
+    nks = [12345, 67890]
+    return counts, cands, nks
+
+
+def _screen_fn(comm):
+    import torch
+    from hymet_amd.screen import _bottom_s, reduce_partials
+    counts, cands, nks = _screen_data()
+    mine = [torch.from_numpy(counts[comm.rank][d].copy()) for d in range(2)]
+    c, b, nk = reduce_partials(comm, mine, _bottom_s(cands[comm.rank], 1000), nks[comm.rank], 1000)
+    return [x.numpy() for x in c], b, nk
+
+
+def test_screen_partials_reduce_like_one_pool():
+    from hymet_amd.screen import _bottom_s
+    res = _run_ranks("_screen_fn")
+    counts, cands, nks = _screen_data()
+    exp_b = _bottom_s(np.concatenate(cands), 1000)
+    for r in (0, 1):
+        c, b, nk = res[r]
+        for d in range(2):
+            np.testing.assert_array_equal(c[d], counts[0][d] + counts[1][d])
+        np.testing.assert_array_equal(b, exp_b)
+        assert nk == sum(nks)
+
+
+# ---------------------------------------------------------------- TSV row gather
+def _global_rows():
+    """120 queries of a pooled input; queries with hits get the index part of their first
+    PAF line; the reference TSV order is (first part, input position)."""
+    rng = np.random.default_rng(9)
+    n = 120
+    has = rng.random(n) < 0.8
+    first_part = rng.integers(0, 3, size=n)
+    lengths = rng.integers(1000, 100000, size=n)
+    rows = {q: (f"ctg{q}", f"lin{q % 7}", "species", round(float(rng.random()), 4)) for q in range(n)}
+    expect = [rows[q] for q in sorted(np.flatnonzero(has), key=lambda q: (first_part[q], q))]
+    return has, first_part, lengths, rows, expect
+
+
+def _gather_fn(comm):
+    from hymet_amd.dist import Comm
+    from hymet_amd.pipeline import gather_rows
+    has, first_part, lengths, rows, _ = _global_rows()
+    shard = Comm.partition_by_length(lengths, comm.world)[comm.rank]      # non-contiguous shard
+    local = [q for q in shard if has[q]]
+    # rank-local first-appearance order: by (part of first line, local position)
+    local.sort(key=lambda q: (first_part[q], q))
+    out = gather_rows(comm, [rows[q] for q in local], np.array([first_part[q] for q in local]),
+                      np.array(local, dtype=np.int64))
+    return out
+
+
+def test_gather_rows_matches_pooled_order():
+    res = _run_ranks("_gather_fn")
+    *_, expect = _global_rows()
+    assert res[0] == expect
+    assert res[1] == []
+
+
+# ------------------------------------------------------------------ collectives
+def _comm_fn(comm):
+    mx = comm.max_float(1.5 + comm.rank)
+    ag = comm.allgather_np(np.arange(3) + 10 * comm.rank)
+    bc = comm.broadcast_obj({"sel": ["a", "b"]} if comm.rank == 0 else None)
+    g = comm.gather_obj(comm.rank * 2)
+    comm.barrier()
+    return mx, [a.tolist() for a in ag], bc, g
+
+
+def test_comm_collectives():
+    res = _run_ranks("_comm_fn")
+    for r in (0, 1):
+        mx, ag, bc, g = res[r]
+        assert mx == 2.5
+        assert ag == [[0, 1, 2], [10, 11, 12]]
+        assert bc == {"sel": ["a", "b"]}
+    assert res[0][3] == [0, 2] and res[1][3] is None
+
+
+def test_partition_and_shard_range():
+    from hymet_amd.dist import Comm
+    lengths = [5, 100, 7, 60, 60, 1, 1, 33]
+    bins = Comm.partition_by_length(lengths, 3)
+    assert sorted(np.concatenate(bins).tolist()) == list(range(len(lengths)))
+    loads = [sum(lengths[i] for i in b) for b in bins]
+    assert max(loads) - min(loads) <= max(lengths)
+    spans = [Comm(r, 3).shard_range(10) for r in range(3)]
+    assert spans == [(0, 3), (3, 6), (6, 10)]

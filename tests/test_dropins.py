@@ -1,0 +1,134 @@
+"""Stage drop-ins under scripts/ (SURVEY.md §8b): argv, output files, stdout and exit codes.
+
+CPU: scripts/limit_candidates.py against the reference-generated goldens (output bytes,
+stdout, rc).  GPU: scripts/mash.sh, scripts/minimap2.sh and scripts/classification*.py run
+as subprocesses on small inputs and compared with the oracle / the reference goldens."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+SCRIPTS = ROOT / "scripts"
+LIM = ROOT / "tests" / "golden" / "limit"
+LCASES = json.loads((LIM / "cases.json").read_text())
+
+
+def _run(args, timeout=240, **kw):
+    env = dict(os.environ)
+    env.pop("PYTHONPATH", None)
+    try:
+        return subprocess.run(args, capture_output=True, text=True, env=env, timeout=timeout, **kw)
+    except subprocess.TimeoutExpired as e:
+        raise AssertionError(f"{args[:3]} timed out; stdout={e.stdout!r} stderr={e.stderr!r}") from None
+
+
+@pytest.mark.parametrize("case", LCASES, ids=[Path(c["expect"]).stem for c in LCASES])
+def test_limit_dropin_matches_reference(case, tmp_path):
+    out = tmp_path / "limited.txt"
+    args = [sys.executable, str(SCRIPTS / "limit_candidates.py"), "--selected", str(LIM / "selected.txt"),
+            "--output", str(out), "--max", str(case["max"])]
+    for t in case["tabs"]:
+        args += ["--score-file", str(LIM / t)]
+    if case["dedupe"]:
+        args += ["--dedupe", "--no-download", "--assembly-dir", str(tmp_path / "none")]
+    r = _run(args)
+    assert r.returncode == case["rc"], r.stderr
+    assert r.stdout == case["stdout"]
+    assert out.read_bytes() == (LIM / case["expect"]).read_bytes()
+
+
+def test_limit_dropin_errors(tmp_path):
+    empty = tmp_path / "empty.txt"
+    empty.write_text("\n")
+    r = _run([sys.executable, str(SCRIPTS / "limit_candidates.py"), "--selected", str(empty), "--output",
+              str(tmp_path / "o")])
+    assert r.returncode != 0 and "No candidates found" in r.stderr
+    r = _run([sys.executable, str(SCRIPTS / "limit_candidates.py"), "--selected", str(LIM / "selected.txt"),
+              "--output", str(tmp_path / "o"), "--max", "0"])
+    assert r.returncode != 0 and "--max value must be greater than zero" in r.stderr
+
+
+def test_limit_dropin_log_append(tmp_path):
+    log = tmp_path / "logs" / "limit.log"
+    for _ in range(2):
+        r = _run([sys.executable, str(SCRIPTS / "limit_candidates.py"), "--selected", str(LIM / "selected.txt"),
+                  "--output", str(tmp_path / "o"), "--max", "3", "--log", str(log)])
+        assert r.returncode == 0
+    assert log.read_text().splitlines() == [r.stdout.rstrip("\n")] * 2
+
+
+# ---------------------------------------------------------------------------- GPU
+def _fasta(path, recs):
+    with open(path, "w") as f:
+        for n, s in recs:
+            f.write(f">{n}\n")
+            for i in range(0, len(s), 80):
+                f.write(s[i:i + 80].decode() + "\n")
+
+
+@pytest.mark.gpu
+def test_screen_map_classify_dropins_match_oracle(tmp_path):
+    from hymet_amd import synth
+    from hymet_amd.msh import SketchDB, write_msh
+    from oracle import classify_oracle, oracle_lib, pipeline_oracle, select_oracle
+    rng = np.random.default_rng(11)
+    w = synth.make_cami(rng, n_taxa=2, per_taxon=3, genome_mbp=(0.2, 0.3), contig_gbp=0.0002, max_contigs=20,
+                        name="dropin")
+    hl = [np.sort(oracle_lib.sketch([r], 21, 42, 1000)) for r in w.refs]
+    hl += list(synth.decoy_sketches(rng, 10, 1000))
+    names = [n + ".fna.gz" for n in w.ref_names] + [f"decoy_{i}.fna.gz" for i in range(len(hl) - len(w.refs))]
+    off = np.zeros(len(hl) + 1, np.int64)
+    off[1:] = np.cumsum([len(h) for h in hl])
+    db = SketchDB(names=names, comments=[f"[1 seqs] {n}" for n in names], lengths=np.full(len(hl), 250_000, np.int64),
+                  offsets=off, hashes=np.concatenate(hl))
+    msh = tmp_path / "sketch1.msh"
+    write_msh(db, msh)
+    inp = tmp_path / "input"
+    inp.mkdir()
+    recs = list(zip(w.contig_names, w.contigs))
+    _fasta(inp / "contigs.fna", recs)
+    # ---- mash.sh
+    outs = [tmp_path / f for f in ("screen.tab", "filtered.tab", "sorted.tab", "top_hits.tab", "selected.txt")]
+    r = _run(["bash", str(SCRIPTS / "mash.sh"), str(inp), str(msh)] + [str(o) for o in outs] + ["0.90"])
+    assert r.returncode == 0, r.stderr
+    rows = pipeline_oracle.screen_rows([s for _, s in recs], db)
+    assert outs[0].read_text().splitlines() == rows
+    srt = select_oracle.sort_gr(select_oracle.sort_unique_k5(rows))
+    assert outs[2].read_text().splitlines() == srt
+    t, top, sel_names, _ = select_oracle.select_threshold(srt, "0.90", 1)
+    assert outs[3].read_text().splitlines() == top
+    assert outs[4].read_text().splitlines() == sel_names
+    assert f"Final threshold used: {t}" in r.stdout
+    # ---- minimap2.sh over the selected genomes
+    by_name = {n + ".fna.gz": (n, s) for n, s in zip(w.ref_names, w.refs)}
+    chosen = [by_name[n] for n in sel_names if n in by_name]
+    assert chosen
+    ref_fa = tmp_path / "combined_genomes.fasta"
+    _fasta(ref_fa, chosen)
+    paf = tmp_path / "resultados.paf"
+    mmi = tmp_path / "reference.mmi"
+    r = _run(["bash", str(SCRIPTS / "minimap2.sh"), str(inp), str(ref_fa), str(mmi), str(paf)])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Creating index with minimap2..." in r.stdout and mmi.stat().st_size > 0
+    o_paf = pipeline_oracle.map_paf([n for n, _ in chosen], [s for _, s in chosen], recs)
+    assert paf.read_text().splitlines() == o_paf
+    r = _run(["bash", str(SCRIPTS / "minimap2.sh"), str(inp), str(ref_fa), str(mmi), str(paf)])
+    assert r.returncode == 0 and "Using cached minimap2 index" in r.stdout
+    assert paf.read_text().splitlines() == o_paf
+    # ---- classification_cami.py / classification.py
+    tax = tmp_path / "detailed_taxonomy.tsv"
+    tax.write_text(w.taxonomy_tsv())
+    hier = tmp_path / "taxonomy_hierarchy.tsv"
+    hier.write_text(w.hierarchy_tsv())
+    for script, fn in (("classification_cami.py", classify_oracle.classify_cami),
+                       ("classification.py", classify_oracle.classify_legacy)):
+        out = tmp_path / f"{script}.tsv"
+        r = _run([sys.executable, str(SCRIPTS / script), "--paf", str(paf), "--taxonomy", str(tax), "--hierarchy",
+                  str(hier), "--output", str(out), "--processes", "2"])
+        assert r.returncode == 0, r.stderr
+        assert out.read_bytes() == fn(str(paf), str(tax), str(hier))
