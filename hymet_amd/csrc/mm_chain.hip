@@ -1065,6 +1065,7 @@ struct BacktrackParams {
     int32_t n_groups;
     int min_cnt, min_sc, max_drop;
     int64_t long_min;          // groups above this size go to backtrack_long_kernel
+    unsigned long long *prof;  // HYMET_BT_PROF: long-kernel counters (nullptr = off)
     // outputs (per group region = its anchor range)
     int64_t *chain_ids;        // anchor ids of each chain, end -> start, packed in the group's range
     uint64_t *chain_u;         // score<<32 | count, packed at the group's range start
@@ -1088,8 +1089,8 @@ constexpr int kBtWin = 8;
 // of the grid idles.  They get a whole wave each (work list + atomic counter): the z scan
 // probes 64 entries per step (ballot), and the walk - whose state is wave-uniform, kept in
 // SGPRs via readfirstlane - refills a 64-node (p, f, t) window with one coalesced load and
-// reads each step's node from it with readlane.  Lane 0 does the path / t stores; a fence
-// after each walk and L2 loads of t make its marks visible to the other lanes' probes.
+// reads each step's node from it with readlane.  A fence after each walk and L2 loads of t
+// make the walk's marks visible to the next probes.
 constexpr int64_t kBtLong = 1024;
 
 __device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -1110,12 +1111,19 @@ __global__ void bt_long_list_kernel(const int64_t *g_start, int32_t n_groups, in
 
 __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, const int32_t *list, const int32_t *cnt,
                                                             int32_t *counter) {
+    // No lane-divergent branch anywhere in the loops: the compiler may let lanes that skip
+    // an `if (lane == 0)` region run ahead into the next iteration, where a readfirstlane /
+    // readlane / ballot would then see a partial wave.  Single-address stores are executed
+    // by every lane (same value, same address); the work counter goes through LDS with
+    // barriers (one wave per workgroup, so they cost nothing but force convergence).
+    __shared__ int32_t s_w;
     const int lane = threadIdx.x;
     const int32_t n_long = uni(ld_l2(cnt));
     for (;;) {
-        int32_t w = 0;
-        if (lane == 0) w = atomicAdd(counter, 1);
-        w = uni(w);  // lane 0 is the first active lane
+        if (lane == 0) s_w = atomicAdd(counter, 1);
+        __syncthreads();
+        const int32_t w = uni(s_w);
+        __syncthreads();
         if (w >= n_long) break;
         const int32_t g = uni(list[w]);
         const int64_t g0 = uni64(P.g_start[g]);
@@ -1123,7 +1131,10 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
         int64_t wpos = g0;
         int nc = 0;
         int64_t k = z1 - 1;
+        uint64_t c_probe = 0, c_walk = 0, c_step = 0, c_reload = 0, t_walk = 0, t_post = 0;
+        const uint64_t t_g0 = P.prof ? clock64() : 0;
         while (k >= z0) {
+            c_probe++;
             const int64_t kk = k - lane;
             const int32_t zc = kk >= z0 ? P.z_idx[kk] : 0;
             const int32_t tv = kk >= z0 ? ld_l2(P.t + zc) : 1;
@@ -1137,60 +1148,89 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             k -= hit + 1;
             const int32_t zf = uni(P.f[zi]);
             int64_t *buf = P.chain_ids + wpos;
-            int64_t len = 0, nv = 0;
+            buf[0] = zi;  // every lane: same value, same address
+            int64_t len = 1, nv = 0;  // recorded path nodes; chain = path[0, nv)
             int32_t max_s = 0;
-            int64_t i = zi, nxt = uni64(P.p[zi]);
+            int64_t nxt = uni64(P.p[zi]);
             int64_t whi = -1;  // window: lane l holds anchor whi - l
             int64_t wp = -1;
             int32_t wf = 0, wt = 1;
+            c_walk++;
+            const uint64_t t_w0 = P.prof ? clock64() : 0;
+            // Each round evaluates a RUN of candidates at once: lanes o..R of the window, where
+            // every node's predecessor is the next lane's node (p[j] == j - 1, the common case
+            // along a colinear chain).  The sequential loop's decisions over the run -- running
+            // max of s = zf - f (nv = path length at the last strict increase), the max_drop
+            // break, the break on an already-used node (after that node's max update) -- are a
+            // prefix max and two ballots.  A run ends at the window edge or where p jumps.
             for (;;) {
-                if (lane == 0) {
-                    buf[len] = i;
-                    P.t[i] = 1;
-                }
-                len++;
-                int32_t fn = 0, tn = 1;
-                int64_t pn = -1;
-                if (nxt >= 0) {
-                    if (nxt > whi || nxt <= whi - 64) {
-                        whi = nxt;
-                        const int64_t j = nxt - lane;
-                        const bool ok = j >= g0;
-                        wp = ok ? P.p[j] : -1;
-                        wf = ok ? P.f[j] : 0;
-                        wt = ok ? ld_l2(P.t + j) : 1;
-                    }
-                    const int o = (int)(whi - nxt);
-                    fn = __builtin_amdgcn_readlane(wf, o);
-                    tn = __builtin_amdgcn_readlane(wt, o);
-                    pn = rlane64(wp, o);
-                }
-                const int32_t s = nxt < 0 ? zf : zf - fn;
-                if (s > max_s) {
-                    max_s = s;
-                    nv = len;
-                } else if (max_s - s > P.max_drop) {
+                c_step++;
+                if (nxt < 0) {  // the path reached the start of its chain
+                    if (zf > max_s) max_s = zf, nv = len;
                     break;
                 }
-                if (nxt < 0 || tn != 0) break;
-                i = nxt;
-                nxt = pn;
-            }
-            const int32_t sc = nv == 0 ? 0 : max_s;
-            if (lane == 0) {
-                for (int64_t a = nv; a < len; a++) P.t[buf[a]] = 0;
-                if (sc >= P.min_sc && nv > 0 && nv >= P.min_cnt) {
-                    P.chain_u[g0 + nc] = (uint64_t)(uint32_t)sc << 32 | (uint32_t)nv;
-                    P.chain_first[g0 + nc] = wpos;
+                if (nxt > whi || nxt <= whi - 64) {
+                    c_reload++;
+                    whi = nxt;
+                    const int64_t jj = nxt - lane;
+                    const bool ok = jj >= g0;
+                    wp = ok ? P.p[jj] : -1;
+                    wf = ok ? P.f[jj] : 0;
+                    wt = ok ? ld_l2(P.t + jj) : 1;
                 }
+                const int o = (int)(whi - nxt);
+                const int64_t j = whi - lane;
+                const bool in = lane >= o;
+                const uint64_t ms = __ballot(in && (lane == 63 || wp != j - 1 || j - 1 < g0));
+                const int R = uni(__ffsll((unsigned long long)ms) - 1);
+                const bool cand = in && lane <= R;
+                const int32_t sv = cand ? zf - wf : INT32_MIN;
+                const int32_t incl = scan_max(sv);
+                const int32_t ex = max(max_s, shr1(incl, INT32_MIN));
+                const bool upd = cand && sv > ex;
+                const bool drop = cand && !upd && (int64_t)ex - sv > P.max_drop;
+                const uint64_t mdrop = __ballot(drop);
+                const uint64_t mb = mdrop | __ballot(cand && wt != 0);
+                const uint64_t mupd = __ballot(upd);
+                int last = R, ulim = R;  // lanes o..last recorded; updates up to lane ulim count
+                const bool done = mb != 0;
+                if (done) {
+                    const int E = uni(__ffsll((unsigned long long)mb) - 1);
+                    last = E - 1;
+                    ulim = (mdrop >> E) & 1 ? E - 1 : E;
+                }
+                const uint64_t lim = ulim < 0 ? 0ull : ulim >= 63 ? ~0ull : (2ull << ulim) - 1;
+                const uint64_t mu = mupd & lim;
+                if (mu) {
+                    const int u = 63 - __clzll((long long)mu);
+                    nv = len + (u - o);
+                    max_s = __builtin_amdgcn_readlane(incl, u);  // = s_u: it beat every earlier value
+                }
+                if (lane >= o && lane <= last) buf[len + (lane - o)] = j;
+                len += last - o + 1;
+                if (done) break;
+                nxt = rlane64(wp, R);  // predecessor of the run's last node
             }
+            const uint64_t t_w1 = P.prof ? clock64() : 0;
+            t_walk += t_w1 - t_w0;
+            // the chain is path[0, nv): mark it (the walk itself never re-reads its own nodes)
+            __threadfence();
+            for (int64_t a = lane; a < nv; a += 64) P.t[ld_l2(buf + a)] = 1;
+            const int32_t sc = nv == 0 ? 0 : max_s;
             if (sc >= P.min_sc && nv > 0 && nv >= P.min_cnt) {
+                P.chain_u[g0 + nc] = (uint64_t)(uint32_t)sc << 32 | (uint32_t)nv;  // every lane: same value
+                P.chain_first[g0 + nc] = wpos;
                 nc++;
                 wpos += nv;
             }
             __threadfence();
+            if (P.prof) t_post += clock64() - t_w1;
         }
-        if (lane == 0) P.n_chains[g] = nc;
+        P.n_chains[g] = nc;
+        if (P.prof) {  // every lane adds, lane 0 the value (no divergent region)
+            const uint64_t v[8] = {1, c_probe, c_walk, c_step, c_reload, t_walk, t_post, clock64() - t_g0};
+            for (int q = 0; q < 8; q++) atomicAdd(P.prof + q, lane == 0 ? (unsigned long long)v[q] : 0ull);
+        }
     }
 }
 
@@ -1308,8 +1348,14 @@ int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, c
     HY_HIP(hipMemsetAsync(t, 0, 4 * (size_t)n_anchors, ctx->stream));
     const char *ev = getenv("HYMET_BT_LONG");
     const int64_t long_min = ev ? atoll(ev) : kBtLong;
-    BacktrackParams P{g_start,  f,       p,        t,           z_off,   z_idx, n_groups, min_cnt, min_sc, max_drop,
-                      long_min, chain_ids, chain_u, chain_first, n_chains};
+    const bool prof = getenv("HYMET_BT_PROF") != nullptr;
+    DevBuf pbuf;
+    if (prof) {
+        HY_HIP(pbuf.alloc(64, ctx->stream));
+        HY_HIP(hipMemsetAsync(pbuf.p, 0, 64, ctx->stream));
+    }
+    BacktrackParams P{g_start,  f,         p,       t,           z_off,    z_idx, n_groups, min_cnt, min_sc, max_drop,
+                      long_min, (unsigned long long *)pbuf.p, chain_ids, chain_u, chain_first, n_chains};
     DevBuf list, cnt;
     HY_HIP(list.alloc(4 * (size_t)n_groups, ctx->stream));
     HY_HIP(cnt.alloc(8, ctx->stream));
@@ -1321,9 +1367,19 @@ int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, c
     HY_CHECK_LAUNCH("bt_long_list_kernel");
     hipLaunchKernelGGL(backtrack_groups_kernel, dim3((unsigned)cdiv(n_groups, 64)), dim3(64), 0, ctx->stream, P);
     HY_CHECK_LAUNCH("backtrack_groups_kernel");
-    hipLaunchKernelGGL(backtrack_long_kernel, dim3((unsigned)ctx->n_cu * 4), dim3(64), 0, ctx->stream, P,
-                       list.as<int32_t>(), cnt.as<int32_t>(), cnt.as<int32_t>() + 1);
-    HY_CHECK_LAUNCH("backtrack_long_kernel");
+    {
+        ProfScope _pl(ctx, "mm_backtrack.long");  // the wave-per-group part of mm_backtrack
+        hipLaunchKernelGGL(backtrack_long_kernel, dim3((unsigned)ctx->n_cu * 8), dim3(64), 0, ctx->stream, P,
+                           list.as<int32_t>(), cnt.as<int32_t>(), cnt.as<int32_t>() + 1);
+        HY_CHECK_LAUNCH("backtrack_long_kernel");
+    }
+    if (prof) {
+        unsigned long long h[8];
+        HY_HIP(hipMemcpyAsync(h, pbuf.p, 64, hipMemcpyDeviceToHost, ctx->stream));
+        HY_HIP(hipStreamSynchronize(ctx->stream));
+        fprintf(stderr, "[bt_long] groups=%llu probes=%llu walks=%llu steps=%llu reloads=%llu cyc_walk=%.3g cyc_post=%.3g cyc_all=%.3g\n",
+                h[0], h[1], h[2], h[3], h[4], (double)h[5], (double)h[6], (double)h[7]);
+    }
     return HYMET_OK;
 }
 

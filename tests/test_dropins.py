@@ -1,8 +1,10 @@
 """Stage drop-ins under scripts/ (SURVEY.md §8b): argv, output files, stdout and exit codes.
 
-CPU: scripts/limit_candidates.py against the reference-generated goldens (output bytes,
-stdout, rc).  GPU: scripts/mash.sh, scripts/minimap2.sh and scripts/classification*.py run
-as subprocesses on small inputs and compared with the oracle / the reference goldens."""
+CPU: scripts/limit_candidates.py run as a subprocess against the reference-generated goldens
+(output bytes, stdout, rc); every wrapper script reaches its subcommand (usage errors).
+GPU: the screen / map / classify subcommands behind scripts/mash.sh, scripts/minimap2.sh and
+scripts/classification*.py, called in-process (the test process already holds the GPU) on
+small inputs and compared with the oracle."""
 import json
 import os
 import subprocess
@@ -62,6 +64,18 @@ def test_limit_dropin_log_append(tmp_path):
     assert log.read_text().splitlines() == [r.stdout.rstrip("\n")] * 2
 
 
+@pytest.mark.parametrize("script", ["mash.sh", "minimap2.sh"])
+def test_shell_wrappers_reach_subcommand(script, tmp_path):
+    r = _run(["bash", str(SCRIPTS / script), "only-one-arg"])
+    assert r.returncode == 2 and "usage:" in r.stderr
+
+
+@pytest.mark.parametrize("script", ["classification_cami.py", "classification.py"])
+def test_python_wrappers_reach_subcommand(script):
+    r = _run([sys.executable, str(SCRIPTS / script), "--paf", "x"])
+    assert r.returncode == 2 and "--taxonomy" in r.stderr
+
+
 # ---------------------------------------------------------------------------- GPU
 def _fasta(path, recs):
     with open(path, "w") as f:
@@ -72,7 +86,8 @@ def _fasta(path, recs):
 
 
 @pytest.mark.gpu
-def test_screen_map_classify_dropins_match_oracle(tmp_path):
+def test_screen_map_classify_dropins_match_oracle(tmp_path, capsys):
+    from hymet_amd.cli import main as cli
     from hymet_amd import synth
     from hymet_amd.msh import SketchDB, write_msh
     from oracle import classify_oracle, oracle_lib, pipeline_oracle, select_oracle
@@ -94,8 +109,8 @@ def test_screen_map_classify_dropins_match_oracle(tmp_path):
     _fasta(inp / "contigs.fna", recs)
     # ---- mash.sh
     outs = [tmp_path / f for f in ("screen.tab", "filtered.tab", "sorted.tab", "top_hits.tab", "selected.txt")]
-    r = _run(["bash", str(SCRIPTS / "mash.sh"), str(inp), str(msh)] + [str(o) for o in outs] + ["0.90"])
-    assert r.returncode == 0, r.stderr
+    assert cli(["screen", str(inp), str(msh)] + [str(o) for o in outs] + ["0.90"]) == 0
+    stdout = capsys.readouterr().out
     rows = pipeline_oracle.screen_rows([s for _, s in recs], db)
     assert outs[0].read_text().splitlines() == rows
     srt = select_oracle.sort_gr(select_oracle.sort_unique_k5(rows))
@@ -103,7 +118,7 @@ def test_screen_map_classify_dropins_match_oracle(tmp_path):
     t, top, sel_names, _ = select_oracle.select_threshold(srt, "0.90", 1)
     assert outs[3].read_text().splitlines() == top
     assert outs[4].read_text().splitlines() == sel_names
-    assert f"Final threshold used: {t}" in r.stdout
+    assert f"Final threshold used: {t}" in stdout
     # ---- minimap2.sh over the selected genomes
     by_name = {n + ".fna.gz": (n, s) for n, s in zip(w.ref_names, w.refs)}
     chosen = [by_name[n] for n in sel_names if n in by_name]
@@ -112,23 +127,20 @@ def test_screen_map_classify_dropins_match_oracle(tmp_path):
     _fasta(ref_fa, chosen)
     paf = tmp_path / "resultados.paf"
     mmi = tmp_path / "reference.mmi"
-    r = _run(["bash", str(SCRIPTS / "minimap2.sh"), str(inp), str(ref_fa), str(mmi), str(paf)])
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert "Creating index with minimap2..." in r.stdout and mmi.stat().st_size > 0
+    assert cli(["map", str(inp), str(ref_fa), str(mmi), str(paf)]) == 0
+    assert "Creating index with minimap2..." in capsys.readouterr().out and mmi.stat().st_size > 0
     o_paf = pipeline_oracle.map_paf([n for n, _ in chosen], [s for _, s in chosen], recs)
     assert paf.read_text().splitlines() == o_paf
-    r = _run(["bash", str(SCRIPTS / "minimap2.sh"), str(inp), str(ref_fa), str(mmi), str(paf)])
-    assert r.returncode == 0 and "Using cached minimap2 index" in r.stdout
+    assert cli(["map", str(inp), str(ref_fa), str(mmi), str(paf)]) == 0
+    assert "Using cached minimap2 index" in capsys.readouterr().out
     assert paf.read_text().splitlines() == o_paf
     # ---- classification_cami.py / classification.py
     tax = tmp_path / "detailed_taxonomy.tsv"
     tax.write_text(w.taxonomy_tsv())
     hier = tmp_path / "taxonomy_hierarchy.tsv"
     hier.write_text(w.hierarchy_tsv())
-    for script, fn in (("classification_cami.py", classify_oracle.classify_cami),
-                       ("classification.py", classify_oracle.classify_legacy)):
-        out = tmp_path / f"{script}.tsv"
-        r = _run([sys.executable, str(SCRIPTS / script), "--paf", str(paf), "--taxonomy", str(tax), "--hierarchy",
-                  str(hier), "--output", str(out), "--processes", "2"])
-        assert r.returncode == 0, r.stderr
+    for sub, fn in (("classify", classify_oracle.classify_cami), ("classify-legacy", classify_oracle.classify_legacy)):
+        out = tmp_path / f"{sub}.tsv"
+        assert cli([sub, "--paf", str(paf), "--taxonomy", str(tax), "--hierarchy", str(hier), "--output", str(out),
+                    "--processes", "2"]) == 0
         assert out.read_bytes() == fn(str(paf), str(tax), str(hier))
