@@ -59,6 +59,13 @@ struct DevBuf {
     }
     template <typename T>
     T *as() const { return reinterpret_cast<T *>(p); }
+    // exchange whole buffers: the size class travels with the pointer (the scratch cache
+    // files a block under its class when it is released)
+    void swap(DevBuf &o) {
+        std::swap(p, o.p);
+        std::swap(n, o.n);
+        std::swap(cls, o.cls);
+    }
 };
 
 struct SketchParams {

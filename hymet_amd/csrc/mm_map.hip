@@ -17,6 +17,7 @@
 #include "mm_common.hpp"
 
 #include <algorithm>
+#include <utility>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -293,9 +294,106 @@ __global__ void write_anchors_kernel(AnchorParams P) {
     }
 }
 
-__global__ void group_flag_kernel(const uint64_t *k1, int64_t n, uint32_t *flag) {
+// Anchor keys (the default path): one 64-bit key per anchor packing exactly the sort order
+// of (query, x) -- K = q | rev | rid | rpos, field widths from the batch (query count,
+// index sequences, longest index sequence) -- and the low 32 bits of y as the value.  The
+// high bits of y hold the span, which is k for every minimizer of a non-HPC sketch.  One
+// block per 256 consecutive minimizers: the block stages their anchor offsets, position-list
+// starts and query coordinates in LDS, then its 256 lanes sweep the block's anchors
+// (contiguous in both the position lists and the output), finding each anchor's minimizer
+// by binary search in LDS -- coalesced reads and writes where a lane per minimizer would
+// write 20-60 scattered anchors.
+struct AnchorKeyParams {
+    const uint64_t *mx, *my;
+    const uint32_t *seed_n;
+    const int64_t *a_pos;     // anchor offset of every minimizer (M + 1 entries)
+    const uint32_t *qid;
+    const int64_t *qlen;
+    const uint32_t *koff;
+    const uint64_t *ipos;
+    int64_t n;                // minimizers
+    int rb, pb;               // bits for rid / rpos
+    uint64_t *key;
+    uint32_t *val;
+    const int64_t *mp_pos;
+    uint64_t *mini_pos;
+};
+
+__global__ __launch_bounds__(256) void write_anchor_keys_kernel(AnchorKeyParams P) {
+    __shared__ int64_t s_a[257];
+    __shared__ uint64_t s_r[256];   // start of the minimizer's position list
+    __shared__ uint32_t s_yf[256], s_yr[256], s_strand[256];
+    __shared__ uint64_t s_q[256];   // q << (1 + rb + pb)
+    const int tid = threadIdx.x;
+    const int64_t m0 = (int64_t)blockIdx.x * 256;
+    const int cnt = (int)min((int64_t)256, P.n - m0);
+    if (tid < cnt) {
+        const int64_t i = m0 + tid;
+        const uint32_t n = P.seed_n[i];
+        const uint64_t mx = P.mx[i], my = P.my[i];
+        const uint32_t q_pos = (uint32_t)my, q_span = (uint32_t)(mx & 0xff);
+        const uint32_t q = P.qid[i];
+        if (n) P.mini_pos[P.mp_pos[i]] = (uint64_t)q_span << 32 | (q_pos >> 1);
+        s_a[tid] = P.a_pos[i];
+        s_r[tid] = P.koff[mx >> 8];
+        s_yf[tid] = q_pos >> 1;
+        s_yr[tid] = (uint32_t)((int32_t)P.qlen[q] - (int32_t)((q_pos >> 1) + 1 - q_span) - 1);
+        s_strand[tid] = q_pos & 1;
+        s_q[tid] = (uint64_t)q << (1 + P.rb + P.pb);
+    }
+    if (tid == 0) s_a[cnt] = P.a_pos[m0 + cnt];
+    __syncthreads();
+    const int64_t a0 = s_a[0], a1 = s_a[cnt];
+    const int sh_rev = P.rb + P.pb;
+    for (int64_t a = a0 + tid; a < a1; a += 256) {
+        int lo = 0, hi = cnt - 1;  // last s with s_a[s] <= a (its list is non-empty)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_a[mid] <= a) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint64_t rk = P.ipos[s_r[lo] + (a - s_a[lo])];
+        const uint32_t rpos = (uint32_t)rk >> 1;
+        const uint64_t rid = rk >> 32;
+        const uint32_t rev = ((uint32_t)rk & 1) != s_strand[lo];
+        P.key[a] = s_q[lo] | (uint64_t)rev << sh_rev | rid << P.pb | rpos;
+        P.val[a] = rev ? s_yr[lo] : s_yf[lo];
+    }
+}
+
+// sorted keys -> (x, y); runs of equal key (one query minimizer position hit by several
+// query minimizers) are ordered by y here: the lane at a run's start writes the run's y
+// values by insertion sort (runs are short and rare), the other lanes of the run skip y.
+__global__ void anchor_unpack_kernel(const uint64_t *key, const uint32_t *val, int64_t n, int rb, int pb, uint64_t yhi,
+                                     uint64_t *ax, uint64_t *ay) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) flag[i] = (i == 0 || k1[i] != k1[i - 1]) ? 1u : 0u;
+    if (i >= n) return;
+    const uint64_t k = key[i];
+    const uint64_t rev = k >> (rb + pb) & 1, rid = k >> pb & ((1ull << rb) - 1), rpos = k & ((1ull << pb) - 1);
+    ax[i] = rev << 63 | rid << 32 | rpos;
+    const bool prev_eq = i > 0 && key[i - 1] == k;
+    const bool next_eq = i + 1 < n && key[i + 1] == k;
+    if (!prev_eq && !next_eq) {
+        ay[i] = yhi << 32 | val[i];
+    } else if (!prev_eq) {
+        int64_t e = i + 1;
+        while (e + 1 < n && key[e + 1] == k) e++;
+        for (int64_t a = i; a <= e; a++) {
+            const uint64_t v = yhi << 32 | val[a];
+            int64_t b = a;
+            while (b > i && ay[b - 1] > v) {
+                ay[b] = ay[b - 1];
+                b--;
+            }
+            ay[b] = v;
+        }
+    }
+}
+
+// group = (query, strand, target): the key without its low `shift` (rpos) bits
+__global__ void group_flag_kernel(const uint64_t *k1, int64_t n, int shift, uint32_t *flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[i] = (i == 0 || (k1[i] >> shift) != (k1[i - 1] >> shift)) ? 1u : 0u;
 }
 
 __global__ void group_flag_x_kernel(const uint64_t *x, int64_t n, uint32_t *flag) {
@@ -467,7 +565,8 @@ static int bits_for(int64_t v) {
 
 // An anchor set sorted by (query, x, y): arrays + per-query offsets (device + host).
 struct AnchorSet {
-    DevBuf ax, ay, k1;
+    DevBuf ax, ay, k1;  // k1 >> gshift = group (query, strand, target)
+    int gshift = 0;
     int64_t n = 0;
     std::vector<int64_t> h_off;  // n_q + 1
     DevBuf d_off;
@@ -510,6 +609,30 @@ static int sort_anchor_set(hymet_ctx *ctx, DevBuf &x, DevBuf &y, DevBuf &k1, Dev
     return HYMET_OK;
 }
 
+// sort anchor keys (write_anchor_keys_kernel / rechain_keys_kernel) into an AnchorSet: one
+// LSD radix sort over the key's significant bits, then unpack to (x, y)
+static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n, int end_bit, int rb, int pb, int yhi,
+                            AnchorSet &out) {
+    DevBuf kb, vb;
+    HY_HIP(kb.alloc(8 * (size_t)n, ctx->stream));
+    HY_HIP(vb.alloc(4 * (size_t)n, ctx->stream));
+    uint64_t *kk = key.as<uint64_t>(), *kka = kb.as<uint64_t>();
+    uint32_t *vv = val.as<uint32_t>(), *vva = vb.as<uint32_t>();
+    int rc = sort_pairs(ctx, kk, kka, vv, vva, n, 0, end_bit, "radix_sort_anchors");
+    if (rc) return rc;
+    HY_HIP(out.ax.alloc(8 * (size_t)n, ctx->stream));
+    HY_HIP(out.ay.alloc(8 * (size_t)n, ctx->stream));
+    {
+        ProfScope _ps(ctx, "mm_anchor_unpack", 28.0 * (double)n);  // key + value read, x + y write
+        LAUNCH1(anchor_unpack_kernel, n, kk, vv, n, rb, pb, (uint64_t)yhi, out.ax.as<uint64_t>(), out.ay.as<uint64_t>());
+    }
+    if (kk == kb.as<uint64_t>()) out.k1.swap(kb);
+    else out.k1.swap(key);
+    out.gshift = pb;
+    out.n = n;
+    return HYMET_OK;
+}
+
 // chaining + backtrack + compact_a over an anchor set
 static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, float pen_skip, int bw, AnchorSet &A,
                      int n_q, ChainSet &C) {
@@ -526,7 +649,7 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
     // groups
     DevBuf flag, gpos, gid;
     HY_HIP(flag.alloc(4 * (size_t)n, ctx->stream));
-    LAUNCH1(group_flag_kernel, n, A.k1.as<uint64_t>(), n, flag.as<uint32_t>());
+    LAUNCH1(group_flag_kernel, n, A.k1.as<uint64_t>(), n, A.gshift, flag.as<uint32_t>());
     int64_t G = 0;
     int rc = scan_flags(ctx, flag.as<uint32_t>(), n, gpos, &G);
     if (rc) return rc;
@@ -668,7 +791,7 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(cf_s.alloc(8 * (size_t)(NC + 1), ctx->stream));
         LAUNCH1(gather_kernel<uint64_t>, NC, C.cu.as<uint64_t>(), pp, cu_s.as<uint64_t>(), NC);
         LAUNCH1(gather_kernel<int64_t>, NC, cfirst.as<int64_t>(), pp, cf_s.as<int64_t>(), NC);
-        std::swap(C.cu.p, cu_s.p);
+        C.cu.swap(cu_s);
         // anchors of every chain, compacted in chain order
         DevBuf ccnt;
         HY_HIP(ccnt.alloc(4 * (size_t)(NC + 1), ctx->stream));
@@ -750,6 +873,20 @@ __global__ void rechain_gather_kernel(const uint64_t *bx, const uint64_t *by, co
         k1[a] = (uint64_t)q << (1 + rb) | (ax >> 63) << rb | (ax << 1 >> 33);
         k2[a] = (uint64_t)(uint32_t)ax << 32 | (uint32_t)ay;
         val[a] = (uint32_t)a;
+    }
+}
+
+__global__ void rechain_keys_kernel(const uint64_t *bx, const uint64_t *by, const int64_t *qb, const uint32_t *qflag,
+                                    const int64_t *new_off, int n_q, int rb, int pb, uint64_t *key, uint32_t *val) {
+    const int q = blockIdx.x;
+    if (q >= n_q || !qflag[q]) return;
+    const int64_t b0 = qb[q], b1 = qb[q + 1], o = new_off[q];
+    const uint64_t kq = (uint64_t)q << (1 + rb + pb);
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
+        const int64_t a = o + (i - b0);
+        const uint64_t ax = bx[i];
+        key[a] = kq | (ax >> 63) << (rb + pb) | (ax << 1 >> 33) << pb | (uint32_t)ax;
+        val[a] = (uint32_t)by[i];
     }
 }
 
@@ -844,9 +981,9 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
         hipLaunchKernelGGL(sample_off_kernel, dim3((unsigned)cdiv(n_q + 1, 256)), dim3(256), 0, st, kpos.as<int64_t>(),
                            qm_off.as<int64_t>(), n_q, M2, nqm.as<int64_t>());
         HY_CHECK_LAUNCH("sample_off_kernel");
-        std::swap(mx.p, nx.p);
-        std::swap(my.p, ny.p);
-        std::swap(qm_off.p, nqm.p);
+        mx.swap(nx);
+        my.swap(ny);
+        qm_off.swap(nqm);
         M = M2;
         HY_HIP(hipMemcpyAsync(h_qm.data(), qm_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, st));
         HY_HIP(hipStreamSynchronize(st));
@@ -898,7 +1035,29 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
     const int rb = bits_for(idx->n_seq);
     const int key1_bits = bits_for(n_q) + 1 + rb;
     HY_ARG(key1_bits <= 64, "hymet_mm_map: too many queries x targets for the sort key");
-    {
+    int64_t max_len = 1;
+    for (int64_t l : idx->h_len) max_len = std::max(max_len, l);
+    const int pb = bits_for(max_len - 1);
+    // one-key anchor sort when (query, strand, rid, rpos) fits 64 bits (always, short of
+    // ~2^20 queries per batch against chromosome-scale targets); else the two-key path
+    const bool key_path = key1_bits + pb <= 64 && !getenv("HYMET_ANCHOR_LEGACY");
+    if (key_path) {
+        DevBuf key, val;
+        HY_HIP(key.alloc(8 * (size_t)(A + 1), st));
+        HY_HIP(val.alloc(4 * (size_t)(A + 1), st));
+        AnchorKeyParams P{mx.as<uint64_t>(), my.as<uint64_t>(), seed_n.as<uint32_t>(), a_pos.as<int64_t>(),
+                          qid.as<uint32_t>(), d_qlen.as<int64_t>(), idx->d_koff, idx->d_pos, M, rb, pb,
+                          key.as<uint64_t>(), val.as<uint32_t>(), mp_pos.as<int64_t>(), mini_pos.as<uint64_t>()};
+        {
+            ProfScope _ps(ctx, "mm_anchors", (double)A * (8.0 + 12.0));  // position fetch + key/value write
+            if (M > 0) {
+                hipLaunchKernelGGL(write_anchor_keys_kernel, dim3((unsigned)cdiv(M, 256)), dim3(256), 0, st, P);
+                HY_CHECK_LAUNCH("write_anchor_keys_kernel");
+            }
+        }
+        rc = sort_anchor_keys(ctx, key, val, A, key1_bits + pb, rb, pb, k, S1);
+        if (rc) return rc;
+    } else {
         DevBuf x, y, k1, k2, val;
         HY_HIP(x.alloc(8 * (size_t)(A + 1), st));
         HY_HIP(y.alloc(8 * (size_t)(A + 1), st));
@@ -942,18 +1101,30 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
             const int64_t A2 = S2.h_off[n_q];
             HY_HIP(S2.d_off.alloc(8 * (size_t)(n_q + 1), st));
             HY_HIP(hipMemcpyAsync(S2.d_off.p, S2.h_off.data(), 8 * (size_t)(n_q + 1), hipMemcpyHostToDevice, st));
-            DevBuf x, y, k1, k2, val;
-            HY_HIP(x.alloc(8 * (size_t)(A2 + 1), st));
-            HY_HIP(y.alloc(8 * (size_t)(A2 + 1), st));
-            HY_HIP(k1.alloc(8 * (size_t)(A2 + 1), st));
-            HY_HIP(k2.alloc(8 * (size_t)(A2 + 1), st));
-            HY_HIP(val.alloc(4 * (size_t)(A2 + 1), st));
-            hipLaunchKernelGGL(rechain_gather_kernel, dim3((unsigned)n_q), dim3(256), 0, st, C1.bx.as<uint64_t>(),
-                               C1.by.as<uint64_t>(), C1.d_qb.as<int64_t>(), flag.as<uint32_t>(), S2.d_off.as<int64_t>(), n_q,
-                               rb, x.as<uint64_t>(), y.as<uint64_t>(), k1.as<uint64_t>(), k2.as<uint64_t>(), val.as<uint32_t>());
-            HY_CHECK_LAUNCH("rechain_gather_kernel");
-            rc = sort_anchor_set(ctx, x, y, k1, k2, val, A2, key1_bits, S2);
-            if (rc) return rc;
+            if (key_path) {
+                DevBuf key, val;
+                HY_HIP(key.alloc(8 * (size_t)(A2 + 1), st));
+                HY_HIP(val.alloc(4 * (size_t)(A2 + 1), st));
+                hipLaunchKernelGGL(rechain_keys_kernel, dim3((unsigned)n_q), dim3(256), 0, st, C1.bx.as<uint64_t>(),
+                                   C1.by.as<uint64_t>(), C1.d_qb.as<int64_t>(), flag.as<uint32_t>(), S2.d_off.as<int64_t>(),
+                                   n_q, rb, pb, key.as<uint64_t>(), val.as<uint32_t>());
+                HY_CHECK_LAUNCH("rechain_keys_kernel");
+                rc = sort_anchor_keys(ctx, key, val, A2, key1_bits + pb, rb, pb, k, S2);
+                if (rc) return rc;
+            } else {
+                DevBuf x, y, k1, k2, val;
+                HY_HIP(x.alloc(8 * (size_t)(A2 + 1), st));
+                HY_HIP(y.alloc(8 * (size_t)(A2 + 1), st));
+                HY_HIP(k1.alloc(8 * (size_t)(A2 + 1), st));
+                HY_HIP(k2.alloc(8 * (size_t)(A2 + 1), st));
+                HY_HIP(val.alloc(4 * (size_t)(A2 + 1), st));
+                hipLaunchKernelGGL(rechain_gather_kernel, dim3((unsigned)n_q), dim3(256), 0, st, C1.bx.as<uint64_t>(),
+                                   C1.by.as<uint64_t>(), C1.d_qb.as<int64_t>(), flag.as<uint32_t>(), S2.d_off.as<int64_t>(), n_q,
+                                   rb, x.as<uint64_t>(), y.as<uint64_t>(), k1.as<uint64_t>(), k2.as<uint64_t>(), val.as<uint32_t>());
+                HY_CHECK_LAUNCH("rechain_gather_kernel");
+                rc = sort_anchor_set(ctx, x, y, k1, k2, val, A2, key1_bits, S2);
+                if (rc) return rc;
+            }
             rc = chain_set(ctx, opt, pen_gap, pen_skip, opt->bw_long, S2, n_q, C2);
             if (rc) return rc;
             // merge: flagged queries take C2's chains, the others keep C1's

@@ -46,14 +46,22 @@ def _queries(rng, refs):
     qs.append(("empty", b""))
     qs.append(("allN", b"N" * 3000))
     qs.append(("long", mutate(rng, refs[1][0:300_000], 0.01)))
+    # several copies of the 2 kb repeat: query minimizers of every copy hit the same target
+    # positions, so anchors tie on (query, x) and are ordered by y (both strands)
+    qs.append(("repeat_fwd", refs[5][49_000:62_500]))
+    qs.append(("repeat_rev", revcomp(refs[5][49_500:63_000])))
     return qs
 
 
-@pytest.mark.parametrize("bt_long", [None, "4"])
-def test_map_matches_oracle(gpu, monkeypatch, bt_long):
-    """bt_long = "4": nearly every chain group takes the wave-per-group backtrack path."""
+@pytest.mark.parametrize("bt_long,legacy", [(None, None), ("4", None), (None, "1")])
+def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy):
+    """bt_long = "4": nearly every chain group takes the wave-per-group backtrack path.
+    legacy = "1": anchors take the two-key sort path (used when the one-key anchor sort key
+    would exceed 64 bits)."""
     if bt_long is not None:
         monkeypatch.setenv("HYMET_BT_LONG", bt_long)
+    if legacy is not None:
+        monkeypatch.setenv("HYMET_ANCHOR_LEGACY", legacy)
     from hymet_amd import mapper
     from hymet_amd.seqio import DevicePool, from_records
     from oracle import oracle_lib as ol
