@@ -60,10 +60,11 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise HymetError(f"{LIB_PATH} not found: build the HIP extension (python -m hymet_amd.build); "
+    path = os.environ.get("HYMET_LIB", LIB_PATH)  # a compile-time variant (tools/variants.py) for A/B timing
+    if not os.path.exists(path):
+        raise HymetError(f"{path} not found: build the HIP extension (python -m hymet_amd.build); "
                          "hymet_amd has no CPU fallback")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -20,31 +20,32 @@ def _needs(obj, src, deps):
     return any(os.path.getmtime(d) > t for d in [src] + deps)
 
 
-def build(verbose=False, jobs=8):
-    os.makedirs(OBJ, exist_ok=True)
+def build(verbose=False, jobs=8, extra=(), out=OUT, obj=OBJ):
+    """extra / out / obj: compile-time variants for A/B timing (tools/variants.py)."""
+    os.makedirs(obj, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     deps = glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(HERE, "..", "include", "*.h"))
     objs, procs = [], []
     for s in srcs:
-        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        o = os.path.join(obj, os.path.basename(s) + ".o")
         objs.append(o)
         if _needs(o, s, deps):
-            cmd = ["hipcc", *FLAGS, "-c", s, "-o", o]
+            cmd = ["hipcc", *FLAGS, *extra, "-c", s, "-o", o]
             if verbose:
                 print(" ".join(cmd))
             procs.append((s, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
             while len([p for _, p in procs if p.poll() is None]) >= jobs:
                 procs[0][1].wait()
     for s, p in procs:
-        out = p.communicate()[0].decode()
+        log = p.communicate()[0].decode()
         if p.returncode != 0:
-            raise RuntimeError(f"hipcc failed on {s}:\n{out}")
-        if out.strip() and verbose:
-            print(out)
-    if not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
-        cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT, *objs]
+            raise RuntimeError(f"hipcc failed on {s}:\n{log}")
+        if log.strip() and verbose:
+            print(log)
+    if not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
+        cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out, *objs]
         subprocess.check_call(cmd)
-    return OUT
+    return out
 
 
 if __name__ == "__main__":

@@ -49,18 +49,36 @@ namespace hymet {
 namespace mm {
 namespace {
 
-constexpr int kRing = 256;      // LDS ring of recent anchors, int4 each: 4 KB
+// Occupancy: the kernel is latency-bound, so it is sized for 16 resident waves per CU --
+// registers capped at 128 VGPRs (4 waves per SIMD) and ~9.75 KB of LDS per wave.  Measured
+// on C4: 8 -> 12 -> 16 waves/CU took mm_chain 2198 -> 1873 -> 1744 ms per step.  Every ring
+// and deque has an HBM or slow-path fallback when it overflows.
+#ifndef HYMET_CHAIN_RING
+#define HYMET_CHAIN_RING 128
+#endif
+#ifndef HYMET_CHAIN_SUMRING
+#define HYMET_CHAIN_SUMRING 16
+#endif
+#ifndef HYMET_CHAIN_BDQ
+#define HYMET_CHAIN_BDQ 32
+#endif
+#ifndef HYMET_CHAIN_IDQ
+#define HYMET_CHAIN_IDQ 64
+#endif
+#ifndef HYMET_CHAIN_WPE  // waves per SIMD the register allocation targets (0: compiler's choice)
+#define HYMET_CHAIN_WPE 4
+#endif
+constexpr int kRing = HYMET_CHAIN_RING;  // LDS ring of recent anchors, int4 each (2 KB)
 constexpr int kRingMask = kRing - 1;
 constexpr int kStair = 4;       // staircase entries kept per block summary
 constexpr int kSumInts = kStair + 1;  // int4 words per block summary: staircase + (ymin, ymax, n|trunc, -)
-constexpr int kSumRing = 64;    // LDS ring of block summaries (the last 64 complete blocks): 5 KB
+constexpr int kSumRing = HYMET_CHAIN_SUMRING;  // LDS ring of the last complete block summaries (1.25 KB)
 constexpr int kInnerCap = 256;  // LDS inner-window list (ring-deque) + stamps: 3 KB
-constexpr int kBdq = 128;       // block-argmin deque, 2 int4 per element: 4 KB
-constexpr int kIdq = 256;       // inner max-deque (idx, f + span): 2 KB
+constexpr int kBdq = HYMET_CHAIN_BDQ;  // block-argmin deque, 2 int4 per element (1 KB)
+constexpr int kIdq = HYMET_CHAIN_IDQ;  // inner max-deque (idx, f + span) (0.5 KB)
 constexpr size_t kChainLds = kRing * sizeof(int4) + kSumRing * kSumInts * sizeof(int4) + 64 * 2 * sizeof(int4) +
                              kInnerCap * (sizeof(int2) + sizeof(int32_t)) + kBdq * 2 * sizeof(int4) + kIdq * sizeof(int2);
 constexpr int kNegInf = -(1 << 29);
-constexpr int kMaxGroup = 1 << 24;  // p+1 and span share one 32-bit ring word
 
 // Section cycle counters for tools/chain_prof (built with -DHYMET_CHAIN_PROF); no-ops otherwise.
 #ifdef HYMET_CHAIN_PROF
@@ -281,7 +299,12 @@ __device__ __forceinline__ int4 pack_st(double pr, int32_t j, int32_t y) {
 }
 __device__ __forceinline__ double st_pr(const int4 &v) { return __hiloint2double(v.y, v.x); }
 
-__global__ __launch_bounds__(64) void chain_groups_kernel(ChainParams P) {
+#if HYMET_CHAIN_WPE > 0
+#define HYMET_CHAIN_ATTR __attribute__((amdgpu_waves_per_eu(HYMET_CHAIN_WPE)))
+#else
+#define HYMET_CHAIN_ATTR
+#endif
+__global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(ChainParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
     unsigned char *sp = smem;
@@ -799,7 +822,9 @@ __global__ __launch_bounds__(64) void chain_groups_kernel(ChainParams P) {
                         // entry k-1 (k = i + lane, lane >= 1) is inserted at anchor k
                         if (lane >= 1 && !key_less(py, i + lane - 1, gy, gj)) ok = false;
                     }
+#ifdef HYMET_CHAIN_PROF
                     const bool ok_geom = ok;
+#endif
                     ok = ok && cand_ok && wok;
                     const uint64_t bad = __ballot(!ok);
                     const int acc = bad ? __ffsll((unsigned long long)bad) - 1 : 64;
@@ -1331,9 +1356,13 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
     if (max_dist < bw) max_dist = bw;
     if (max_dist_inner <= 0 || max_dist_inner >= max_dist) max_dist_inner = 0;
     ChainParams P{ax, ay, g_start, g_qfirst, order, n_work, cnt.as<int32_t>(), f, p, t_global, sum.as<int4>(), max_dist, max_dist_inner, bw, max_chn_skip, cap_rmq_size, pen_gap, pen_skip};
-    // one wave per block; LDS (kChainLds ~20 KB) allows 8 resident waves per CU
+    // one wave per block, as many resident per CU as registers and LDS allow
     int64_t blocks = n_work;
-    const int64_t cap = (int64_t)ctx->n_cu * 8;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_groups_kernel, 64, kChainLds) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 8;
+    const int64_t cap = (int64_t)ctx->n_cu * per_cu;
     if (blocks > cap) blocks = cap;
     ProfScope _ps(ctx, max_dist > 10000 ? "mm_chain_long" : "mm_chain", 28.0 * (double)n_anchors);  // x,y read + f,p write per anchor
     hipLaunchKernelGGL(chain_groups_kernel, dim3((unsigned)blocks), dim3(64), kChainLds, ctx->stream, P);

@@ -449,6 +449,116 @@ __global__ void zoff_kernel(const uint32_t *zg_sorted, int64_t nz, int32_t G, in
     for (int64_t g = gp + 1; g <= gc; g++) z_off[g] = p;
 }
 
+// ---- backtrack order: z = anchors with f >= min_sc, per group ascending (f, idx) (the
+// backtrack walks it from the end: canonical T3).  A group's z entries are a contiguous,
+// idx-ordered run of the flag scan, so the order is a segmented sort of 64-bit (f << 32 |
+// idx) keys: a wave per group of <= 64 entries (bitonic across lanes), a block per group of
+// <= kZs entries (bitonic in LDS), and one global radix sort over the few larger groups.
+constexpr int kZs = 2048;
+
+__global__ void zoff_direct_kernel(const int64_t *g_start, const int64_t *zpos, int32_t G, int64_t nz, int64_t *z_off) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < G) z_off[g] = zpos[g_start[g]];
+    else if (g == G) z_off[G] = nz;
+}
+
+__global__ void zfill_key_kernel(const int32_t *f, const uint32_t *flag, const int64_t *pos, int64_t n, uint64_t *zkey) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && flag[i]) zkey[pos[i]] = (uint64_t)(uint32_t)f[i] << 32 | (uint32_t)i;
+}
+
+__global__ void zclass_kernel(const int64_t *z_off, int32_t G, int32_t *mid_list, int32_t *mid_cnt, uint32_t *big_flag,
+                              uint32_t *big_size) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    const int64_t n = z_off[g + 1] - z_off[g];
+    big_flag[g] = n > kZs ? 1u : 0u;
+    big_size[g] = n > kZs ? (uint32_t)n : 0u;
+    if (n > 64 && n <= kZs) mid_list[atomicAdd(mid_cnt, 1)] = g;
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return (uint64_t)hi << 32 | lo;
+}
+
+// one wave per group with <= 64 z entries (4 groups per 256-thread block)
+__global__ __launch_bounds__(256) void zsort_wave_kernel(const uint64_t *zkey, const int64_t *z_off, int32_t G,
+                                                         int32_t *z_idx) {
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= G) return;
+    const int64_t z0 = z_off[g], n = z_off[g + 1] - z0;
+    if (n > 64 || n == 0) return;
+    uint64_t v = lane < n ? zkey[z0 + lane] : ~0ull;
+    if (n > 1) {
+        for (int k = 2; k <= 64; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const uint64_t o = shfl_xor64(v, j);
+                const bool up = (lane & k) == 0, low = (lane & j) == 0;
+                v = (low == up) ? (o < v ? o : v) : (o > v ? o : v);
+            }
+    }
+    if (lane < n) z_idx[z0 + lane] = (int32_t)(uint32_t)v;
+}
+
+// one block per group with 64 < n <= kZs z entries (grid-stride over the list)
+__global__ __launch_bounds__(256) void zsort_block_kernel(const uint64_t *zkey, const int64_t *z_off, const int32_t *list,
+                                                          const int32_t *cnt, int32_t *z_idx) {
+    __shared__ uint64_t s[kZs];
+    const int n_list = *cnt;
+    for (int w = blockIdx.x; w < n_list; w += gridDim.x) {
+        const int g = list[w];
+        const int64_t z0 = z_off[g];
+        const int n = (int)(z_off[g + 1] - z0);
+        int np = 128;
+        while (np < n) np <<= 1;
+        for (int i = threadIdx.x; i < np; i += 256) s[i] = i < n ? zkey[z0 + i] : ~0ull;
+        __syncthreads();
+        for (int k = 2; k <= np; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = threadIdx.x; i < np; i += 256) {
+                    const int ij = i ^ j;
+                    if (ij > i) {
+                        const uint64_t a = s[i], b = s[ij];
+                        if (((i & k) == 0) == (a > b)) {
+                            s[i] = b;
+                            s[ij] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        for (int i = threadIdx.x; i < n; i += 256) z_idx[z0 + i] = (int32_t)(uint32_t)s[i];
+        __syncthreads();
+    }
+}
+
+__global__ void zbig_list_kernel(const uint32_t *big_flag, const int64_t *big_rank, int32_t G, int32_t *big_list) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < G && big_flag[g]) big_list[big_rank[g]] = g;
+}
+
+// entries of the large groups, group-major: key = rank << 32 | f, value = idx
+__global__ void zbig_gather_kernel(const uint64_t *zkey, const int64_t *z_off, const int32_t *big_list,
+                                   const int64_t *sub_off, uint64_t *skey, uint32_t *sval) {
+    const int r = blockIdx.x, g = big_list[r];
+    const int64_t z0 = z_off[g], n = z_off[g + 1] - z0, o = sub_off[g];
+    for (int64_t t = threadIdx.x; t < n; t += blockDim.x) {
+        const uint64_t k = zkey[z0 + t];
+        skey[o + t] = (uint64_t)r << 32 | (k >> 32);
+        sval[o + t] = (uint32_t)k;
+    }
+}
+
+__global__ void zbig_scatter_kernel(const uint32_t *sval, const int64_t *z_off, const int32_t *big_list,
+                                    const int64_t *sub_off, int32_t *z_idx) {
+    const int g = big_list[blockIdx.x];
+    const int64_t z0 = z_off[g], n = z_off[g + 1] - z0, o = sub_off[g];
+    for (int64_t t = threadIdx.x; t < n; t += blockDim.x) z_idx[z0 + t] = (int32_t)sval[o + t];
+}
+
 // chain list entries: (key = first anchor index) -> sorted
 __global__ void chain_list_kernel(const int64_t *g_start, const int32_t *n_chains, const int64_t *c_pos, int32_t G,
                                   const uint64_t *chain_u, const int64_t *chain_first, const int64_t *chain_ids,
@@ -705,33 +815,58 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         int64_t nz = 0;
         rc = scan_flags(ctx, zflag.as<uint32_t>(), n, zpos, &nz);
         if (rc) return rc;
-        DevBuf zf, zi, zg, zf2, zi2, zg2, zz;
-        const size_t zb = 4 * (size_t)(nz + 1);
-        HY_HIP(zf.alloc(zb, ctx->stream));
-        HY_HIP(zi.alloc(zb, ctx->stream));
-        HY_HIP(zg.alloc(zb, ctx->stream));
-        HY_HIP(zf2.alloc(zb, ctx->stream));
-        HY_HIP(zi2.alloc(zb, ctx->stream));
-        HY_HIP(zg2.alloc(zb, ctx->stream));
-        LAUNCH1(zfill_kernel, n, f.as<int32_t>(), zflag.as<uint32_t>(), zpos.as<int64_t>(), gid.as<int32_t>(), n,
-                zf.as<uint32_t>(), zi.as<uint32_t>(), zg.as<uint32_t>());
-        uint32_t *kf = zf.as<uint32_t>(), *kfa = zf2.as<uint32_t>(), *vi = zi.as<uint32_t>(), *via = zi2.as<uint32_t>();
-        rc = sort_pairs(ctx, kf, kfa, vi, via, nz, 0, 32, "radix_sort_z_f");
-        if (rc) return rc;
-        DevBuf zgg;
-        HY_HIP(zgg.alloc(zb, ctx->stream));
-        LAUNCH1(gather_kernel<uint32_t>, nz, gid.as<uint32_t>(), vi, zgg.as<uint32_t>(), nz);
-        uint32_t *kg = zgg.as<uint32_t>(), *kga = zg2.as<uint32_t>();
-        rc = sort_pairs(ctx, kg, kga, vi, via, nz, 0, bits_for(G), "radix_sort_z_group");
-        if (rc) return rc;
-        DevBuf z_off;
+        DevBuf z_off, zkey, zidx;
         HY_HIP(z_off.alloc(8 * (size_t)(G + 1), ctx->stream));
-        if (nz > 0) {
-            hipLaunchKernelGGL(zoff_kernel, dim3((unsigned)cdiv(nz + 1, 256)), dim3(256), 0, ctx->stream, kg, nz, (int32_t)G,
-                               z_off.as<int64_t>());
-            HY_CHECK_LAUNCH("zoff_kernel");
-        } else {
-            HY_HIP(hipMemsetAsync(z_off.p, 0, 8 * (size_t)(G + 1), ctx->stream));
+        HY_HIP(zkey.alloc(8 * (size_t)(nz + 1), ctx->stream));
+        HY_HIP(zidx.alloc(4 * (size_t)(nz + 1), ctx->stream));
+        const int32_t *vi = zidx.as<int32_t>();
+        {
+            ProfScope _ps(ctx, "mm_z_order", 8.0 * (double)n + 28.0 * (double)nz);  // f read, key write + read, idx write
+            LAUNCH1(zoff_direct_kernel, G + 1, g_start.as<int64_t>(), zpos.as<int64_t>(), (int32_t)G, nz,
+                    z_off.as<int64_t>());
+            LAUNCH1(zfill_key_kernel, n, f.as<int32_t>(), zflag.as<uint32_t>(), zpos.as<int64_t>(), n, zkey.as<uint64_t>());
+            DevBuf mid_list, zcnt, big_flag, big_size;
+            HY_HIP(mid_list.alloc(4 * (size_t)G, ctx->stream));
+            HY_HIP(zcnt.alloc(4, ctx->stream));
+            HY_HIP(big_flag.alloc(4 * (size_t)(G + 1), ctx->stream));
+            HY_HIP(big_size.alloc(4 * (size_t)(G + 1), ctx->stream));
+            HY_HIP(hipMemsetAsync(zcnt.p, 0, 4, ctx->stream));
+            LAUNCH1(zclass_kernel, G, z_off.as<int64_t>(), (int32_t)G, mid_list.as<int32_t>(), zcnt.as<int32_t>(),
+                    big_flag.as<uint32_t>(), big_size.as<uint32_t>());
+            hipLaunchKernelGGL(zsort_wave_kernel, dim3((unsigned)cdiv(G, 4)), dim3(256), 0, ctx->stream,
+                               zkey.as<uint64_t>(), z_off.as<int64_t>(), (int32_t)G, zidx.as<int32_t>());
+            HY_CHECK_LAUNCH("zsort_wave_kernel");
+            const int64_t nb = std::min<int64_t>(G, (int64_t)ctx->n_cu * 8);
+            hipLaunchKernelGGL(zsort_block_kernel, dim3((unsigned)nb), dim3(256), 0, ctx->stream, zkey.as<uint64_t>(),
+                               z_off.as<int64_t>(), mid_list.as<int32_t>(), zcnt.as<int32_t>(), zidx.as<int32_t>());
+            HY_CHECK_LAUNCH("zsort_block_kernel");
+            DevBuf big_rank, sub_off;
+            int64_t n_big = 0, nz_big = 0;
+            rc = scan_flags(ctx, big_flag.as<uint32_t>(), G, big_rank, &n_big);
+            if (rc) return rc;
+            rc = scan_flags(ctx, big_size.as<uint32_t>(), G, sub_off, &nz_big);
+            if (rc) return rc;
+            if (n_big > 0) {
+                DevBuf big_list, sk, sk2, sv, sv2;
+                HY_HIP(big_list.alloc(4 * (size_t)n_big, ctx->stream));
+                HY_HIP(sk.alloc(8 * (size_t)nz_big, ctx->stream));
+                HY_HIP(sk2.alloc(8 * (size_t)nz_big, ctx->stream));
+                HY_HIP(sv.alloc(4 * (size_t)nz_big, ctx->stream));
+                HY_HIP(sv2.alloc(4 * (size_t)nz_big, ctx->stream));
+                LAUNCH1(zbig_list_kernel, G, big_flag.as<uint32_t>(), big_rank.as<int64_t>(), (int32_t)G,
+                        big_list.as<int32_t>());
+                hipLaunchKernelGGL(zbig_gather_kernel, dim3((unsigned)n_big), dim3(256), 0, ctx->stream, zkey.as<uint64_t>(),
+                                   z_off.as<int64_t>(), big_list.as<int32_t>(), sub_off.as<int64_t>(), sk.as<uint64_t>(),
+                                   sv.as<uint32_t>());
+                HY_CHECK_LAUNCH("zbig_gather_kernel");
+                uint64_t *kp = sk.as<uint64_t>(), *ka = sk2.as<uint64_t>();
+                uint32_t *vp2 = sv.as<uint32_t>(), *va2 = sv2.as<uint32_t>();
+                rc = sort_pairs(ctx, kp, ka, vp2, va2, nz_big, 0, 32 + bits_for(n_big), "radix_sort_z_big");
+                if (rc) return rc;
+                hipLaunchKernelGGL(zbig_scatter_kernel, dim3((unsigned)n_big), dim3(256), 0, ctx->stream, vp2,
+                                   z_off.as<int64_t>(), big_list.as<int32_t>(), sub_off.as<int64_t>(), zidx.as<int32_t>());
+                HY_CHECK_LAUNCH("zbig_scatter_kernel");
+            }
         }
         DevBuf chain_ids, chain_u, chain_first, n_chains;
         HY_HIP(chain_ids.alloc(8 * (size_t)n, ctx->stream));
