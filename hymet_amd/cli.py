@@ -10,6 +10,10 @@
         == scripts/classification_cami.py:345-354
     python -m hymet_amd.cli classify-legacy (same flags)
         == scripts/classification.py:184-200
+    python -m hymet_amd.cli build-id-map detailed_taxonomy.tsv out_map.tsv
+        == tools/build_id_map.py (classification fallback, run_hymet_cami.sh:191)
+    python -m hymet_amd.cli mini-classify input.paf id_to_taxid.tsv out.tsv
+        == tools/mini_classify.py (classification fallback, run_hymet_cami.sh:192)
 
 The thin wrappers under scripts/ call these, so run_hymet_cami.sh / main.pl can use them
 in place of the reference stage scripts unchanged.  All device work goes through
@@ -229,6 +233,12 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         return cmd_classify(rest)
     if cmd == "classify-legacy":
         return cmd_classify(rest, legacy=True)
+    if cmd == "build-id-map":
+        from .fallback import main_build_id_map
+        return main_build_id_map(rest)
+    if cmd == "mini-classify":
+        from .fallback import main_mini_classify
+        return main_mini_classify(rest)
     print(f"unknown subcommand {cmd!r}", file=sys.stderr)
     return 2
 

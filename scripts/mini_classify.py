@@ -1,0 +1,11 @@
+#!/usr/bin/env python3
+"""Drop-in for HYMET tools/mini_classify.py (same argv, output bytes and messages; the classification
+fallback of run_hymet_cami.sh:183-205)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hymet_amd.cli import main  # noqa: E402
+
+if __name__ == "__main__":
+    sys.exit(main(["mini-classify"] + sys.argv[1:]))

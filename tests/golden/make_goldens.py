@@ -10,6 +10,8 @@ What it writes (all small, all data -- inputs + expected outputs):
              case/truth/zymo_mc/truth_profile.cami.tsv (recipe: case/results_summary.md:132-156),
              synthetic edge-case PAFs, and the expected TSV bytes of
              scripts/classification_cami.py and scripts/classification.py for each combination.
+  fallback/  expected outputs of tools/build_id_map.py and tools/mini_classify.py (the
+             run_hymet_cami.sh:183-205 classification fallback) on the classify fixtures.
   limit/     synthetic screen tables + selected lists and the expected output of
              scripts/limit_candidates.py (offline flags only: never --dedupe without --no-download).
 """
@@ -210,6 +212,48 @@ def make_limit(ref: Path, gdir: Path):
     print(f"limit: {len(cases)} cases")
 
 
+def make_fallback(ref: Path, gdir: Path):
+    """C9: tools/build_id_map.py + tools/mini_classify.py run as scripts on the classify
+    fixtures' taxonomy TSVs and PAFs; expected: the id map bytes, the first-hit TSV bytes and
+    stdout of each."""
+    import subprocess
+    out = gdir / "fallback"
+    out.mkdir(parents=True, exist_ok=True)
+    cdir = gdir / "classify"
+    # a PAF whose targets mix versioned / versionless / unknown names and repeated queries
+    lines = [l for l in (cdir / "zymo.paf").read_text().splitlines() if l.strip()][:400]
+    mixed = []
+    for i, l in enumerate(lines):
+        p = l.split("\t")
+        if i % 7 == 0:
+            p[5] = p[5].split(".", 1)[0]          # versionless target
+        elif i % 11 == 0:
+            p[5] = "NZ_UNKNOWN%d.1" % i           # no TaxID: the next line of that query may hit
+        mixed.append("\t".join(p))
+    mixed.insert(3, "# comment line")
+    mixed.insert(5, "short\tline")
+    (out / "mixed.paf").write_text("\n".join(mixed) + "\n")
+    cases = []
+    for tax in ["zymo_taxonomy.tsv", "regex_taxonomy.tsv"]:
+        with tempfile.TemporaryDirectory() as td:
+            m = Path(td) / "map.tsv"
+            r = subprocess.run([sys.executable, str(ref / "tools/build_id_map.py"), str(cdir / tax), str(m)],
+                               capture_output=True, text=True, check=True)
+            mkey = f"idmap__{tax[:-4]}.tsv"
+            (out / mkey).write_bytes(m.read_bytes())
+            for paf, pdir in [("zymo.paf", cdir), ("mixed.paf", out), ("empty.paf", cdir)]:
+                o = Path(td) / "fb.tsv"
+                r2 = subprocess.run([sys.executable, str(ref / "tools/mini_classify.py"), str(pdir / paf), str(m), str(o)],
+                                    capture_output=True, text=True, check=True)
+                key = f"mini__{paf[:-4]}__{tax[:-4]}.tsv"
+                (out / key).write_bytes(o.read_bytes())
+                cases.append({"taxonomy": tax, "paf": paf, "paf_dir": "classify" if pdir == cdir else "fallback",
+                              "idmap": mkey, "idmap_stdout": r.stdout.replace(str(m), "MAP"),
+                              "expect": key, "stdout": r2.stdout.replace(str(o), "OUT")})
+    (out / "cases.json").write_text(json.dumps(cases, indent=1))
+    print(f"fallback: {len(cases)} cases")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -217,6 +261,7 @@ def main():
     ref = Path(a.ref)
     make_classify(ref, HERE)
     make_limit(ref, HERE)
+    make_fallback(ref, HERE)
     big = HERE / "classify" / "big_zymo_x100.paf"
     if big.exists():
         big.unlink()  # regenerated by tests from zymo.paf (deterministic), keeps the repo small
