@@ -37,17 +37,37 @@ def log(*a):
         print(f"[bench {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
 
 
+# profiling scope (hymet_amd/csrc ProfScope tag) -> kernel symbol in rocprofv3 output
+SCOPE_KERNEL = {"mm_chain": "chain_groups_kernel<0>", "mm_chain_long": "chain_groups_kernel<1>",
+                "screen_count": "screen_count_kernel<21>", "mm_anchors": "write_anchor_keys_kernel",
+                "mm_backtrack": "backtrack_groups_kernel"}
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # tools/pmc_summary.py output
+
+
+def pmc_traffic(scope):
+    """HBM bytes per launch of the scope's kernel from the committed PMC passes (FETCH_SIZE /
+    WRITE_SIZE, gfx950-corrected: tools/pmc_summary.py), or None."""
+    try:
+        with open(PMC_FILE) as fh:
+            tab = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    r = tab.get(SCOPE_KERNEL.get(scope, ""), {})
+    return r.get("traffic_bytes")
+
+
 def roofline_from_prof(prof, prefer=None):
-    """Dominant kernel = the largest summed device time (every hot kernel has a byte model)."""
-    cand = dict(prof)
+    """Dominant kernel = the largest summed device time (every hot kernel has a byte model).
+    The sub-scope `mm_backtrack.long` is part of `mm_backtrack` and never a candidate."""
+    cand = {k: v for k, v in prof.items() if "." not in k}
     if not cand:
         return None
     name = prefer if prefer in cand else max(cand, key=lambda k: cand[k][0])
     ms, n, b = cand[name]
     achieved = b / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None, "kernel": name, "kernel_avg_ms": ms / max(n, 1), "launches": n,
-            "alg_bytes_per_launch": b / max(n, 1)}
+            "traffic": pmc_traffic(name), "kernel": name, "kernel_symbol": SCOPE_KERNEL.get(name),
+            "kernel_avg_ms": ms / max(n, 1), "launches": n, "alg_bytes_per_launch": b / max(n, 1)}
 
 
 # ------------------------------------------------------------------ CAMI-medium

@@ -304,6 +304,9 @@ __device__ __forceinline__ double st_pr(const int4 &v) { return __hiloint2double
 #else
 #define HYMET_CHAIN_ATTR
 #endif
+// kLongPass only names the instantiation (the long-join re-chain, bw_long) so that profiles
+// separate the two passes; the code is the same.
+template <int kLongPass>
 __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(ChainParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
@@ -1359,13 +1362,15 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
     // one wave per block, as many resident per CU as registers and LDS allow
     int64_t blocks = n_work;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_groups_kernel, 64, kChainLds) != hipSuccess ||
+    const bool long_pass = max_dist > 10000;
+    auto kern = long_pass ? chain_groups_kernel<1> : chain_groups_kernel<0>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, kChainLds) != hipSuccess ||
         per_cu <= 0)
         per_cu = 8;
     const int64_t cap = (int64_t)ctx->n_cu * per_cu;
     if (blocks > cap) blocks = cap;
     ProfScope _ps(ctx, max_dist > 10000 ? "mm_chain_long" : "mm_chain", 28.0 * (double)n_anchors);  // x,y read + f,p write per anchor
-    hipLaunchKernelGGL(chain_groups_kernel, dim3((unsigned)blocks), dim3(64), kChainLds, ctx->stream, P);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64), kChainLds, ctx->stream, P);
     HY_CHECK_LAUNCH("chain_groups_kernel");
     return HYMET_OK;
 }

@@ -90,7 +90,7 @@ int main(int argc, char **argv) {
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
         CK(hipEventRecord(e0, 0));
-        hipLaunchKernelGGL(chain_groups_kernel, dim3(nblk), dim3(64), kChainLds, 0, P);
+        hipLaunchKernelGGL(chain_groups_kernel<0>, dim3(nblk), dim3(64), kChainLds, 0, P);
         CK(hipGetLastError());
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
