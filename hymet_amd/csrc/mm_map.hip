@@ -452,9 +452,14 @@ __global__ void zoff_kernel(const uint32_t *zg_sorted, int64_t nz, int32_t G, in
 // ---- backtrack order: z = anchors with f >= min_sc, per group ascending (f, idx) (the
 // backtrack walks it from the end: canonical T3).  A group's z entries are a contiguous,
 // idx-ordered run of the flag scan, so the order is a segmented sort of 64-bit (f << 32 |
-// idx) keys: a wave per group of <= 64 entries (bitonic across lanes), a block per group of
-// <= kZs entries (bitonic in LDS), and one global radix sort over the few larger groups.
+// idx) keys.  Those segments are nearly sorted already: f grows along a colinear chain, so
+// a group is a few ascending runs (one per chain or chain piece).  Runs are found by a flat
+// descent scan; a group of <= kZRuns runs is merged in place of a sort -- every entry's
+// position is its offset in its own run plus, per other run, a binary search (keys are
+// unique).  Groups with more runs fall back to a block bitonic sort in LDS (<= kZs entries)
+// or one global radix sort over all such larger groups.
 constexpr int kZs = 2048;
+constexpr int kZRuns = 16;
 
 __global__ void zoff_direct_kernel(const int64_t *g_start, const int64_t *zpos, int32_t G, int64_t nz, int64_t *z_off) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -462,19 +467,86 @@ __global__ void zoff_direct_kernel(const int64_t *g_start, const int64_t *zpos, 
     else if (g == G) z_off[G] = nz;
 }
 
-__global__ void zfill_key_kernel(const int32_t *f, const uint32_t *flag, const int64_t *pos, int64_t n, uint64_t *zkey) {
+__global__ void zfill_key_kernel(const int32_t *f, const uint32_t *flag, const int64_t *pos, const int32_t *gid, int64_t n,
+                                 uint64_t *zkey, uint32_t *zg) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && flag[i]) zkey[pos[i]] = (uint64_t)(uint32_t)f[i] << 32 | (uint32_t)i;
+    if (i < n && flag[i]) {
+        const int64_t o = pos[i];
+        zkey[o] = (uint64_t)(uint32_t)f[i] << 32 | (uint32_t)i;
+        zg[o] = (uint32_t)gid[i];
+    }
 }
 
-__global__ void zclass_kernel(const int64_t *z_off, int32_t G, int32_t *mid_list, int32_t *mid_cnt, uint32_t *big_flag,
-                              uint32_t *big_size) {
+// a descent starts a new ascending run inside a group
+__global__ void zdesc_kernel(const uint64_t *zkey, const uint32_t *zg, int64_t nz, uint32_t *desc) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < nz) desc[p] = (p > 0 && zg[p - 1] == zg[p] && zkey[p] < zkey[p - 1]) ? 1u : 0u;
+}
+
+__global__ void zruns_kernel(const uint32_t *desc, const int64_t *dpos, const uint32_t *zg, const int64_t *z_off, int64_t nz,
+                             int64_t *run_start) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= nz || !desc[p]) return;
+    const uint32_t g = zg[p];
+    const int64_t r = dpos[p] - dpos[z_off[g]] + 1;
+    if (r < kZRuns) run_start[(int64_t)g * kZRuns + r] = p;
+}
+
+__device__ __forceinline__ int64_t z_runs(const int64_t *dpos, int64_t z0, int64_t z1) { return dpos[z1] - dpos[z0] + 1; }
+
+// groups with more than kZRuns runs: a block sort (<= kZs entries) or the big radix path
+__global__ void zclass_kernel(const int64_t *z_off, const int64_t *dpos, int32_t G, int max_runs, int32_t *mid_list,
+                              int32_t *mid_cnt, uint32_t *big_flag, uint32_t *big_size) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
-    const int64_t n = z_off[g + 1] - z_off[g];
-    big_flag[g] = n > kZs ? 1u : 0u;
-    big_size[g] = n > kZs ? (uint32_t)n : 0u;
-    if (n > 64 && n <= kZs) mid_list[atomicAdd(mid_cnt, 1)] = g;
+    const int64_t z0 = z_off[g], n = z_off[g + 1] - z0;
+    const bool many = n > 1 && z_runs(dpos, z0, z0 + n) > max_runs;
+    big_flag[g] = many && n > kZs ? 1u : 0u;
+    big_size[g] = many && n > kZs ? (uint32_t)n : 0u;
+    // one atomic per wave
+    const bool mid = many && n <= kZs;
+    const uint64_t m = __ballot(mid);
+    if (m) {
+        const int lane = threadIdx.x & 63, first = __ffsll((unsigned long long)m) - 1;
+        int base = 0;
+        if (lane == first) base = atomicAdd(mid_cnt, __popcll(m));
+        base = __shfl(base, first, 64);
+        if (mid) mid_list[base + __popcll(m & ((1ull << lane) - 1))] = g;
+    }
+}
+
+// groups of <= kZRuns ascending runs: merge by ranks
+__global__ void zmerge_kernel(const uint64_t *zkey, const uint32_t *zg, const int64_t *z_off, const int64_t *dpos,
+                              const uint32_t *desc, const int64_t *run_start, int64_t nz, int max_runs, int32_t *z_idx) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= nz) return;
+    const uint32_t g = zg[p];
+    const int64_t z0 = z_off[g], z1 = z_off[g + 1];
+    const int64_t K = z_runs(dpos, z0, z1);
+    const uint64_t key = zkey[p];
+    if (K == 1) {
+        z_idx[p] = (int32_t)(uint32_t)key;
+        return;
+    }
+    if (K > max_runs) return;
+    const int r = (int)(dpos[p] + desc[p] - dpos[z0]);
+    const int64_t *rs = run_start + (int64_t)g * kZRuns;
+    int64_t pos = 0;
+    for (int k = 0; k < K; k++) {
+        const int64_t s0 = k == 0 ? z0 : rs[k], s1 = k + 1 < K ? rs[k + 1] : z1;
+        if (k == r) {
+            pos += p - s0;
+            continue;
+        }
+        int64_t lo = s0, hi = s1;  // first entry >= key
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (zkey[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        pos += lo - s0;
+    }
+    z_idx[z0 + pos] = (int32_t)(uint32_t)key;
 }
 
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
@@ -483,27 +555,7 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     return (uint64_t)hi << 32 | lo;
 }
 
-// one wave per group with <= 64 z entries (4 groups per 256-thread block)
-__global__ __launch_bounds__(256) void zsort_wave_kernel(const uint64_t *zkey, const int64_t *z_off, int32_t G,
-                                                         int32_t *z_idx) {
-    const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (g >= G) return;
-    const int64_t z0 = z_off[g], n = z_off[g + 1] - z0;
-    if (n > 64 || n == 0) return;
-    uint64_t v = lane < n ? zkey[z0 + lane] : ~0ull;
-    if (n > 1) {
-        for (int k = 2; k <= 64; k <<= 1)
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                const uint64_t o = shfl_xor64(v, j);
-                const bool up = (lane & k) == 0, low = (lane & j) == 0;
-                v = (low == up) ? (o < v ? o : v) : (o > v ? o : v);
-            }
-    }
-    if (lane < n) z_idx[z0 + lane] = (int32_t)(uint32_t)v;
-}
-
-// one block per group with 64 < n <= kZs z entries (grid-stride over the list)
+// one block per listed group of <= kZs z entries (grid-stride over the list)
 __global__ __launch_bounds__(256) void zsort_block_kernel(const uint64_t *zkey, const int64_t *z_off, const int32_t *list,
                                                           const int32_t *cnt, int32_t *z_idx) {
     __shared__ uint64_t s[kZs];
@@ -821,21 +873,35 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(zidx.alloc(4 * (size_t)(nz + 1), ctx->stream));
         const int32_t *vi = zidx.as<int32_t>();
         {
-            ProfScope _ps(ctx, "mm_z_order", 8.0 * (double)n + 28.0 * (double)nz);  // f read, key write + read, idx write
+            ProfScope _ps(ctx, "mm_z_order", 8.0 * (double)n + 48.0 * (double)nz);  // f, gid read; key/group write, read twice; idx write
             LAUNCH1(zoff_direct_kernel, G + 1, g_start.as<int64_t>(), zpos.as<int64_t>(), (int32_t)G, nz,
                     z_off.as<int64_t>());
-            LAUNCH1(zfill_key_kernel, n, f.as<int32_t>(), zflag.as<uint32_t>(), zpos.as<int64_t>(), n, zkey.as<uint64_t>());
+            DevBuf zg, desc, dpos, run_start;
+            HY_HIP(zg.alloc(4 * (size_t)(nz + 1), ctx->stream));
+            LAUNCH1(zfill_key_kernel, n, f.as<int32_t>(), zflag.as<uint32_t>(), zpos.as<int64_t>(), gid.as<int32_t>(), n,
+                    zkey.as<uint64_t>(), zg.as<uint32_t>());
+            HY_HIP(desc.alloc(4 * (size_t)(nz + 1), ctx->stream));
+            LAUNCH1(zdesc_kernel, nz, zkey.as<uint64_t>(), zg.as<uint32_t>(), nz, desc.as<uint32_t>());
+            int64_t n_desc = 0;
+            rc = scan_flags(ctx, desc.as<uint32_t>(), nz, dpos, &n_desc);
+            if (rc) return rc;
+            HY_HIP(hipMemcpyAsync(dpos.as<int64_t>() + nz, &n_desc, 8, hipMemcpyHostToDevice, ctx->stream));
+            HY_HIP(run_start.alloc(8 * (size_t)G * kZRuns, ctx->stream));
+            LAUNCH1(zruns_kernel, nz, desc.as<uint32_t>(), dpos.as<int64_t>(), zg.as<uint32_t>(), z_off.as<int64_t>(), nz,
+                    run_start.as<int64_t>());
             DevBuf mid_list, zcnt, big_flag, big_size;
             HY_HIP(mid_list.alloc(4 * (size_t)G, ctx->stream));
             HY_HIP(zcnt.alloc(4, ctx->stream));
             HY_HIP(big_flag.alloc(4 * (size_t)(G + 1), ctx->stream));
             HY_HIP(big_size.alloc(4 * (size_t)(G + 1), ctx->stream));
             HY_HIP(hipMemsetAsync(zcnt.p, 0, 4, ctx->stream));
-            LAUNCH1(zclass_kernel, G, z_off.as<int64_t>(), (int32_t)G, mid_list.as<int32_t>(), zcnt.as<int32_t>(),
-                    big_flag.as<uint32_t>(), big_size.as<uint32_t>());
-            hipLaunchKernelGGL(zsort_wave_kernel, dim3((unsigned)cdiv(G, 4)), dim3(256), 0, ctx->stream,
-                               zkey.as<uint64_t>(), z_off.as<int64_t>(), (int32_t)G, zidx.as<int32_t>());
-            HY_CHECK_LAUNCH("zsort_wave_kernel");
+            // HYMET_Z_RUNS (tests): merge groups of at most that many runs, sort the others
+            const char *ev = getenv("HYMET_Z_RUNS");
+            const int max_runs = ev ? std::max(1, std::min(kZRuns, atoi(ev))) : kZRuns;
+            LAUNCH1(zclass_kernel, G, z_off.as<int64_t>(), dpos.as<int64_t>(), (int32_t)G, max_runs, mid_list.as<int32_t>(),
+                    zcnt.as<int32_t>(), big_flag.as<uint32_t>(), big_size.as<uint32_t>());
+            LAUNCH1(zmerge_kernel, nz, zkey.as<uint64_t>(), zg.as<uint32_t>(), z_off.as<int64_t>(), dpos.as<int64_t>(),
+                    desc.as<uint32_t>(), run_start.as<int64_t>(), nz, max_runs, zidx.as<int32_t>());
             const int64_t nb = std::min<int64_t>(G, (int64_t)ctx->n_cu * 8);
             hipLaunchKernelGGL(zsort_block_kernel, dim3((unsigned)nb), dim3(256), 0, ctx->stream, zkey.as<uint64_t>(),
                                z_off.as<int64_t>(), mid_list.as<int32_t>(), zcnt.as<int32_t>(), zidx.as<int32_t>());

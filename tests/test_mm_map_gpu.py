@@ -53,15 +53,19 @@ def _queries(rng, refs):
     return qs
 
 
-@pytest.mark.parametrize("bt_long,legacy", [(None, None), ("4", None), (None, "1")])
-def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy):
+@pytest.mark.parametrize("bt_long,legacy,z_runs", [(None, None, None), ("4", None, None), (None, "1", "1"),
+                                                  (None, None, "2")])
+def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy, z_runs):
     """bt_long = "4": nearly every chain group takes the wave-per-group backtrack path.
     legacy = "1": anchors take the two-key sort path (used when the one-key anchor sort key
-    would exceed 64 bits)."""
+    would exceed 64 bits).  z_runs: backtrack-order groups of more ascending runs than this
+    take the sort fallbacks (block bitonic / global radix) instead of the run merge."""
     if bt_long is not None:
         monkeypatch.setenv("HYMET_BT_LONG", bt_long)
     if legacy is not None:
         monkeypatch.setenv("HYMET_ANCHOR_LEGACY", legacy)
+    if z_runs is not None:
+        monkeypatch.setenv("HYMET_Z_RUNS", z_runs)
     from hymet_amd import mapper
     from hymet_amd.seqio import DevicePool, from_records
     from oracle import oracle_lib as ol
