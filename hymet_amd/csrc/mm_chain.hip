@@ -1120,6 +1120,14 @@ constexpr int kBtWin = 8;
 // reads each step's node from it with readlane.  A fence after each walk and L2 loads of t
 // make the walk's marks visible to the next probes.
 constexpr int64_t kBtLong = 1024;
+// The wave kernel's z probes and walk window cover kBtChunks * 64 entries per memory round
+// trip.  Measured on C4: 4 chunks are slower than 1 (mm_backtrack.long 549 -> 814 ms per
+// step) -- most walks are short (an off-path anchor walks into a marked chain after a step
+// or two), so the kernel is throughput-bound, not bound by its longest walk.
+#ifndef HYMET_BT_CHUNKS
+#define HYMET_BT_CHUNKS 1
+#endif
+constexpr int kBtChunks = HYMET_BT_CHUNKS;
 
 __device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int64_t uni64(int64_t v) {
@@ -1131,10 +1139,18 @@ __device__ __forceinline__ int64_t rlane64(int64_t v, int l) {
     return (int64_t)((uint64_t)hi << 32 | lo);
 }
 
-__global__ void bt_long_list_kernel(const int64_t *g_start, int32_t n_groups, int64_t long_min, int32_t *list,
-                                    int32_t *cnt) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < n_groups && g_start[g + 1] - g_start[g] > long_min) list[atomicAdd(cnt, 1)] = g;
+// order: the chaining work list (groups of >= min_cnt anchors by descending size); the
+// wave kernel takes its prefix of groups larger than long_min, biggest first
+__global__ void bt_long_count_kernel(const int64_t *g_start, const int32_t *order, int32_t n_work, int64_t long_min,
+                                     int32_t *cnt) {
+    int lo = 0, hi = n_work;  // first w with size(order[w]) <= long_min
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const int g = order[mid];
+        if (g_start[g + 1] - g_start[g] > long_min) lo = mid + 1;
+        else hi = mid;
+    }
+    cnt[0] = lo;
 }
 
 __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, const int32_t *list, const int32_t *cnt,
@@ -1162,17 +1178,36 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
         uint64_t c_probe = 0, c_walk = 0, c_step = 0, c_reload = 0, t_walk = 0, t_post = 0;
         const uint64_t t_g0 = P.prof ? clock64() : 0;
         while (k >= z0) {
+            // probe kBtChunks * 64 z entries per round trip: all index loads, then all t loads
             c_probe++;
-            const int64_t kk = k - lane;
-            const int32_t zc = kk >= z0 ? P.z_idx[kk] : 0;
-            const int32_t tv = kk >= z0 ? ld_l2(P.t + zc) : 1;
-            const uint64_t m = __ballot(tv == 0);
-            if (m == 0) {
-                k -= 64;
+            int32_t zc[kBtChunks], tv[kBtChunks];
+#pragma unroll
+            for (int c = 0; c < kBtChunks; c++) {
+                const int64_t kk = k - 64 * c - lane;
+                zc[c] = kk >= z0 ? P.z_idx[kk] : 0;
+            }
+#pragma unroll
+            for (int c = 0; c < kBtChunks; c++) {
+                const int64_t kk = k - 64 * c - lane;
+                tv[c] = kk >= z0 ? ld_l2(P.t + zc[c]) : 1;
+            }
+            int hit = -1;
+            int32_t zsel = 0;
+#pragma unroll
+            for (int c = kBtChunks - 1; c >= 0; c--) {  // the nearest chunk with an unmarked entry wins
+                const uint64_t m = __ballot(tv[c] == 0);
+                if (m) {
+                    const int h = __ffsll((unsigned long long)m) - 1;
+                    hit = 64 * c + h;
+                    zsel = __builtin_amdgcn_readlane(zc[c], h);
+                }
+            }
+            hit = uni(hit);
+            if (hit < 0) {
+                k -= 64 * kBtChunks;
                 continue;
             }
-            const int hit = uni(__ffsll((unsigned long long)m) - 1);
-            const int64_t zi = (int64_t)__builtin_amdgcn_readlane(zc, hit);
+            const int64_t zi = (int64_t)uni(zsel);
             k -= hit + 1;
             const int32_t zf = uni(P.f[zi]);
             int64_t *buf = P.chain_ids + wpos;
@@ -1180,9 +1215,11 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             int64_t len = 1, nv = 0;  // recorded path nodes; chain = path[0, nv)
             int32_t max_s = 0;
             int64_t nxt = uni64(P.p[zi]);
-            int64_t whi = -1;  // window: lane l holds anchor whi - l
-            int64_t wp = -1;
-            int32_t wf = 0, wt = 1;
+            int64_t whi = -1;  // window: chunk c, lane l holds anchor whi - 64c - l
+            int64_t wpc[kBtChunks];
+            int32_t wfc[kBtChunks], wtc[kBtChunks];
+#pragma unroll
+            for (int c = 0; c < kBtChunks; c++) wpc[c] = -1, wfc[c] = 0, wtc[c] = 1;
             c_walk++;
             const uint64_t t_w0 = P.prof ? clock64() : 0;
             // Each round evaluates a RUN of candidates at once: lanes o..R of the window, where
@@ -1197,17 +1234,26 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                     if (zf > max_s) max_s = zf, nv = len;
                     break;
                 }
-                if (nxt > whi || nxt <= whi - 64) {
+                if (nxt > whi || nxt <= whi - 64 * kBtChunks) {
                     c_reload++;
                     whi = nxt;
-                    const int64_t jj = nxt - lane;
-                    const bool ok = jj >= g0;
-                    wp = ok ? P.p[jj] : -1;
-                    wf = ok ? P.f[jj] : 0;
-                    wt = ok ? ld_l2(P.t + jj) : 1;
+#pragma unroll
+                    for (int c = 0; c < kBtChunks; c++) {
+                        const int64_t jj = nxt - 64 * c - lane;
+                        const bool ok = jj >= g0;
+                        wpc[c] = ok ? P.p[jj] : -1;
+                        wfc[c] = ok ? P.f[jj] : 0;
+                        wtc[c] = ok ? ld_l2(P.t + jj) : 1;
+                    }
                 }
-                const int o = (int)(whi - nxt);
-                const int64_t j = whi - lane;
+                const int d = (int)(whi - nxt);
+                const int cc = d >> 6, o = d & 63;  // chunk of nxt, and its lane there
+                int64_t wp = wpc[0];
+                int32_t wf = wfc[0], wt = wtc[0];
+#pragma unroll
+                for (int c = 1; c < kBtChunks; c++)
+                    if (cc == c) wp = wpc[c], wf = wfc[c], wt = wtc[c];
+                const int64_t j = whi - 64 * cc - lane;
                 const bool in = lane >= o;
                 const uint64_t ms = __ballot(in && (lane == 63 || wp != j - 1 || j - 1 < g0));
                 const int R = uni(__ffsll((unsigned long long)ms) - 1);
@@ -1376,8 +1422,9 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
 }
 
 int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, const int64_t *p, int32_t *t,
-                     const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, int min_cnt, int min_sc, int max_drop,
-                     int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first, int32_t *n_chains, int64_t n_anchors) {
+                     const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, const int32_t *order, int32_t n_work,
+                     int min_cnt, int min_sc, int max_drop, int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first,
+                     int32_t *n_chains, int64_t n_anchors) {
     if (n_groups <= 0) return HYMET_OK;
     HY_HIP(hipMemsetAsync(t, 0, 4 * (size_t)n_anchors, ctx->stream));
     const char *ev = getenv("HYMET_BT_LONG");
@@ -1390,21 +1437,27 @@ int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, c
     }
     BacktrackParams P{g_start,  f,         p,       t,           z_off,    z_idx, n_groups, min_cnt, min_sc, max_drop,
                       long_min, (unsigned long long *)pbuf.p, chain_ids, chain_u, chain_first, n_chains};
-    DevBuf list, cnt;
-    HY_HIP(list.alloc(4 * (size_t)n_groups, ctx->stream));
+    DevBuf cnt;
     HY_HIP(cnt.alloc(8, ctx->stream));
     HY_HIP(hipMemsetAsync(cnt.p, 0, 8, ctx->stream));
     // z index + t probe + walked (p, f) + t mark + chain id write, per anchor
     ProfScope _ps(ctx, "mm_backtrack", 32.0 * (double)n_anchors);
-    hipLaunchKernelGGL(bt_long_list_kernel, dim3((unsigned)cdiv(n_groups, 256)), dim3(256), 0, ctx->stream, g_start,
-                       n_groups, long_min, list.as<int32_t>(), cnt.as<int32_t>());
-    HY_CHECK_LAUNCH("bt_long_list_kernel");
+    if (n_work > 0) {
+        hipLaunchKernelGGL(bt_long_count_kernel, dim3(1), dim3(1), 0, ctx->stream, g_start, order, n_work, long_min,
+                           cnt.as<int32_t>());
+        HY_CHECK_LAUNCH("bt_long_count_kernel");
+    }
+    // (running the two kernels concurrently on two streams measured no faster: both are
+    // throughput-bound)
     hipLaunchKernelGGL(backtrack_groups_kernel, dim3((unsigned)cdiv(n_groups, 64)), dim3(64), 0, ctx->stream, P);
     HY_CHECK_LAUNCH("backtrack_groups_kernel");
-    {
+    if (n_work > 0) {
         ProfScope _pl(ctx, "mm_backtrack.long");  // the wave-per-group part of mm_backtrack
-        hipLaunchKernelGGL(backtrack_long_kernel, dim3((unsigned)ctx->n_cu * 8), dim3(64), 0, ctx->stream, P,
-                           list.as<int32_t>(), cnt.as<int32_t>(), cnt.as<int32_t>() + 1);
+        const char *ew = getenv("HYMET_BT_WAVES");  // resident waves per CU for the wave kernel
+        const int per_cu = ew ? std::max(1, atoi(ew)) : 16;
+        const int64_t nb = std::min<int64_t>(n_work, (int64_t)ctx->n_cu * per_cu);
+        hipLaunchKernelGGL(backtrack_long_kernel, dim3((unsigned)nb), dim3(64), 0, ctx->stream, P, order,
+                           cnt.as<int32_t>(), cnt.as<int32_t>() + 1);
         HY_CHECK_LAUNCH("backtrack_long_kernel");
     }
     if (prof) {

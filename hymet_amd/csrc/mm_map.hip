@@ -37,8 +37,9 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
                  int max_dist_inner, int bw, int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip,
                  int64_t n_anchors, int64_t n_groups);
 int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, const int64_t *p, int32_t *t,
-                     const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, int min_cnt, int min_sc, int max_drop,
-                     int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first, int32_t *n_chains, int64_t n_anchors);
+                     const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, const int32_t *order, int32_t n_work,
+                     int min_cnt, int min_sc, int max_drop, int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first,
+                     int32_t *n_chains, int64_t n_anchors);
 
 namespace {
 
@@ -955,7 +956,8 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         }
         const auto bt0 = std::chrono::steady_clock::now();
         rc = launch_backtrack(ctx, g_start.as<int64_t>(), f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(),
-                              z_off.as<int64_t>(), (const int32_t *)vi, (int32_t)G, opt->min_cnt, opt->min_chain_score, bw,
+                              z_off.as<int64_t>(), (const int32_t *)vi, (int32_t)G, (const int32_t *)vp, (int32_t)n_work,
+                              opt->min_cnt, opt->min_chain_score, bw,
                               chain_ids.as<int64_t>(), chain_u.as<uint64_t>(), chain_first.as<int64_t>(),
                               n_chains.as<int32_t>(), n);
         if (rc) return rc;
