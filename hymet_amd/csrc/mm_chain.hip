@@ -1119,7 +1119,9 @@ constexpr int kBtWin = 8;
 // SGPRs via readfirstlane - refills a 64-node (p, f, t) window with one coalesced load and
 // reads each step's node from it with readlane.  A fence after each walk and L2 loads of t
 // make the walk's marks visible to the next probes.
-constexpr int64_t kBtLong = 1024;
+// (C4: threshold 1024 -> 128 took mm_backtrack 623 -> 301 ms per step once the wave kernel
+// stopped issuing agent-scope fences)
+constexpr int64_t kBtLong = 128;
 // The wave kernel's z probes and walk window cover kBtChunks * 64 entries per memory round
 // trip.  Measured on C4: 4 chunks are slower than 1 (mm_backtrack.long 549 -> 814 ms per
 // step) -- most walks are short (an off-path anchor walks into a marked chain after a step
@@ -1212,6 +1214,7 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             const int32_t zf = uni(P.f[zi]);
             int64_t *buf = P.chain_ids + wpos;
             buf[0] = zi;  // every lane: same value, same address
+            P.t[zi] = 1;  // path nodes are marked as recorded; those past the best end are unmarked after
             int64_t len = 1, nv = 0;  // recorded path nodes; chain = path[0, nv)
             int32_t max_s = 0;
             int64_t nxt = uni64(P.p[zi]);
@@ -1280,16 +1283,23 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                     nv = len + (u - o);
                     max_s = __builtin_amdgcn_readlane(incl, u);  // = s_u: it beat every earlier value
                 }
-                if (lane >= o && lane <= last) buf[len + (lane - o)] = j;
+                if (lane >= o && lane <= last) {
+                    buf[len + (lane - o)] = j;
+                    P.t[j] = 1;  // the walk never re-reads a node it has passed (p[i] < i)
+                }
                 len += last - o + 1;
                 if (done) break;
                 nxt = rlane64(wp, R);  // predecessor of the run's last node
             }
             const uint64_t t_w1 = P.prof ? clock64() : 0;
             t_walk += t_w1 - t_w0;
-            // the chain is path[0, nv): mark it (the walk itself never re-reads its own nodes)
-            __threadfence();
-            for (int64_t a = lane; a < nv; a += 64) P.t[ld_l2(buf + a)] = 1;
+            // the chain is path[0, nv): unmark the few nodes past the best end.  The marks are
+            // only read back by this wave (its probes and later walks, through L2), so the
+            // ordering needed is workgroup scope -- its stores completed at L2 -- not an
+            // agent-scope fence (an L2 writeback: ~8 us round trips once thousands of waves
+            // issued them).
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            for (int64_t a = nv + lane; a < len; a += 64) P.t[ld_l2(buf + a)] = 0;
             const int32_t sc = nv == 0 ? 0 : max_s;
             if (sc >= P.min_sc && nv > 0 && nv >= P.min_cnt) {
                 P.chain_u[g0 + nc] = (uint64_t)(uint32_t)sc << 32 | (uint32_t)nv;  // every lane: same value
@@ -1297,7 +1307,7 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                 nc++;
                 wpos += nv;
             }
-            __threadfence();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             if (P.prof) t_post += clock64() - t_w1;
         }
         P.n_chains[g] = nc;
