@@ -1043,9 +1043,20 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
                    const int64_t *qc, const int64_t *qb, const uint64_t *mini_pos, const int64_t *mp_off, const int64_t *qlen,
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
-                   int64_t NB, int64_t NC, int64_t NM, const int32_t *bchain, const uint32_t *cq);
+                   int64_t NB, int64_t NC, int64_t NM, const int32_t *bchain, const uint32_t *cq,
+                   const int32_t *pos_tab, const int64_t *qbase);
 
 namespace {
+// dense query position -> index among the query's seeded minimizers (mini_pos order), for
+// mm_est_err's get_mini_idx (anchor_mini_idx_kernel); positions without one stay -1
+__global__ void mini_table_kernel(const uint64_t *my, const uint32_t *seed_n, const uint32_t *qid, const int64_t *qm_off,
+                                  const int64_t *mp_pos, const int64_t *qbase, int64_t M, int32_t *pos_tab) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M || !seed_n[i]) return;
+    const uint32_t q = qid[i];
+    pos_tab[qbase[q] + ((uint32_t)my[i] >> 1)] = (int32_t)(mp_pos[i] - mp_pos[qm_off[q]]);
+}
+
 __global__ void rechain_flag_kernel(const uint64_t *by, const uint64_t *cu, const int64_t *qc, const int64_t *qb,
                                     const int64_t *qlen, int n_q, int rescue_size, float rescue_ratio, uint32_t *flag) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1079,18 +1090,17 @@ __global__ void rechain_gather_kernel(const uint64_t *bx, const uint64_t *by, co
     }
 }
 
-__global__ void rechain_keys_kernel(const uint64_t *bx, const uint64_t *by, const int64_t *qb, const uint32_t *qflag,
-                                    const int64_t *new_off, int n_q, int rb, int pb, uint64_t *key, uint32_t *val) {
-    const int q = blockIdx.x;
-    if (q >= n_q || !qflag[q]) return;
-    const int64_t b0 = qb[q], b1 = qb[q + 1], o = new_off[q];
-    const uint64_t kq = (uint64_t)q << (1 + rb + pb);
-    for (int64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
-        const int64_t a = o + (i - b0);
-        const uint64_t ax = bx[i];
-        key[a] = kq | (ax >> 63) << (rb + pb) | (ax << 1 >> 33) << pb | (uint32_t)ax;
-        val[a] = (uint32_t)by[i];
-    }
+// one thread per re-chain anchor (flat: a block per query left the long queries' blocks as
+// the tail); its query by binary search over the new offsets
+__global__ void rechain_keys_kernel(const uint64_t *bx, const uint64_t *by, const int64_t *qb, const int64_t *new_off,
+                                    int n_q, int64_t n, int rb, int pb, uint64_t *key, uint32_t *val) {
+    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= n) return;
+    const int q = upper_idx(new_off, n_q, a);  // last q with new_off[q] <= a (non-empty)
+    const int64_t i = qb[q] + (a - new_off[q]);
+    const uint64_t ax = bx[i];
+    key[a] = (uint64_t)q << (1 + rb + pb) | (ax >> 63) << (rb + pb) | (ax << 1 >> 33) << pb | (uint32_t)ax;
+    val[a] = (uint32_t)by[i];
 }
 
 __global__ void qlen_sizes_kernel(const int64_t *off, int n_q, const uint32_t *flag, uint32_t *sz) {
@@ -1230,6 +1240,18 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
     hipLaunchKernelGGL(sample_off_kernel, dim3((unsigned)cdiv(n_q + 1, 256)), dim3(256), 0, st, mp_pos.as<int64_t>(),
                        qm_off.as<int64_t>(), n_q, NM, mp_off.as<int64_t>());
     HY_CHECK_LAUNCH("sample_off_kernel");
+    // mm_est_err's minimizer lookup table (filled once seed_n is final, below)
+    DevBuf d_qbase, pos_tab;
+    std::vector<int64_t> qbase(n_q + 1, 0);  // lives until the call returns (async H2D source)
+    {
+        for (int q = 0; q < n_q; q++) qbase[q + 1] = qbase[q] + h_lens[q];
+        HY_HIP(d_qbase.alloc(8 * (size_t)(n_q + 1), st));
+        HY_HIP(hipMemcpyAsync(d_qbase.p, qbase.data(), 8 * (size_t)(n_q + 1), hipMemcpyHostToDevice, st));
+        HY_HIP(pos_tab.alloc(4 * (size_t)(qbase[n_q] + 1), st));
+        HY_HIP(hipMemsetAsync(pos_tab.p, 0xFF, 4 * (size_t)(qbase[n_q] + 1), st));
+        LAUNCH1(mini_table_kernel, M, my.as<uint64_t>(), seed_n.as<uint32_t>(), qid.as<uint32_t>(), qm_off.as<int64_t>(),
+                mp_pos.as<int64_t>(), d_qbase.as<int64_t>(), M, pos_tab.as<int32_t>());
+    }
     AnchorSet S1;
     HY_HIP(S1.d_off.alloc(8 * (size_t)(n_q + 1), st));
     hipLaunchKernelGGL(sample_off_kernel, dim3((unsigned)cdiv(n_q + 1, 256)), dim3(256), 0, st, a_pos.as<int64_t>(),
@@ -1308,10 +1330,8 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
                 DevBuf key, val;
                 HY_HIP(key.alloc(8 * (size_t)(A2 + 1), st));
                 HY_HIP(val.alloc(4 * (size_t)(A2 + 1), st));
-                hipLaunchKernelGGL(rechain_keys_kernel, dim3((unsigned)n_q), dim3(256), 0, st, C1.bx.as<uint64_t>(),
-                                   C1.by.as<uint64_t>(), C1.d_qb.as<int64_t>(), flag.as<uint32_t>(), S2.d_off.as<int64_t>(),
-                                   n_q, rb, pb, key.as<uint64_t>(), val.as<uint32_t>());
-                HY_CHECK_LAUNCH("rechain_keys_kernel");
+                LAUNCH1(rechain_keys_kernel, A2, C1.bx.as<uint64_t>(), C1.by.as<uint64_t>(), C1.d_qb.as<int64_t>(),
+                        S2.d_off.as<int64_t>(), n_q, A2, rb, pb, key.as<uint64_t>(), val.as<uint32_t>());
                 rc = sort_anchor_keys(ctx, key, val, A2, key1_bits + pb, rb, pb, k, S2);
                 if (rc) return rc;
             } else {
@@ -1349,7 +1369,8 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
                                 C.d_qc.as<int64_t>(), C.d_qb.as<int64_t>(), mini_pos.as<uint64_t>(), mp_off.as<int64_t>(),
                                 d_qlen.as<int64_t>(), d_hash.as<uint32_t>(), rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
                                 z.p, rg.as<hymet_mm_reg>(), wv.as<int32_t>(), cov.as<uint64_t>(), tmp.as<int32_t>(),
-                                nr.as<int32_t>(), C.n_anchor, NC, NM, C.bchain.as<int32_t>(), C.cq.as<uint32_t>());
+                                nr.as<int32_t>(), C.n_anchor, NC, NM, C.bchain.as<int32_t>(), C.cq.as<uint32_t>(),
+                                pos_tab.as<int32_t>(), d_qbase.as<int64_t>());
         if (r2) return r2;
         regs.resize(NC);
         nreg.resize(n_q);

@@ -3,7 +3,7 @@
 // mm_select_sub (+ mm_sync_regs), mm_est_err, mm_filter_strand_retained, mm_set_mapq.
 // Everything that walks a chain's anchors is anchor-parallel and runs first:
 //   anchor_mini_idx_kernel  one thread per chained anchor: its index among the query
-//                           minimizers (mm_est_err's get_mini_idx binary search);
+//                           minimizers (mm_est_err's get_mini_idx, by table lookup);
 //   chain_stats_kernel      one wave per chain: mlen/blen sums (mm_reg_set_coor) and the first
 //                           anchor, in est_err's walking order, whose minimizer index does not
 //                           increase -- est_err's sequential two-pointer walk matches exactly
@@ -122,19 +122,6 @@ __device__ __forceinline__ int64_t chain_of(const int64_t *cboff, int64_t c0, in
     return lo;
 }
 
-__device__ int get_mini_idx(int qlen, uint64_t ax, uint64_t ay, int32_t n, const uint64_t *mini_pos) {
-    int32_t x = (int32_t)ay, L = 0, R = n - 1;
-    if (ax >> 63) x = qlen - 1 - (int32_t)ay + (int32_t)(ay >> 32 & 0xff) - 1;
-    while (L <= R) {
-        const int32_t m = (int32_t)(((uint64_t)L + R) >> 1);
-        const int32_t y = (int32_t)mini_pos[m];
-        if (y < x) L = m + 1;
-        else if (y > x) R = m - 1;
-        else return m;
-    }
-    return -1;
-}
-
 struct AnchorStatParams {
     const uint64_t *bx, *by, *cu;
     const int64_t *cboff, *qb, *qlen, *mp_off;
@@ -144,16 +131,23 @@ struct AnchorStatParams {
     const int32_t *bchain;   // chain of each anchor (chain_copy_kernel)
     const uint32_t *cq;      // query of each chain
     int32_t *a_idx, *c_mlen, *c_blen, *c_st, *c_last;
+    const int32_t *pos_tab;  // query base -> minimizer index (or -1), at qbase[q] + position
+    const int64_t *qbase;
 };
 
-// per chained anchor: its index among the query minimizers (mm_est_err's get_mini_idx)
+// per chained anchor: its index among the query minimizers (mm_est_err's get_mini_idx).  The
+// binary search over the query's minimizer positions is replaced by one load from a dense
+// position -> index table (pos_tab, one int32 per query base, -1 where no seeded minimizer
+// starts; built by mini_table_kernel in hymet_mm_map): same result, one random read.
 __global__ void anchor_mini_idx_kernel(AnchorStatParams P) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= P.NB) return;
     const int64_t q = P.cq[P.bchain[b]];
-    const int64_t m0 = P.mp_off[q];
-    const int32_t nm = (int32_t)(P.mp_off[q + 1] - m0);
-    P.a_idx[b] = nm > 0 ? get_mini_idx((int)P.qlen[q], P.bx[b], P.by[b], nm, P.mini_pos + m0) : -1;
+    const int qlen = (int)P.qlen[q];
+    const uint64_t ax = P.bx[b], ay = P.by[b];
+    int32_t x = (int32_t)ay;
+    if (ax >> 63) x = qlen - 1 - (int32_t)ay + (int32_t)(ay >> 32 & 0xff) - 1;
+    P.a_idx[b] = (x >= 0 && x < qlen) ? P.pos_tab[P.qbase[q] + x] : -1;
 }
 
 __device__ __forceinline__ int wsum(int v) {
@@ -420,7 +414,8 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
                    const int64_t *qc, const int64_t *qb, const uint64_t *mini_pos, const int64_t *mp_off, const int64_t *qlen,
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
-                   int64_t NB, int64_t NC, int64_t NM, const int32_t *bchain, const uint32_t *cq) {
+                   int64_t NB, int64_t NC, int64_t NM, const int32_t *bchain, const uint32_t *cq,
+                   const int32_t *pos_tab, const int64_t *qbase) {
     if (n_q <= 0) return HYMET_OK;
     hipStream_t st = ctx->stream;
     DevBuf a_idx, cst, sumk;
@@ -432,7 +427,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
     {
         ProfScope _ps(ctx, "mm_chain_stats", (double)NB * (16.0 + 16.0 + 8.0) + (double)NM * 8.0);
         AnchorStatParams A{bx, by, cu, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, bchain, cq, a_idx.as<int32_t>(),
-                           c_mlen, c_blen, c_st, c_last};
+                           c_mlen, c_blen, c_st, c_last, pos_tab, qbase};
         if (NB > 0) {
             hipLaunchKernelGGL(anchor_mini_idx_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A);
             HY_CHECK_LAUNCH("anchor_mini_idx_kernel");
