@@ -611,7 +611,7 @@ static void backtrack_group(int64_t g0, int64_t g1, const int32_t *f, const int6
     free(tmp); free(z);
 }
 
-static const m128 *g_sort_a;
+static __thread const m128 *g_sort_a;  /* qsort context; thread-local so bench.py can map from threads */
 static int cmp_chain_first(const void *pa, const void *pb) {
     const chain_t *a = (const chain_t *)pa, *b = (const chain_t *)pb;
     return cmp128(&g_sort_a[a->first], &g_sort_a[b->first]);  /* compact_a: first-anchor x (ties: y) */

@@ -111,3 +111,25 @@ def test_repeat_and_edge_queries(toy):
     for q in [b"", b"ACGT", b"N" * 500, g[2][:14], (g[1][:300] * 40), g[3][1000:1300] + b"N" * 50 + g[3][5000:9000]]:
         regs, rl = ol.mm_map(idx, opt, q, "edge")
         assert (regs["qe"] <= len(q)).all()
+
+
+def test_map_from_threads_matches_sequential(toy):
+    """bench.py's CPU baseline maps from worker threads (the C mapper releases the GIL): the
+    oracle keeps no shared mutable state, so threaded results equal sequential ones."""
+    from concurrent.futures import ThreadPoolExecutor
+    _, refs, idx, opt = toy
+    rng = np.random.default_rng(5)
+    qs = []
+    for i in range(24):
+        t = int(rng.integers(0, len(refs)))
+        L = int(rng.integers(2000, 20000))
+        st = int(rng.integers(0, len(refs[t]) - L))
+        s = mutate(rng, refs[t][st:st + L], 0.02)
+        qs.append((f"q{i}", revcomp(s) if i % 3 == 0 else s))
+    seq = [ol.mm_map(idx, opt, s, n) for n, s in qs]
+    with ThreadPoolExecutor(8) as ex:
+        par = list(ex.map(lambda q: ol.mm_map(idx, opt, q[1], q[0]), qs * 3))
+    for k, (regs, rl) in enumerate(par):
+        sr, srl = seq[k % len(qs)]
+        assert rl == srl
+        np.testing.assert_array_equal(regs, sr)
