@@ -17,7 +17,15 @@
 #include "mm_common.hpp"
 
 #include <algorithm>
+#include <type_traits>
 #include <utility>
+
+#ifndef HYMET_ANCHOR_RB  // digit bits of the anchor-key radix sort (0: rocPRIM's default, 8)
+#define HYMET_ANCHOR_RB 0
+#endif
+#ifndef HYMET_ANCHOR_HIST_BLOCK
+#define HYMET_ANCHOR_HIST_BLOCK 512
+#endif
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -692,16 +700,28 @@ struct PhaseTrace {
     }
 };
 
-template <typename K, typename V>
+// RB > 0: onesweep with RB-bit digits (fewer passes over the data) instead of rocPRIM's
+// gfx950 default (8)
+template <int RB>
+using OnesweepCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<HYMET_ANCHOR_HIST_BLOCK, 16>, rocprim::kernel_config<512, 16>,
+                                        RB, rocprim::block_radix_rank_algorithm::match>>;
+
+template <typename K, typename V, int RB = 0>
 static int sort_pairs(hymet_ctx *ctx, K *&keys, K *&keys_alt, V *&vals, V *&vals_alt, int64_t n, int begin_bit, int end_bit,
                       const char *tag = "radix_sort") {
     if (n <= 1) return HYMET_OK;
-    ProfScope _ps(ctx, tag, 2.0 * (double)n * (sizeof(K) + sizeof(V)) * (double)((end_bit - begin_bit + 7) / 8));
+    const int digit = RB > 0 ? RB : 8;
+    ProfScope _ps(ctx, tag, 2.0 * (double)n * (sizeof(K) + sizeof(V)) * (double)((end_bit - begin_bit + digit - 1) / digit));
+    using Cfg = std::conditional_t<(RB > 0), OnesweepCfg<(RB > 0 ? RB : 8)>, rocprim::default_config>;
     size_t tmp = 0;
-    HY_HIP(rocprim::radix_sort_pairs(nullptr, tmp, keys, keys_alt, vals, vals_alt, (size_t)n, begin_bit, end_bit, ctx->stream));
+    HY_HIP(rocprim::radix_sort_pairs<Cfg>(nullptr, tmp, keys, keys_alt, vals, vals_alt, (size_t)n, begin_bit, end_bit,
+                                          ctx->stream));
     DevBuf t;
     HY_HIP(t.alloc(tmp, ctx->stream));
-    HY_HIP(rocprim::radix_sort_pairs(t.p, tmp, keys, keys_alt, vals, vals_alt, (size_t)n, begin_bit, end_bit, ctx->stream));
+    HY_HIP(rocprim::radix_sort_pairs<Cfg>(t.p, tmp, keys, keys_alt, vals, vals_alt, (size_t)n, begin_bit, end_bit,
+                                          ctx->stream));
     std::swap(keys, keys_alt);
     std::swap(vals, vals_alt);
     return HYMET_OK;
@@ -781,7 +801,7 @@ static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n,
     HY_HIP(vb.alloc(4 * (size_t)n, ctx->stream));
     uint64_t *kk = key.as<uint64_t>(), *kka = kb.as<uint64_t>();
     uint32_t *vv = val.as<uint32_t>(), *vva = vb.as<uint32_t>();
-    int rc = sort_pairs(ctx, kk, kka, vv, vva, n, 0, end_bit, "radix_sort_anchors");
+    int rc = sort_pairs<uint64_t, uint32_t, HYMET_ANCHOR_RB>(ctx, kk, kka, vv, vva, n, 0, end_bit, "radix_sort_anchors");
     if (rc) return rc;
     HY_HIP(out.ax.alloc(8 * (size_t)n, ctx->stream));
     HY_HIP(out.ay.alloc(8 * (size_t)n, ctx->stream));
