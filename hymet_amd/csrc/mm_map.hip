@@ -113,136 +113,143 @@ __global__ void sample_off_kernel(const int64_t *pos, const int64_t *qm_off, int
     out[q] = q == n_q ? total : pos[qm_off[q]];
 }
 
-struct SeedParams {
-    const uint64_t *mx, *my;
-    const int64_t *qm_off;
-    const int64_t *qlen;
-    const uint32_t *koff;
-    int64_t n_buckets;
-    int n_q;
-    int max_occ, max_max_occ, dist;
-    uint32_t *seed_n;    // occurrences of every minimizer (seed_count_kernel); out: 0 = not a seed or filtered
-    int32_t *rep_len;    // out per query
-    const uint32_t *q_high;  // query holds a seed above max_occ
-};
-
-// occurrences of every minimizer (one thread each); flags the queries holding a seed above
-// max_occ -- only those need the sequential streak selection below
-__global__ void seed_count_kernel(const uint64_t *mx, const uint32_t *qid, int64_t n, const uint32_t *koff,
-                                  int64_t n_buckets, int max_occ, uint32_t *seed_n, uint32_t *q_high) {
+// occurrences of every minimizer (one thread each)
+__global__ void seed_count_kernel(const uint64_t *mx, int64_t n, const uint32_t *koff, int64_t n_buckets,
+                                  uint32_t *seed_n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t h = mx[i] >> 8;
     uint32_t c = 0;
     if ((int64_t)h < n_buckets) c = koff[h + 1] - koff[h];
     seed_n[i] = c;
-    if ((int)c > max_occ) q_high[qid[i]] = 1;
 }
 
-// one thread per query: mm_seed_collect_all + mm_seed_select + mm_collect_matches
-__global__ __launch_bounds__(64) void seed_select_kernel(SeedParams P) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= P.n_q) return;
-    if (!P.q_high[q]) {  // no seed above max_occ: nothing is filtered, rep_len = 0
-        P.rep_len[q] = 0;
-        return;
-    }
-    const int64_t m0 = P.qm_off[q], m1 = P.qm_off[q + 1];
-    const int len = (int)P.qlen[q];
-    int n_seed = 0, n_high = 0;
-    for (int64_t i = m0; i < m1; i++) {
-        const uint32_t n = P.seed_n[i];
-        if (n) {
-            n_seed++;
-            if ((int)n > P.max_occ) n_high++;
-        }
-    }
-    // flt flags are kept in bit 31 of seed_n (n < 2^31)
-    const uint32_t FLT = 0x80000000u;
-    if (P.dist > 0 && P.max_max_occ > P.max_occ) {
-        if (n_seed > 1 && n_high > 0) {
-            int64_t last0 = -1;  // minimizer index of the last low-occurrence seed
-            int last0_j = -1;    // its seed number
-            int j = 0;           // seed number
-            int64_t st_i = -1;   // first minimizer of the current streak
-            int st_j = 0;
-            for (int64_t i = m0; i <= m1; i++) {
-                uint32_t n = 0;
-                if (i < m1) {
-                    n = P.seed_n[i];
-                    if (!n) continue;
-                }
-                const bool low = (i == m1) || (int)n <= P.max_occ;
-                if (low) {
-                    if (st_i >= 0 && j - last0_j > 1) {
-                        const int32_t ps = last0 < 0 ? 0 : (int32_t)((uint32_t)P.my[last0] >> 1);
-                        const int32_t pe = i == m1 ? len : (int32_t)((uint32_t)P.my[i] >> 1);
-                        int32_t mh = (int32_t)((double)(pe - ps) / P.dist + .499);
-                        if (mh > 128) mh = 128;
-                        const int cnt = j - st_j;
-                        uint64_t thr = 0;  // keep seeds with key <= thr (the mh smallest (n, j))
-                        bool keep_all = mh >= cnt, keep_none = mh <= 0;
-                        if (!keep_all && !keep_none) {
-                            uint64_t lo = 0, hi = ~0ull;
-                            while (lo < hi) {  // smallest T with #(key <= T) >= mh
-                                const uint64_t mid = lo + (hi - lo) / 2;
-                                int c = 0, jj = st_j;
-                                for (int64_t a = st_i; a < i; a++) {
-                                    const uint32_t na = P.seed_n[a] & ~FLT;
-                                    if (!na) continue;
-                                    const uint64_t key = (uint64_t)na << 32 | (uint32_t)jj;
-                                    c += key <= mid;
-                                    jj++;
-                                }
-                                if (c >= mh) hi = mid;
-                                else lo = mid + 1;
-                            }
-                            thr = lo;
-                        }
-                        int jj = st_j;
-                        for (int64_t a = st_i; a < i; a++) {
-                            uint32_t na = P.seed_n[a] & ~FLT;
-                            if (!na) continue;
-                            const uint64_t key = (uint64_t)na << 32 | (uint32_t)jj;
-                            bool chosen = keep_all || (!keep_none && key <= thr);
-                            bool flt = !chosen;
-                            if ((int)na > P.max_max_occ) flt = true;
-                            P.seed_n[a] = na | (flt ? FLT : 0u);
-                            jj++;
-                        }
-                    }
-                    if (i < m1) {
-                        last0 = i;
-                        last0_j = j;
-                    }
-                    st_i = -1;
-                } else if (st_i < 0) {
-                    st_i = i;
-                    st_j = j;
-                }
-                if (i < m1) j++;
-            }
-        }
+// ---- mm_seed_select + mm_collect_matches (seed.c), flat over the batch's minimizers.
+// The sequential per-query loop is decomposed:
+//   * every seed is low (n <= max_occ) or high; one scan of packed (low, high) counts ranks
+//     them, and the low / high seeds are listed in order;
+//   * a streak (maximal run of high seeds) ends at a low seed or at its query's end: one
+//     thread per such end selects the streak's mh kept seeds -- the mh smallest (n, seed
+//     number) keys, mh = round((pe - ps) / dist) capped at 128 from the bounding low seeds'
+//     positions -- and flags the rest (and every seed above max_max_occ) as filtered;
+//   * rep_len = sum over filtered seeds of en - max(st, en of the query's previous filtered
+//     seed), the union of their spans (ends increase along the query): one max-scan finds
+//     each one's predecessor, one integer atomic per seed sums the query.
+constexpr uint32_t kFlt = 0x80000000u;  // filtered flag, kept in bit 31 of seed_n (n < 2^31)
+
+__global__ void seed_class_kernel(const uint32_t *seed_n, int64_t M, int max_occ, uint64_t *cls) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const uint32_t n = seed_n[i];
+    const bool hi = (int)n > max_occ, lo = n > 0 && !hi;
+    cls[i] = (uint64_t)(hi ? 1u : 0u) << 32 | (lo ? 1u : 0u);
+}
+
+__global__ void seed_list_kernel(const uint32_t *seed_n, const uint64_t *rank, int64_t M, int max_occ, int32_t *low_idx,
+                                 int32_t *high_idx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M) return;
+    const uint32_t n = seed_n[i];
+    if (!n) return;
+    if ((int)n > max_occ) high_idx[rank[i] >> 32] = (int32_t)i;
+    else low_idx[(uint32_t)rank[i]] = (int32_t)i;
+}
+
+struct StreakParams {
+    const uint64_t *my;
+    const uint32_t *qid;
+    const int64_t *qm_off, *qlen;
+    const uint64_t *rank;      // exclusive (low, high) counts, M + 1 entries
+    const int32_t *low_idx, *high_idx;
+    int64_t n_low;
+    int n_q;
+    int max_occ, max_max_occ, dist;
+    uint32_t *seed_n;
+    uint32_t *flt_high;        // per high rank: filtered
+};
+
+__global__ void streak_kernel(StreakParams P) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= P.n_low + P.n_q) return;
+    int q;
+    int64_t e_idx = -1, p_idx = -1;  // ending low seed, previous low seed (minimizer indices)
+    uint64_t re, rp;                 // (low, high) ranks at the streak's end and start
+    if (t < P.n_low) {
+        e_idx = P.low_idx[t];
+        q = (int)P.qid[e_idx];
+        re = P.rank[e_idx];
+        if (t > 0 && P.qid[P.low_idx[t - 1]] == (uint32_t)q) p_idx = P.low_idx[t - 1];
     } else {
-        for (int64_t i = m0; i < m1; i++)
-            if ((int)P.seed_n[i] > P.max_occ) P.seed_n[i] |= FLT;
+        q = (int)(t - P.n_low);
+        re = P.rank[P.qm_off[q + 1]];
+        const uint64_t r0 = P.rank[P.qm_off[q]];
+        if ((uint32_t)re > (uint32_t)r0) p_idx = P.low_idx[(uint32_t)re - 1];
     }
-    // mm_collect_matches: rep_len over filtered seeds, then clear filtered counts
-    int rep_st = 0, rep_en = 0, rep = 0;
-    for (int64_t i = m0; i < m1; i++) {
-        const uint32_t n = P.seed_n[i];
-        if (!n) continue;
-        if (n & FLT) {
-            const int en = (int)((uint32_t)P.my[i] >> 1) + 1, st = en - (int)(P.mx[i] & 0xff);
-            if (st > rep_en) {
-                rep += rep_en - rep_st;
-                rep_st = st, rep_en = en;
-            } else rep_en = en;
-            P.seed_n[i] = 0;
+    rp = p_idx >= 0 ? P.rank[p_idx] : P.rank[P.qm_off[q]];
+    const int64_t h0 = (int64_t)(rp >> 32), h1 = (int64_t)(re >> 32);  // the streak's high ranks
+    const int cnt = (int)(h1 - h0);
+    if (cnt <= 0) return;
+    const bool case_a = P.dist > 0 && P.max_max_occ > P.max_occ;
+    bool keep_all = false, keep_none = false;
+    uint64_t thr = 0;
+    if (case_a) {
+        const uint64_t rq0 = P.rank[P.qm_off[q]], rq1 = P.rank[P.qm_off[q + 1]];
+        const int64_t n_seed = (int64_t)((uint32_t)rq1 - (uint32_t)rq0) + (int64_t)((rq1 >> 32) - (rq0 >> 32));
+        if (n_seed <= 1) return;  // seed.c: nothing is filtered for a single seed
+        const int32_t ps = p_idx >= 0 ? (int32_t)((uint32_t)P.my[p_idx] >> 1) : 0;
+        const int32_t pe = e_idx >= 0 ? (int32_t)((uint32_t)P.my[e_idx] >> 1) : (int32_t)P.qlen[q];
+        int32_t mh = (int32_t)((double)(pe - ps) / P.dist + .499);
+        if (mh > 128) mh = 128;
+        keep_all = mh >= cnt, keep_none = mh <= 0;
+        if (!keep_all && !keep_none) {  // the mh-th smallest (n, index) key
+            uint64_t lo = 0, hi = ~0ull;
+            while (lo < hi) {
+                const uint64_t mid = lo + (hi - lo) / 2;
+                int c = 0;
+                for (int64_t r = h0; r < h1; r++) {
+                    const int32_t a = P.high_idx[r];
+                    c += ((uint64_t)P.seed_n[a] << 32 | (uint32_t)a) <= mid;
+                }
+                if (c >= mh) hi = mid;
+                else lo = mid + 1;
+            }
+            thr = lo;
         }
     }
-    rep += rep_en - rep_st;
-    P.rep_len[q] = rep;
+    for (int64_t r = h0; r < h1; r++) {
+        const int32_t a = P.high_idx[r];
+        const uint32_t n = P.seed_n[a];
+        bool flt = true;  // case B: every seed above max_occ
+        if (case_a) {
+            const bool chosen = keep_all || (!keep_none && ((uint64_t)n << 32 | (uint32_t)a) <= thr);
+            flt = !chosen || (int)n > P.max_max_occ;
+        }
+        P.flt_high[r] = flt ? 1u : 0u;
+    }
+}
+
+// previous filtered high seed: inclusive max-scan of (flt ? rank : -1)
+__global__ void flt_mark_kernel(const uint32_t *flt_high, int64_t n_high, int32_t *v) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n_high) v[r] = flt_high[r] ? (int32_t)r : -1;
+}
+
+__global__ void rep_len_kernel(const uint32_t *flt_high, const int32_t *prev_max, const int32_t *high_idx, int64_t n_high,
+                               const uint64_t *mx, const uint64_t *my, const uint32_t *qid, int32_t *rep_len,
+                               uint32_t *seed_n) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_high || !flt_high[r]) return;
+    const int32_t a = high_idx[r];
+    const uint32_t q = qid[a];
+    const int32_t en = (int32_t)((uint32_t)my[a] >> 1) + 1, st = en - (int32_t)(mx[a] & 0xff);
+    int32_t en_prev = 0;
+    const int32_t pr = r > 0 ? prev_max[r - 1] : -1;
+    if (pr >= 0) {
+        const int32_t b = high_idx[pr];
+        if (qid[b] == q) en_prev = (int32_t)((uint32_t)my[b] >> 1) + 1;
+    }
+    atomicAdd(rep_len + q, en - max(st, en_prev));
+    seed_n[a] = 0;  // filtered: not a seed any more
 }
 
 __global__ void nz_flag_kernel(const uint32_t *v, int64_t n, uint32_t *flag) {
@@ -1223,25 +1230,63 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
     }
     tr.mark("mz_flt");
     // ------------------------------------------------------------- 3 seeds
-    DevBuf seed_n, rep_len, qid, q_high;
+    DevBuf seed_n, rep_len, qid;
     HY_HIP(seed_n.alloc(4 * (size_t)(M + 1), st));
     HY_HIP(rep_len.alloc(4 * (size_t)n_q, st));
     HY_HIP(qid.alloc(4 * (size_t)(M + 1), st));
-    HY_HIP(q_high.alloc(4 * (size_t)n_q, st));
-    HY_HIP(hipMemsetAsync(q_high.p, 0, 4 * (size_t)n_q, st));
+    HY_HIP(hipMemsetAsync(rep_len.p, 0, 4 * (size_t)n_q, st));
     LAUNCH1(fill_qid_kernel, M, qm_off.as<int64_t>(), n_q, M, qid.as<uint32_t>());
     {
         ProfScope _ps(ctx, "mm_seed_count", (double)M * (8.0 + 8.0 + 4.0));  // minimizer, 2 offsets, count
-        LAUNCH1(seed_count_kernel, M, mx.as<uint64_t>(), qid.as<uint32_t>(), M, idx->d_koff, idx->n_buckets, opt->mid_occ,
-                seed_n.as<uint32_t>(), q_high.as<uint32_t>());
+        LAUNCH1(seed_count_kernel, M, mx.as<uint64_t>(), M, idx->d_koff, idx->n_buckets, seed_n.as<uint32_t>());
     }
-    {
-        SeedParams P{mx.as<uint64_t>(), my.as<uint64_t>(), qm_off.as<int64_t>(), d_qlen.as<int64_t>(), idx->d_koff,
-                     idx->n_buckets, n_q, opt->mid_occ, opt->max_max_occ, opt->occ_dist, seed_n.as<uint32_t>(),
-                     rep_len.as<int32_t>(), q_high.as<uint32_t>()};
-        ProfScope _ps(ctx, "mm_seed_select", (double)M * (8.0 + 8.0 + 4.0 + 4.0));  // minimizer x/y, count, seed flag
-        hipLaunchKernelGGL(seed_select_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P);
-        HY_CHECK_LAUNCH("seed_select_kernel");
+    if (M > 0) {
+        ProfScope _ps(ctx, "mm_seed_select", (double)M * (4.0 + 8.0 + 8.0 + 8.0));  // count, class, rank, list
+        DevBuf cls, rank;
+        HY_HIP(cls.alloc(8 * (size_t)(M + 1), st));
+        HY_HIP(rank.alloc(8 * (size_t)(M + 1), st));
+        LAUNCH1(seed_class_kernel, M, seed_n.as<uint32_t>(), M, opt->mid_occ, cls.as<uint64_t>());
+        HY_HIP(hipMemsetAsync(cls.as<uint64_t>() + M, 0, 8, st));
+        {  // exclusive scan of packed (low, high) counts over M + 1 entries: rank[M] = totals
+            size_t tmp = 0;
+            HY_HIP(rocprim::exclusive_scan(nullptr, tmp, cls.as<uint64_t>(), rank.as<uint64_t>(), (uint64_t)0,
+                                           (size_t)(M + 1), rocprim::plus<uint64_t>(), st));
+            DevBuf t;
+            HY_HIP(t.alloc(tmp, st));
+            HY_HIP(rocprim::exclusive_scan(t.p, tmp, cls.as<uint64_t>(), rank.as<uint64_t>(), (uint64_t)0,
+                                           (size_t)(M + 1), rocprim::plus<uint64_t>(), st));
+        }
+        uint64_t tot = 0;
+        HY_HIP(hipMemcpyAsync(&tot, rank.as<uint64_t>() + M, 8, hipMemcpyDeviceToHost, st));
+        HY_HIP(hipStreamSynchronize(st));
+        const int64_t n_low = (uint32_t)tot, n_high = (int64_t)(tot >> 32);
+        if (n_high > 0) {
+            DevBuf low_idx, high_idx, flt_high, vmax, pmax;
+            HY_HIP(low_idx.alloc(4 * (size_t)(n_low + 1), st));
+            HY_HIP(high_idx.alloc(4 * (size_t)n_high, st));
+            HY_HIP(flt_high.alloc(4 * (size_t)n_high, st));
+            LAUNCH1(seed_list_kernel, M, seed_n.as<uint32_t>(), rank.as<uint64_t>(), M, opt->mid_occ,
+                    low_idx.as<int32_t>(), high_idx.as<int32_t>());
+            StreakParams S{my.as<uint64_t>(), qid.as<uint32_t>(), qm_off.as<int64_t>(), d_qlen.as<int64_t>(),
+                           rank.as<uint64_t>(), low_idx.as<int32_t>(), high_idx.as<int32_t>(), n_low, n_q, opt->mid_occ,
+                           opt->max_max_occ, opt->occ_dist, seed_n.as<uint32_t>(), flt_high.as<uint32_t>()};
+            HY_HIP(hipMemsetAsync(flt_high.p, 0, 4 * (size_t)n_high, st));
+            LAUNCH1(streak_kernel, n_low + n_q, S);
+            HY_HIP(vmax.alloc(4 * (size_t)n_high, st));
+            HY_HIP(pmax.alloc(4 * (size_t)n_high, st));
+            LAUNCH1(flt_mark_kernel, n_high, flt_high.as<uint32_t>(), n_high, vmax.as<int32_t>());
+            {
+                size_t tmp = 0;
+                HY_HIP(rocprim::inclusive_scan(nullptr, tmp, vmax.as<int32_t>(), pmax.as<int32_t>(), (size_t)n_high,
+                                               rocprim::maximum<int32_t>(), st));
+                DevBuf t;
+                HY_HIP(t.alloc(tmp, st));
+                HY_HIP(rocprim::inclusive_scan(t.p, tmp, vmax.as<int32_t>(), pmax.as<int32_t>(), (size_t)n_high,
+                                               rocprim::maximum<int32_t>(), st));
+            }
+            LAUNCH1(rep_len_kernel, n_high, flt_high.as<uint32_t>(), pmax.as<int32_t>(), high_idx.as<int32_t>(), n_high,
+                    mx.as<uint64_t>(), my.as<uint64_t>(), qid.as<uint32_t>(), rep_len.as<int32_t>(), seed_n.as<uint32_t>());
+        }
     }
     tr.mark("seeds");
     // ------------------------------------------------------------ 4 anchors
