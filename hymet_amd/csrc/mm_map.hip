@@ -648,20 +648,34 @@ __global__ void chain_cnt_kernel(const uint64_t *cu, int64_t n, uint32_t *cnt) {
     if (i < n) cnt[i] = (uint32_t)cu[i];
 }
 
-// one wave per chain (grid-stride): anchors of chain c in start -> end order, and c per anchor
-__global__ __launch_bounds__(64) void chain_copy_kernel(const uint64_t *cu, const int64_t *cfirst, const int64_t *bpos,
-                                                        const int64_t *chain_ids, const uint64_t *ax, const uint64_t *ay,
-                                                        int64_t n, uint64_t *bx, uint64_t *by, int32_t *bchain) {
-    for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
-        const int32_t m = (int32_t)cu[c];
-        const int64_t f = cfirst[c], o = bpos[c];
-        for (int32_t j = threadIdx.x; j < m; j += 64) {
-            const int64_t a = chain_ids[f + m - 1 - j];  // backtrack stores end -> start
-            bx[o + j] = ax[a];
-            by[o + j] = ay[a];
-            bchain[o + j] = (int32_t)c;
+// anchors of chain c in start -> end order, and c per anchor
+__global__ __launch_bounds__(256) void chain_copy_kernel(const uint64_t *cu, const int64_t *cfirst, const int64_t *bpos,
+                                                         const int64_t *chain_ids, const uint64_t *ax, const uint64_t *ay,
+                                                         int64_t n_chain, int64_t nb, uint64_t *bx, uint64_t *by,
+                                                         int32_t *bchain) {
+    // flat over the output anchors: the block's first chain by binary search over bpos, each
+    // lane's by a short forward walk (chains are tens to thousands of anchors long)
+    __shared__ int64_t s_c0;
+    const int64_t b0 = (int64_t)blockIdx.x * blockDim.x;
+    if (threadIdx.x == 0) {
+        int64_t lo = 0, hi = n_chain - 1;  // last c with bpos[c] <= b0
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) >> 1;
+            if (bpos[mid] <= b0) lo = mid;
+            else hi = mid - 1;
         }
+        s_c0 = lo;
     }
+    __syncthreads();
+    const int64_t b = b0 + threadIdx.x;
+    if (b >= nb) return;
+    int64_t c = s_c0;
+    while (c + 1 < n_chain && bpos[c + 1] <= b) c++;
+    const int32_t m = (int32_t)cu[c];
+    const int64_t a = chain_ids[cfirst[c] + m - 1 - (b - bpos[c])];  // backtrack stores end -> start
+    bx[b] = ax[a];
+    by[b] = ay[a];
+    bchain[b] = (int32_t)c;
 }
 
 // query of each chain (from the sorted first-anchor key, via the anchor query offsets)
@@ -1033,13 +1047,10 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(C.bx.alloc(8 * (size_t)(NB + 1), ctx->stream));
         HY_HIP(C.by.alloc(8 * (size_t)(NB + 1), ctx->stream));
         HY_HIP(C.bchain.alloc(4 * (size_t)(NB + 1), ctx->stream));
-        if (NC > 0) {
-            const int64_t nb = NC < (int64_t)ctx->n_cu * 64 ? NC : (int64_t)ctx->n_cu * 64;
-            hipLaunchKernelGGL(chain_copy_kernel, dim3((unsigned)nb), dim3(64), 0, ctx->stream, C.cu.as<uint64_t>(),
-                               cf_s.as<int64_t>(), C.cboff.as<int64_t>(), chain_ids.as<int64_t>(), A.ax.as<uint64_t>(),
-                               A.ay.as<uint64_t>(), NC, C.bx.as<uint64_t>(), C.by.as<uint64_t>(), C.bchain.as<int32_t>());
-            HY_CHECK_LAUNCH("chain_copy_kernel");
-        }
+        if (NC > 0 && NB > 0)
+            LAUNCH1(chain_copy_kernel, NB, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), C.cboff.as<int64_t>(),
+                    chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, NB, C.bx.as<uint64_t>(),
+                    C.by.as<uint64_t>(), C.bchain.as<int32_t>());
         // per-query chain offsets
         DevBuf &cq = C.cq;
         HY_HIP(cq.alloc(4 * (size_t)(NC + 1), ctx->stream));
@@ -1118,12 +1129,18 @@ __global__ void rechain_gather_kernel(const uint64_t *bx, const uint64_t *by, co
 }
 
 // one thread per re-chain anchor (flat: a block per query left the long queries' blocks as
-// the tail); its query by binary search over the new offsets
-__global__ void rechain_keys_kernel(const uint64_t *bx, const uint64_t *by, const int64_t *qb, const int64_t *new_off,
-                                    int n_q, int64_t n, int rb, int pb, uint64_t *key, uint32_t *val) {
-    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// the tail); the block's first query by one binary search, each lane's by a short forward walk
+__global__ __launch_bounds__(256) void rechain_keys_kernel(const uint64_t *bx, const uint64_t *by, const int64_t *qb,
+                                                           const int64_t *new_off, int n_q, int64_t n, int rb, int pb,
+                                                           uint64_t *key, uint32_t *val) {
+    __shared__ int s_q0;
+    const int64_t a0 = (int64_t)blockIdx.x * blockDim.x;
+    if (threadIdx.x == 0) s_q0 = upper_idx(new_off, n_q, a0);
+    __syncthreads();
+    const int64_t a = a0 + threadIdx.x;
     if (a >= n) return;
-    const int q = upper_idx(new_off, n_q, a);  // last q with new_off[q] <= a (non-empty)
+    int q = s_q0;
+    while (q + 1 < n_q && new_off[q + 1] <= a) q++;  // last q with new_off[q] <= a
     const int64_t i = qb[q] + (a - new_off[q]);
     const uint64_t ax = bx[i];
     key[a] = (uint64_t)q << (1 + rb + pb) | (ax >> 63) << (rb + pb) | (ax << 1 >> 33) << pb | (uint32_t)ax;
