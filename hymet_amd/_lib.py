@@ -26,6 +26,8 @@ _SIGS = {
     "hymet_prof_reset": (_i32, [_vp]),
     "hymet_prof_query": (_i32, [_vp, _c.c_char_p, _c.POINTER(_c.c_double), _c.POINTER(_i64), _c.POINTER(_c.c_double)]),
     "hymet_prof_names": (_i32, [_vp, _c.c_char_p, _i64]),
+    "hymet_scratch_trim": (_i32, [_vp, _c.POINTER(_i64)]),
+    "hymet_scratch_cached": (_i32, [_vp, _c.POINTER(_i64)]),
     "hymet_pack": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "hymet_screen_table_slots": (_i64, [_i64]),
     "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
@@ -127,6 +129,12 @@ class Gpu:
             check(self.lib.hymet_prof_query(self.ctx, name.encode(), _c.byref(ms), _c.byref(n), _c.byref(b)), "hymet_prof_query")
             out[name] = (ms.value, n.value, b.value)
         return out
+
+    def trim(self) -> int:
+        """Return the library's cached kernel scratch to HIP; bytes freed."""
+        out = _i64()
+        check(self.lib.hymet_scratch_trim(self.ctx, _c.byref(out)), "hymet_scratch_trim")
+        return out.value
 
     def empty(self, n, dtype):
         return self.torch.empty(int(n), dtype=dtype, device=self.dev)

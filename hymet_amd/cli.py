@@ -73,13 +73,10 @@ def cmd_screen(argv: Sequence[str]) -> int:
     print(f"Number of input sequences: {n_files}")
     print(f"Minimum expected candidates: {need}")
     print("====================================")
-    best, top, names = sel.select_threshold(s_rows, thresh, n_files)
+    best, top, names, log = sel.threshold_walk(s_rows, thresh, n_files)
     _write_lines(top_hits, top)
     _write_lines(selected, names)
-    print("====================================")
-    print(f"Final threshold used: {best}")
-    print(f"Candidates found: {len(top)}")
-    print("====================================")
+    print("\n".join(log))     # mash.sh:35-36,50,57-60: per-threshold lines, fallback note, summary
     return 0
 
 

@@ -4,6 +4,8 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <tuple>
+#include <cstdlib>
 #include <vector>
 
 namespace hymet {
@@ -19,7 +21,25 @@ int hip_fail(hipError_t e, const char *what) {
 }
 
 static std::mutex g_cache_mu;
-static std::map<std::pair<int, size_t>, std::vector<void *>> g_cache;  // (device, class) -> free blocks
+struct CacheKey {
+    int dev;
+    hipStream_t stream;
+    size_t cls;
+    bool operator<(const CacheKey &o) const {
+        return std::tie(dev, stream, cls) < std::tie(o.dev, o.stream, o.cls);
+    }
+};
+static std::map<CacheKey, std::vector<void *>> g_cache;  // free blocks
+static size_t g_cached = 0;                                // bytes held in g_cache
+
+static size_t cache_cap() {
+    static const size_t cap = [] {
+        const char *e = getenv("HYMET_SCRATCH_CAP_GB");
+        const double gb = e ? atof(e) : 96.0;
+        return (size_t)(gb * 1073741824.0);
+    }();
+    return cap;
+}
 
 static size_t size_class(size_t b) {
     if (b <= 4096) return 4096;
@@ -28,17 +48,30 @@ static size_t size_class(size_t b) {
     return (b + q - 1) / q * q;
 }
 
-hipError_t scratch_alloc(size_t bytes, void **p, size_t *cls) {
+// free every cached block of `dev` (all streams); caller holds g_cache_mu
+static void drop_cached(int dev) {
+    for (auto &kv : g_cache)
+        if (kv.first.dev == dev) {
+            for (void *q : kv.second) {
+                (void)hipFree(q);
+                g_cached -= kv.first.cls;
+            }
+            kv.second.clear();
+        }
+}
+
+hipError_t scratch_alloc(size_t bytes, hipStream_t stream, void **p, size_t *cls) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     *cls = size_class(bytes);
     {
         std::lock_guard<std::mutex> lk(g_cache_mu);
-        auto it = g_cache.find({dev, *cls});
+        auto it = g_cache.find({dev, stream, *cls});
         if (it != g_cache.end() && !it->second.empty()) {
             *p = it->second.back();
             it->second.pop_back();
+            g_cached -= *cls;
             return hipSuccess;
         }
     }
@@ -47,21 +80,35 @@ hipError_t scratch_alloc(size_t bytes, void **p, size_t *cls) {
         (void)hipGetLastError();
         (void)hipDeviceSynchronize();
         std::lock_guard<std::mutex> lk(g_cache_mu);
-        for (auto &kv : g_cache)
-            if (kv.first.first == dev) {
-                for (void *q : kv.second) (void)hipFree(q);
-                kv.second.clear();
-            }
+        drop_cached(dev);
         e = hipMalloc(p, *cls);
     }
     return e;
 }
 
-void scratch_free(void *p, size_t cls) {
+void scratch_free(void *p, hipStream_t stream, size_t cls) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> lk(g_cache_mu);
-    g_cache[{dev, cls}].push_back(p);
+    if (g_cached + cls > cache_cap()) {  // over the cap: hand it back (hipFree waits for the device)
+        (void)hipFree(p);
+        return;
+    }
+    g_cache[{dev, stream, cls}].push_back(p);
+    g_cached += cls;
+}
+
+int scratch_trim(int dev, int64_t *freed) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    const size_t before = g_cached;
+    drop_cached(dev);
+    if (freed) *freed = (int64_t)(before - g_cached);
+    return HYMET_OK;
+}
+
+int64_t scratch_cached() {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    return (int64_t)g_cached;
 }
 }  // namespace hymet
 
@@ -151,6 +198,19 @@ int hymet_prof_names(hymet_ctx *ctx, char *buf, int64_t cap) {
     for (auto &kv : ctx->ev) all += kv.first + "\n";
     if ((int64_t)all.size() + 1 > cap) return hymet::fail(HYMET_E_CAPACITY, "hymet_prof_names: buffer too small");
     memcpy(buf, all.c_str(), all.size() + 1);
+    return HYMET_OK;
+}
+
+int hymet_scratch_trim(hymet_ctx *ctx, int64_t *freed_bytes) {
+    HY_ARG(ctx != nullptr, "hymet_scratch_trim: null ctx");
+    HY_HIP(hipSetDevice(ctx->device));
+    HY_HIP(hipStreamSynchronize(ctx->stream));
+    return hymet::scratch_trim(ctx->device, freed_bytes);
+}
+
+int hymet_scratch_cached(hymet_ctx *ctx, int64_t *bytes) {
+    HY_ARG(ctx && bytes, "hymet_scratch_cached: null argument");
+    *bytes = hymet::scratch_cached();
     return HYMET_OK;
 }
 

@@ -37,23 +37,25 @@ __host__ __device__ __forceinline__ uint64_t hash64(uint64_t key) {
 }
 
 // Device scratch from the library's caching allocator (hymet::scratch_alloc), returned to the
-// cache at scope exit.  All work of a context runs on its one stream, so a block handed back
-// while kernels that use it are still queued can be reissued at once: the next user is queued
-// behind them.
+// cache at scope exit.  The cache is per stream and all work of a context runs on its one
+// stream, so a block handed back while kernels that use it are still queued can be reissued
+// at once: the next user is queued behind them.
 struct DevBuf {
     void *p = nullptr;
     size_t n = 0, cls = 0;
+    hipStream_t st = nullptr;
     DevBuf() = default;
     DevBuf(const DevBuf &) = delete;
     DevBuf &operator=(const DevBuf &) = delete;
     ~DevBuf() { release(); }
-    hipError_t alloc(size_t bytes, hipStream_t) {
+    hipError_t alloc(size_t bytes, hipStream_t stream) {
         release();
         n = bytes;
-        return scratch_alloc(bytes == 0 ? 16 : bytes, &p, &cls);
+        st = stream;
+        return scratch_alloc(bytes == 0 ? 16 : bytes, stream, &p, &cls);
     }
     void release() {
-        if (p) scratch_free(p, cls);
+        if (p) scratch_free(p, st, cls);
         p = nullptr;
         n = 0;
     }
@@ -65,6 +67,7 @@ struct DevBuf {
         std::swap(p, o.p);
         std::swap(n, o.n);
         std::swap(cls, o.cls);
+        std::swap(st, o.st);
     }
 };
 

@@ -45,6 +45,7 @@ class IndexSet:
     lens: np.ndarray
     parts: List[mp.IndexPart]
     part_first: List[int]             # global target index of each part's rid 0
+    opt: mp.MapOpt                    # asm10 options, mid_occ resolved on this set's first part
 
 
 @dataclass
@@ -68,7 +69,14 @@ class Pipeline:
         self.dbs = list(dbs)
         self.tables = [scr.ScreenTable(gpu, db) for db in self.dbs]
         self.ref_lookup = ref_lookup
-        self.classifier = cls.Classifier(gpu, taxonomy, hierarchy, variant)
+        self.taxonomy, self.variant = taxonomy, variant
+        # classification_cami.py runs as `... || true` (run_hymet_cami.sh:175-180): a
+        # classifier that cannot load its inputs leaves an empty TSV, and the fallback runs
+        try:
+            self.classifier = cls.Classifier(gpu, taxonomy, hierarchy, variant)
+            self.classifier_error = None
+        except Exception as e:  # noqa: BLE001 -- any failure of the reference script
+            self.classifier, self.classifier_error = None, e
         self.index_cache: Dict[str, IndexSet] = {}
         self.opt: Optional[mp.MapOpt] = None
 
@@ -98,7 +106,11 @@ class Pipeline:
             sub = refs.subset(p) if len(parts_idx) > 1 else refs
             parts.append(mp.IndexPart(self.gpu, sub, self.cfg.w, self.cfg.k))
             first.append(int(p[0]))
-        ix = IndexSet(list(refs.names), np.asarray(refs.lengths, np.int64), parts, first)
+        # a fresh `minimap2 -x asm10` process per run: mm_mapopt_update resolves mid_occ from
+        # the first part of THIS index (options.c), so the options live with the index set
+        opt = mp.MapOpt.asm10()
+        opt.resolve_mid_occ(parts[0])
+        ix = IndexSet(list(refs.names), np.asarray(refs.lengths, np.int64), parts, first, opt)
         self.index_cache = {key: ix}  # one cached candidate set, like the sha1 cache dir
         return ix
 
@@ -114,9 +126,7 @@ class Pipeline:
 
     def map_all(self, ix: IndexSet, pq: "Prepared"):
         """Per part, per query batch -> list of (part, query offset, MapResult)."""
-        if self.opt is None:
-            self.opt = mp.MapOpt.asm10()
-            self.opt.resolve_mid_occ(ix.parts[0])   # mm_mapopt_update: first part fixes mid_occ
+        self.opt = ix.opt
         out = []
         for pi, part in enumerate(ix.parts):
             for b0, qp, nh in pq.batches:
@@ -159,7 +169,7 @@ class Pipeline:
             line_q, line_t = np.zeros(0, np.int32), np.zeros(0, np.int32)
             line_b, line_l = np.zeros(0, np.int64), np.zeros(0, np.int64)
         exact = np.zeros(len(line_q), np.uint8)
-        if self.classifier.variant == cls.LEGACY and len(line_q):
+        if self.variant == cls.LEGACY and len(line_q):
             # classification.py:141-151: query == target and coverage >= 0.99
             same = np.asarray(qnames, dtype=object)[all_q] == np.asarray(ix.names, dtype=object)[line_t]
             cov = np.where(line_l > 0, line_b / np.maximum(line_l, 1), 0.0)
@@ -180,15 +190,43 @@ class Pipeline:
         ix = self.index_for(selected)
         results = self.map_all(ix, pq)
         table, text = self.paf_table(ix, queries, results, with_paf)
-        res = self.classifier.run(table, comm=self.comm)
-        rws = self.classifier.rows(res)
-        if self.comm is not None and self.comm.world > 1:
-            part, q = self.last_qkey
+        part, q = self.last_qkey
+        multi = self.comm is not None and self.comm.world > 1
+        gid = None
+        if multi:
             gid = (np.asarray(query_ids, np.int64)[q] if query_ids is not None
                    else (np.int64(self.comm.rank) << np.int64(32)) + q)
-            rws = gather_rows(self.comm, rws, part, gid)
-        tsv = self.classifier.tsv_bytes(res, rws)
+        rws, tsv = [], b""
+        if self.classifier is not None:
+            res = self.classifier.run(table, comm=self.comm)
+            rws = self.classifier.rows(res)
+            if multi:
+                rws = gather_rows(self.comm, rws, part, gid)
+            tsv = self.classifier.tsv_bytes(res, rws)
+        n_rows = len(rws)
+        if multi:
+            n_rows = self.comm.broadcast_obj(n_rows)
+        if n_rows < 1:  # fewer than 2 TSV lines: run_hymet_cami.sh:182-206
+            tsv = self._fallback(table, part, gid)
+            rws = []
         return RunResult(selected, rows, thr, tsv, len(rws), sum(1 for r in rws if r[1] != "Unknown"), table.n_lines, text)
+
+    def _fallback(self, table, part, gid) -> bytes:
+        """build_id_map + mini_classify over the PAF lines (first mapped hit per query), then
+        the awk rewrite; dies like the script when even that leaves no row."""
+        from . import fallback
+        pairs = [(table.queries[int(a)], table.targets[int(b)]) for a, b in zip(table.line_q, table.line_t)]
+        if self.comm is not None and self.comm.world > 1:
+            # lines of a query sit together per part; queries sort by (part, input index)
+            key = {table.queries[i]: (int(part[i]), int(gid[i])) for i in range(len(table.queries))}
+            got = self.comm.gather_obj([(key[a], j, a, b) for j, (a, b) in enumerate(pairs)])
+            if self.comm.rank != 0:
+                return b""
+            pairs = [(a, b) for _, _, a, b in sorted(x for g in got for x in g)]
+        tsv = fallback.fallback_tsv(pairs, self.taxonomy)
+        if tsv.count(b"\n") < 2:
+            raise RuntimeError("classification still empty after fallback")  # run_hymet_cami.sh:205
+        return tsv
 
 
 def gather_rows(comm, rows, part: np.ndarray, qid: np.ndarray, dst: int = 0):

@@ -59,8 +59,9 @@ def _bc(d: Decimal) -> str:
     return s[1:] if s.startswith("0.") else s
 
 
-def select_threshold(rows: Sequence[str], initial: str = "0.9", n_files: int = 1) -> Tuple[str, List[str], List[str]]:
-    """Returns (threshold as printed, top-hit rows, selected names = cut -f5)."""
+def threshold_walk(rows: Sequence[str], initial: str = "0.9", n_files: int = 1):
+    """scripts/mash.sh:23-55.  Returns (threshold as printed, top-hit rows, selected names =
+    cut -f5, the script's stdout lines from the walk on)."""
     vals = []
     for r in rows:
         f = r.split()
@@ -70,17 +71,30 @@ def select_threshold(rows: Sequence[str], initial: str = "0.9", n_files: int = 1
             vals.append(0.0)
     need = min_candidates(n_files)
     cur, cur_s = Decimal(initial), initial
-    best = "0.71"
+    best, found, count, log = "0.71", False, 0, []
     while cur >= Decimal("0.70"):
         t = float(cur_s)
-        if sum(v > t for v in vals) >= need:
-            best = cur_s
+        count = sum(v > t for v in vals)
+        log += [f"Testing threshold: {cur_s}", f"Candidates found: {count}"]      # mash.sh:35-36
+        if count >= need:
+            best, found = cur_s, True
             break
         cur -= Decimal("0.02")
         cur_s = _bc(cur)
     t = float(best)
     top = [r for r, v in zip(rows, vals) if v > t]
+    if not found:
+        count = len(top)
+        log.append("No suitable threshold found. Using 0.70.")                     # mash.sh:47-51
+    log += ["====================================", f"Final threshold used: {best}", f"Candidates found: {count}",
+            "===================================="]
     names = [(r.split("\t") + [""] * 5)[4] for r in top]
+    return best, top, names, log
+
+
+def select_threshold(rows: Sequence[str], initial: str = "0.9", n_files: int = 1) -> Tuple[str, List[str], List[str]]:
+    """Returns (threshold as printed, top-hit rows, selected names = cut -f5)."""
+    best, top, names, _ = threshold_walk(rows, initial, n_files)
     return best, top, names
 
 

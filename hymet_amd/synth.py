@@ -85,8 +85,10 @@ class Workload:
 
 def make_cami(rng, n_taxa=12, per_taxon=62, genome_mbp=(3.0, 5.0), div=(0.005, 0.04), contig_gbp=1.0,
               max_contigs=None, name="cami-medium", contig_rng=None) -> Workload:
-    """contig_rng: separate generator for the contigs (per-rank samples of one community)."""
+    """contig_rng: separate generator for the contigs (per-rank samples of one community).
+    per_taxon: candidate genomes per taxon (an int, or one count per taxon)."""
     taxa = [f"Species{chr(65 + t)} synthetica" for t in range(n_taxa)]
+    per = list(per_taxon) if hasattr(per_taxon, "__len__") else [int(per_taxon)] * n_taxa
     ref_names, ref_taxon, ref_strain, refs = [], [], [], []
     sample = []
     for t in range(n_taxa):
@@ -94,7 +96,7 @@ def make_cami(rng, n_taxa=12, per_taxon=62, genome_mbp=(3.0, 5.0), div=(0.005, 0
         backbone = random_codes(rng, L)
         strain = mutate_codes(rng, backbone, 0.01)          # the organism actually sampled
         sample.append(strain)
-        for s in range(per_taxon):
+        for s in range(per[t]):
             r = float(rng.uniform(*div))
             g = mutate_codes(rng, strain, r)
             acc = f"GCF_{(t * 1000 + s) * 7919 % 999999937:09d}.1"

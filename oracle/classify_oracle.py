@@ -191,11 +191,15 @@ def weighted_lca_cami(tw, hier):  # classification_cami.py:251-288
     return lin, RANKS[len(chosen) - 1], min(conf, 1.0)
 
 
-def classify_cami(paf, taxonomy, hierarchy):
-    """Return the exact TSV bytes classification_cami.py writes (:333-339)."""
+def classify_cami(paf, taxonomy, hierarchy, ref_counts=None):
+    """Return the exact TSV bytes classification_cami.py writes (:333-339).  ref_counts
+    (target -> PAF line count) replaces the file's own counts when the PAF is a sample of a
+    larger run (bench.py's CPU leg: ref_abundance is global over the whole PAF)."""
     tax = load_taxonomy_cami(taxonomy)
     hier = load_hierarchy_cami(hierarchy)
     qmap, counts = parse_paf_cami(paf)
+    if ref_counts is not None:
+        counts = ref_counts
     tcache = {}
     buf = io.StringIO(newline="")
     w = csv.writer(buf, delimiter="\t")

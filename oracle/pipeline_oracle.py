@@ -64,8 +64,11 @@ def split_parts(lengths, batch=2e9, mini=50e6):
     return parts
 
 
-def map_paf(ref_names, ref_seqs, queries, part_bases=2e9, mini_batch=50e6):
-    """minimap2 -I<part_bases> -d ; minimap2 -x asm10 : PAF lines in minimap2's order."""
+def map_paf(ref_names, ref_seqs, queries, part_bases=2e9, mini_batch=50e6, threads=1):
+    """minimap2 -I<part_bases> -d ; minimap2 -x asm10 : PAF lines in minimap2's order.
+    threads > 1 maps queries concurrently (the C mapper releases the GIL; its state is
+    per call), then emits them in input order like minimap2's ordered output."""
+    from concurrent.futures import ThreadPoolExecutor
     lens = [len(s) for s in ref_seqs]
     parts = split_parts(lens, part_bases, mini_batch)
     out = []
@@ -75,17 +78,28 @@ def map_paf(ref_names, ref_seqs, queries, part_bases=2e9, mini_batch=50e6):
         if opt is None:
             opt = oracle_lib.asm10_opt()
             oracle_lib._mm_lib().mmo_opt_update_mid_occ(ctypes.byref(opt), idx.h)
-        for qn, qs in queries:
+
+        def one(q):
+            qn, qs = q
             regs, rl = oracle_lib.mm_map(idx, opt, qs, qn)
-            out.extend(oracle_lib.format_paf(qn, len(qs), regs, rl, idx.names, idx.lens))
+            return oracle_lib.format_paf(qn, len(qs), regs, rl, idx.names, idx.lens)
+
+        if threads > 1:
+            with ThreadPoolExecutor(threads) as ex:
+                for lines in ex.map(one, queries, chunksize=16):
+                    out.extend(lines)
+        else:
+            for q in queries:
+                out.extend(one(q))
     return out
 
 
-def run(queries, dbs, ref_lookup, taxonomy, hierarchy, thresh="0.9", cand_max=5000, part_bases=2e9, mini_batch=50e6):
+def run(queries, dbs, ref_lookup, taxonomy, hierarchy, thresh="0.9", cand_max=5000, part_bases=2e9, mini_batch=50e6,
+        threads=1):
     """queries: list of (name, seq bytes).  Returns (selected, paf lines, tsv bytes)."""
     selected, _ = select([q[1] for q in queries], dbs, thresh, cand_max)
     names, seqs = ref_lookup(selected)
-    paf = map_paf(names, seqs, queries, part_bases, mini_batch)
+    paf = map_paf(names, seqs, queries, part_bases, mini_batch, threads)
     with tempfile.TemporaryDirectory() as td:
         p = os.path.join(td, "resultados.paf")
         with open(p, "w") as f:

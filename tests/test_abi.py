@@ -39,3 +39,11 @@ def test_error_path_without_gpu():
     else:
         lib.hymet_destroy(h)
     assert lib.hymet_version() >= 1
+
+
+def test_library_is_built_from_these_sources():
+    """The shipped libhymet_gpu.so carries the digest of the sources, headers and compile
+    commands it was linked from (hymet_amd/build.py); a stale prebuilt library fails here,
+    on the build host and on the GPU box alike."""
+    from hymet_amd import build
+    assert build.is_current(), "libhymet_gpu.so is stale: run python -m hymet_amd.build"

@@ -38,7 +38,27 @@ def test_selection_text_stages_match_oracle():
         assert a == b
         init = rng.choice(["0.9", "0.90", "0.8", "0.95"])
         nf = rng.randrange(1, 4)
-        t1, top1, n1 = sel.select_threshold(a, init, nf)
-        t2, top2, n2, _ = so.select_threshold(b, init, nf)
+        t1, top1, n1, log1 = sel.threshold_walk(a, init, nf)
+        t2, top2, n2, trace = so.select_threshold(b, init, nf)
         assert (t1, top1, n1) == (t2, top2, n2)
+        # mash.sh's stdout from the walk on: one Testing/Candidates pair per threshold tried
+        # (:35-36), the fallback note (:50), the summary (:57-60)
+        exp = [l for t, c in trace for l in (f"Testing threshold: {t}", f"Candidates found: {c}")]
+        found = bool(trace) and trace[-1][1] >= sel.min_candidates(nf)
+        if not found:
+            exp.append("No suitable threshold found. Using 0.70.")
+        exp += ["=" * 36, f"Final threshold used: {t2}", f"Candidates found: {trace[-1][1] if found else len(top2)}", "=" * 36]
+        assert log1 == exp
     assert sel.union_sorted(["b", "a"], ["B"]) == so.union_sorted(["b", "a"], ["B"])
+
+
+def test_threshold_walk_log_known_answer():
+    """scripts/mash.sh:32-60 on a table where 0.90 and 0.88 fail and .86 succeeds (bc prints .88)."""
+    rows = [f"0.87{i}\t900/1000\t1\t0\tG{i}\tc" for i in range(5)] + ["0.95\t990/1000\t3\t0\tTOP\tc"]
+    best, top, names, log = sel.threshold_walk(sel.sort_gr(rows), "0.9", 1)
+    assert best == ".86" and len(top) == 6 and names[0] == "TOP"
+    assert log[:6] == ["Testing threshold: 0.9", "Candidates found: 1", "Testing threshold: .88", "Candidates found: 1",
+                       "Testing threshold: .86", "Candidates found: 6"]
+    assert log[-3:-1] == ["Final threshold used: .86", "Candidates found: 6"]
+    best, top, _, log = sel.threshold_walk(rows[:2], "0.9", 1)
+    assert best == "0.71" and "No suitable threshold found. Using 0.70." in log and log[-2] == "Candidates found: 2"
