@@ -45,12 +45,11 @@ void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
 int hip_fail(hipError_t e, const char *what);
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
-// caching device allocator (ctx.cpp): size classes of a quarter octave, blocks are never given
-// back to the driver (hipMalloc/hipFree and the stream-ordered pool cost 0.1-0.4 s per large
-// block on this stack, at every mapping batch)
 // Caching device allocator for kernel scratch, keyed by (device, stream, size class): a
 // block released on a stream is reissued only to work queued behind it on the same stream.
 // Cached bytes are capped (HYMET_SCRATCH_CAP_GB, default 96); hymet_scratch_trim frees them.
+// (hipMalloc/hipFree and the stream-ordered pool cost 0.1-0.4 s per large block on this
+// stack, at every mapping batch, hence the cache.)
 hipError_t scratch_alloc(size_t bytes, hipStream_t stream, void **p, size_t *cls);
 void scratch_free(void *p, hipStream_t stream, size_t cls);
 }  // namespace hymet
