@@ -1,18 +1,21 @@
 #!/usr/bin/env python3
-"""Benchmark contract.
+"""Benchmark contract (DESIGN.md §5 Measurement).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cami-medium|screen]
 
-One step = one pass of the HYMET hot path (screen -> select -> limit -> map -> LCA -> TSV)
-over one batch of synthetic, HBM-resident input.  Default workload: CAMI-medium (C4,
-BASELINE.json configs[3]; it fits one MI355X): 12 taxa, ~1 Gbp of contigs per rank, 744
-candidate genomes (~3 Gbp, two -I2g index parts), a sketch1-sized DB (1e5 refs x 1000).
-The candidate-keyed index is built in the untimed cold run (run_hymet_cami.sh caches it the
-same way) and its time is reported separately.  Rank 0 prints ONE JSON line.
+One step = one pass of the HYMET hot path over one input, in the SURVEY.md §8(d) window:
+FASTA text in host memory -> record table -> host-to-device copy -> screen -> select ->
+limit -> map (both -I2g parts) -> LCA -> classified_sequences.tsv written (and the
+resultados.paf text emitted to host memory).  Default workload: CAMI-medium (C4,
+BASELINE.json configs[3]): 12 taxa, ~1 Gbp / ~151k contigs, 744 candidate genomes (~3 Gbp,
+two index parts), a sketch1-sized DB (1e5 refs x 1000 hashes).  The candidate-keyed index
+is built in the untimed cold run (run_hymet_cami.sh caches it the same way) and reported
+separately.  Rank 0 prints ONE JSON line.
 
-Multi-GPU (torch.distributed.run, one rank per GPU): every rank holds its own ~1 Gbp contig
-sample of the same community (weak scaling); screen counts and per-target PAF line counts
-are all-reduced over RCCL; rank 0 writes the TSV.
+Multi-GPU (torch.distributed.run, one rank per GPU): STRONG scaling -- every rank holds the
+same FASTA bytes and maps the contiguous record range FastaIndex.shard(rank, N); screen
+counts and per-target PAF line counts are all-reduced over RCCL, LCA row records are
+all-gathered and rank 0 writes the TSV.  value = all contigs / max-over-ranks step time.
 """
 from __future__ import annotations
 
@@ -70,16 +73,48 @@ def roofline_from_prof(prof, prefer=None):
             "kernel_avg_ms": ms / max(n, 1), "launches": n, "alg_bytes_per_launch": b / max(n, 1)}
 
 
+def path_roofline(prof, steps, step_s, L, K, P, n_parts, world, w=10):
+    """Whole-path roofline with SURVEY.md §8(d)'s algorithmic bytes per step:
+    screen 0.25 L + 8 K (packed read, one key probe per k-mer); map per index part
+    0.25 L + 8 M_q + 40 A (M_q = 2L/(w+1) minimizer lookups, A anchors: position fetch,
+    anchor write + read); classify 16 P.  A is counted by the anchor kernel's scope (20 B
+    per anchor, write_anchor_keys).  K_hit count updates and the once-per-run table build
+    are left out (not in a warm step)."""
+    A = prof.get("mm_anchors", (0.0, 0, 0.0))[2] / 20.0 / steps
+    Mq = 2.0 * L / (w + 1)
+    by = 0.25 * L + 8.0 * K + n_parts * (0.25 * L + 8.0 * Mq) + 40.0 * A + 16.0 * P
+    ach = by / step_s / 1e9
+    return {"bound": "hbm", "alg_bytes_per_step": by, "anchors_per_step": A, "achieved": ach,
+            "peak": HBM_PEAK_GBS * world, "unit": "GB/s", "frac": ach / (HBM_PEAK_GBS * world)}
+
+
+def cpu_info():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count() or 0
+
+
 # ------------------------------------------------------------------ CAMI-medium
 def build_cami(args, comm, gpu):
-    from hymet_amd import pipeline, screen as scr, synth
+    from hymet_amd import ingest, pipeline, screen as scr, synth
     from hymet_amd.msh import SketchDB
     from hymet_amd.seqio import DevicePool, from_records
     t0 = time.time()
+    # the same community and the same contig pool on every rank (strong scaling)
     w = synth.make_cami(np.random.default_rng(1234), n_taxa=args.taxa, per_taxon=args.per_taxon,
-                        contig_gbp=args.contig_gbp, contig_rng=np.random.default_rng(5000 + comm.rank))
-    log(f"synth: {len(w.refs)} refs {w.ref_bases/1e9:.2f} Gbp, {len(w.contigs)} contigs {w.contig_bases/1e6:.0f} Mbp "
-        f"({time.time()-t0:.1f}s)")
+                        contig_gbp=args.contig_gbp, contig_rng=np.random.default_rng(5000))
+    # MEGAHIT-style headers, as CAMI's assemblies carry them
+    heads = [f"{n} flag=1 multi={2 + i % 7}.0000 len={len(s)}" for i, (n, s) in enumerate(zip(w.contig_names, w.contigs))]
+    fasta = ingest.to_fasta(heads, w.contigs, width=args.fasta_width)
+    log(f"synth: {len(w.refs)} refs {w.ref_bases/1e9:.2f} Gbp, {len(w.contigs)} contigs {w.contig_bases/1e6:.0f} Mbp, "
+        f"FASTA {len(fasta)/1e6:.0f} MB ({time.time()-t0:.1f}s)")
     t0 = time.time()
     db_names = [n + ".fna.gz" for n in w.ref_names]
     refs_ss = from_records([(n, "", s) for n, s in zip(w.ref_names, w.refs)])
@@ -106,26 +141,23 @@ def build_cami(args, comm, gpu):
 
     cfg = pipeline.Config(map_batch_bases=int(args.batch_mbp * 1e6))
     pipe = pipeline.Pipeline(gpu, [db], ref_lookup, tax, hier, cfg, comm)
-    queries = from_records([(n, "", s) for n, s in zip(w.contig_names, w.contigs)])
-    t0 = time.time()
-    pq = pipe.prepare(queries)
-    gpu.sync()
-    log(f"queries resident: {len(pq.batches)} map batches ({time.time()-t0:.1f}s)")
-    return w, db, pipe, pq, refs_ss, tax, hier, by_name
+    return w, db, pipe, fasta, refs_ss, tax, hier, td
 
 
 def bench_cami(args, comm, gpu, torch):
-    w, db, pipe, pq, refs_ss, tax, hier, by_name = build_cami(args, comm, gpu)
+    from hymet_amd.ingest import FastaIndex
+    w, db, pipe, fasta, refs_ss, tax, hier, td = build_cami(args, comm, gpu)
+    tsv_path = os.path.join(td, "classified_sequences.tsv")
     comm.barrier()
     t0 = time.time()
-    res = pipe.run(pq)                      # cold: builds the candidate index (cached afterwards)
+    res = pipe.run(fasta)                   # cold: builds the candidate index (cached afterwards)
     gpu.sync()
     cold = time.time() - t0
     ix = pipe.index_for(res.selected)
     log(f"cold run {cold:.1f}s: {len(res.selected)} candidates, {len(ix.parts)} index parts, "
-        f"{res.n_classified}/{res.n_queries} classified, {res.n_paf_lines} PAF lines")
+        f"{res.n_classified}/{res.n_queries} classified, {res.n_paf_lines} PAF lines on rank 0")
     for _ in range(max(0, args.warmup - 1)):
-        pipe.run(pq)
+        pipe.run(fasta, with_paf=True)
     gpu.sync()
     comm.barrier()
     gpu.prof_reset()
@@ -139,7 +171,10 @@ def bench_cami(args, comm, gpu, torch):
         cp = cProfile.Profile()
         cp.enable()
     for _ in range(args.steps):
-        res = pipe.run(pq)
+        res = pipe.run(fasta, with_paf=True)        # FASTA bytes in host memory -> TSV + PAF text
+        if comm.rank == 0:
+            with open(tsv_path, "wb") as f:             # classified_sequences.tsv written
+                f.write(res.tsv)
     torch.cuda.synchronize()
     if prof_host:
         import io
@@ -152,55 +187,57 @@ def bench_cami(args, comm, gpu, torch):
     dt = comm.max_float(time.perf_counter() - t0)
     gpu.prof(False)
     prof = gpu.prof_table()
-    # Host-buffer boundary (the drop-in scripts read FASTA into host memory): re-time the
-    # ingest (host alphabet encode + PCIe upload of every pool) once, outside the timed
-    # region.  Reported beside `value` as the PCIe-inclusive rate; never `value` itself.
-    comm.barrier()
-    t_in = time.perf_counter()
-    pq_in = pipe.prepare(pq.queries)
-    torch.cuda.synchronize()
-    ingest_s = comm.max_float(time.perf_counter() - t_in)
-    del pq_in
-    n_contigs = comm.world * len(w.contigs)        # weak scaling: every rank its own sample
-    mbp = sum(comm.allgather_np(np.array([pq.queries.total_bases], np.int64)))[0] / 1e6
+    n_contigs = len(w.contigs)
+    total_bases = w.contig_bases
     step = dt / args.steps
+    kern_ms = sum(v[0] for k, v in prof.items() if "." not in k) / args.steps
     log("kernel time per step (ms): " + ", ".join(f"{k}={v[0]/args.steps:.1f}" for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])))
+    n_lines = sum(int(x[0]) for x in comm.allgather_np(np.array([res.n_paf_lines], np.int64)))
     out = {
         "metric": METRIC, "value": n_contigs / step, "unit": "contigs/s", "n_gpus": comm.world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": step * 1e3, "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": step * 1e3, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-        "mbp_per_s": mbp / step,
-        "config": {"workload": f"CAMI-medium (C4): {args.taxa} taxa, {len(w.contigs)} contigs / {pq.queries.total_bases/1e6:.0f} Mbp "
-                               f"per rank; {len(res.selected)} candidates / {refs_ss.total_bases/1e9:.2f} Gbp in {len(ix.parts)} "
-                               f"-I2g parts; sketch DB {db.n_refs} refs x 1000",
-                   "global_contigs": n_contigs, "parallelism": f"contig-shard x{comm.world}"},
+        "mbp_per_s": total_bases / 1e6 / step,
+        "config": {"workload": f"CAMI-medium (C4): {args.taxa} taxa, {n_contigs} contigs / {total_bases/1e6:.0f} Mbp FASTA "
+                               f"({len(fasta)/1e6:.0f} MB) sharded over {comm.world} GPU(s); {len(res.selected)} candidates / "
+                               f"{refs_ss.total_bases/1e9:.2f} Gbp in {len(ix.parts)} -I2g parts; sketch DB {db.n_refs} refs x 1000",
+                   "global_contigs": n_contigs, "parallelism": f"contig-shard x{comm.world}",
+                   "window": "FASTA bytes in host memory -> classified_sequences.tsv written + resultados.paf text in host "
+                             "memory (ingest, H2D, screen, select, limit, map, LCA, text emit inside every step)"},
         "cold_run_s": cold,
-        "ingest_ms": ingest_s * 1e3,
-        "pcie_inclusive_contigs_per_s": n_contigs / (step + ingest_s),
+        "paf_lines": n_lines,
+        "kernel_ms_per_step_rank0": kern_ms,
         "stage_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
         "roofline": roofline_from_prof(prof),
+        "path_roofline": path_roofline(prof, args.steps, step, total_bases, total_bases, n_lines, len(ix.parts), comm.world),
     }
     if comm.rank == 0 and not args.no_cpu:
         try:
-            out["cpu_baseline"] = cpu_baseline_cami(args, gpu, pipe, pq, db, res, w, tax, hier)
+            out["cpu_baseline"] = cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier)
         except Exception as e:  # the baseline is informative; never lose the GPU line
+            import traceback
+            traceback.print_exc()
             out["cpu_baseline"] = {"error": repr(e)}
     return out
 
 
-def cpu_baseline_cami(args, gpu, pipe, pq, db, res, w, tax, hier, budget_s=20.0):
+def cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier, budget_s=20.0):
     """The CPU oracle restatement on a bounded sample of the same workload, on the host's
-    cores: worker threads take 8-contig batches of a random rank-0 sample and run minimap2
-    asm10 against the same candidate index parts (exported from the device index,
-    content-identical to the oracle's own per tests/test_mm_index_gpu.py; the C mapper
-    releases the GIL) and the classification_cami restatement; then the contigs done are
-    screened in one run (Mash screens the pooled input once: its per-run O(H) statistics
-    pass over the 1e8-hash DB would dominate if paid per batch).  One-time table/index builds
-    are excluded, like the warm GPU step."""
+    cores, CHECKED against the GPU run: worker threads take 8-contig batches of a random
+    sample and run the minimap2 asm10 restatement against the same candidate index parts
+    (exported from the device index, content-identical to the oracle's own build per
+    tests/test_mm_index_gpu.py; the C mapper releases the GIL), then the sampled contigs are
+    screened in one oracle run (Mash screens the pooled input once) and classified by the
+    classification_cami restatement with the run's global ref_abundance (the per-target
+    line counts of the whole PAF, classification_cami.py:181-208).  The sample's PAF lines
+    and TSV rows must equal the GPU's for the same contigs (single GPU)."""
     import threading
     from concurrent.futures import ThreadPoolExecutor
+    from hymet_amd.ingest import FastaIndex
     from oracle import classify_oracle, oracle_lib
     t0 = time.time()
+    fx = FastaIndex(fasta)
+    names = fx.names()
     so = oracle_lib.ScreenOracle(db)
     ix = pipe.index_for(res.selected)
     parts = []
@@ -210,13 +247,17 @@ def cpu_baseline_cami(args, gpu, pipe, pq, db, res, w, tax, hier, budget_s=20.0)
         n = len(part.names)
         parts.append(oracle_lib.mm_index_from_arrays(hs, pos, ix.lens[first:first + n], ix.names[first:first + n]))
     opt = oracle_lib.asm10_opt()
-    opt.mid_occ = pipe.opt.mid_occ
+    opt.mid_occ = ix.opt.mid_occ
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     log(f"cpu baseline setup {time.time()-t0:.1f}s, {threads} threads")
-    qs = pq.queries
-    order = [int(q) for q in np.random.default_rng(7).permutation(qs.n)]
+    d = fasta
+
+    def seq(i):
+        return d[fx.seq_off[i]:fx.seq_end[i]].replace(b"\n", b"").replace(b"\r", b"")
+
+    order = [int(q) for q in np.random.default_rng(7).permutation(fx.n)]
     lock = threading.Lock()
-    state = {"next": 0, "contigs": 0, "bases": 0, "done": []}
+    state = {"next": 0, "contigs": 0, "bases": 0, "done": [], "paf": {}}
     t_start = time.perf_counter()
 
     def worker(_):
@@ -227,32 +268,60 @@ def cpu_baseline_cami(args, gpu, pipe, pq, db, res, w, tax, hier, budget_s=20.0)
             batch = order[b0:b0 + 8]
             if not batch:
                 return
-            seqs = [(qs.names[i], qs.seq(i)) for i in batch]
-            paf = []
+            seqs = [(names[i], seq(i)) for i in batch]
+            got = {}
             for p in parts:                                               # map, part-major
                 for name, s in seqs:
                     regs, rl = oracle_lib.mm_map(p, opt, s, name)
-                    paf.extend(oracle_lib.format_paf(name, len(s), regs, rl, p.names, p.lens))
-            fd, path = tempfile.mkstemp(suffix=".paf")
-            os.write(fd, "".join(l + "\n" for l in paf).encode())
-            os.close(fd)
-            classify_oracle.classify_cami(path, tax, hier)                 # classify
-            os.unlink(path)
+                    got.setdefault(name, []).extend(oracle_lib.format_paf(name, len(s), regs, rl, p.names, p.lens))
             with lock:
                 state["contigs"] += len(batch)
                 state["bases"] += sum(len(s) for _, s in seqs)
                 state["done"].extend(batch)
+                state["paf"].update(got)
 
     with ThreadPoolExecutor(threads) as ex:
         list(ex.map(worker, range(threads)))
-    so.run([qs.seq(i) for i in state["done"]])                              # screen, one pooled run
+    done = state["done"]
+    so.run([seq(i) for i in done])                                           # screen, one pooled run
+    # classify the sample's lines with the run's global per-target line counts
+    q, part, t = pipe.acc.columns()
+    ref_counts = dict(zip(ix.names, np.bincount(t, minlength=len(ix.names)).tolist()))
+    fd, path = tempfile.mkstemp(suffix=".paf")
+    sample_names = [names[i] for i in done]
+    paf_lines = [l for nm in sample_names for l in state["paf"].get(nm, [])]
+    os.write(fd, "".join(l + "\n" for l in paf_lines).encode())
+    os.close(fd)
+    o_tsv = classify_oracle.classify_cami(path, tax, hier, ref_counts=ref_counts)
+    os.unlink(path)
     dt = time.perf_counter() - t_start
-    return {"value": state["contigs"] / dt, "unit": "contigs/s", "cores": threads, "kind": "port",
-            "mbp_per_s": state["bases"] / 1e6 / dt,
-            "sample": f"{state['contigs']} random contigs / {state['bases']/1e6:.2f} Mbp of the rank-0 pool on {threads} "
-                      f"threads: oracle minimap2 asm10 vs the same {len(ix.parts)} index parts + classification_cami "
-                      f"restatement, then one oracle screen run over those contigs (prebuilt table, {db.n_refs} refs), "
-                      f"{dt:.1f}s"}
+    # check against the GPU run of the same contigs
+    want = set(sample_names)
+    g_paf = {}
+    for line in res.paf_bytes.decode().split("\n"):
+        nm = line.split("\t", 1)[0]
+        if nm in want:
+            g_paf.setdefault(nm, []).append(line)
+    paf_ok = sum(1 for nm in sample_names if g_paf.get(nm, []) == state["paf"].get(nm, []))
+    g_rows = {}
+    for row in res.tsv.decode().split("\r\n")[1:]:
+        nm = row.split("\t", 1)[0]
+        if nm in want:
+            g_rows[nm] = row
+    o_rows = {r.split("\t", 1)[0]: r for r in o_tsv.decode().split("\r\n")[1:] if r}
+    tsv_ok = sum(1 for nm in sample_names if g_rows.get(nm) == o_rows.get(nm))
+    model, ncpu = cpu_info()
+    out = {"value": state["contigs"] / dt, "unit": "contigs/s", "cores": threads, "kind": "port",
+           "mbp_per_s": state["bases"] / 1e6 / dt, "cpu_model": model, "nproc": ncpu,
+           "checked": {"contigs": len(done), "paf_identical": paf_ok, "tsv_rows_identical": tsv_ok,
+                       "paf_lines": len(paf_lines)},
+           "sample": f"{state['contigs']} random contigs / {state['bases']/1e6:.2f} Mbp on {threads} threads: oracle "
+                     f"minimap2 asm10 vs the same {len(ix.parts)} index parts, one oracle screen run over those contigs "
+                     f"(prebuilt table, {db.n_refs} refs), classification_cami restatement with the run's global "
+                     f"ref_abundance, {dt:.1f}s"}
+    if paf_ok != len(done) or tsv_ok != len(done):
+        out["error"] = "GPU output differs from the oracle on the sampled contigs"
+    return out
 
 
 # ------------------------------------------------------------------- screen only
@@ -300,13 +369,14 @@ def bench_screen(args, comm, gpu, torch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="cami-medium", choices=["cami-medium", "screen"])
     ap.add_argument("--contig-gbp", type=float, default=1.0)
     ap.add_argument("--taxa", type=int, default=12)
     ap.add_argument("--per-taxon", type=int, default=62)
     ap.add_argument("--batch-mbp", type=float, default=40.0)
+    ap.add_argument("--fasta-width", type=int, default=0, help="FASTA line width (0: one line per contig, as MEGAHIT)")
     ap.add_argument("--screen-refs", type=int, default=100_000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16, help="CPU baseline threads (the GPU box's CPU share is 16)")

@@ -29,6 +29,10 @@ _SIGS = {
     "hymet_scratch_trim": (_i32, [_vp, _c.POINTER(_i64)]),
     "hymet_scratch_cached": (_i32, [_vp, _c.POINTER(_i64)]),
     "hymet_pack": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "hymet_fasta_index": (_i32, [_vp, _i64, _i32, _i64, _c.POINTER(_i64), _vp, _vp, _vp, _vp, _vp]),
+    "hymet_fasta_names": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
+    "hymet_fasta_compact": (_i32, [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp]),
+    "hymet_name_hash": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp]),
     "hymet_screen_table_slots": (_i64, [_i64]),
     "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
     "hymet_screen_count": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _u32, _i32, _c.POINTER(_vp), _c.POINTER(_i64),
@@ -44,6 +48,17 @@ _SIGS = {
     "hymet_mm_result_size": (_i32, [_vp, _c.POINTER(_i64)]),
     "hymet_mm_result_copy": (_i32, [_vp, _vp, _vp, _vp]),
     "hymet_mm_result_destroy": (_i32, [_vp]),
+    "hymet_paf_acc_create": (_i32, [_vp, _c.POINTER(_vp)]),
+    "hymet_paf_acc_reset": (_i32, [_vp]),
+    "hymet_paf_acc_destroy": (_i32, [_vp]),
+    "hymet_paf_acc_info": (_i32, [_vp, _c.POINTER(_i64), _c.POINTER(_vp), _c.POINTER(_vp), _c.POINTER(_vp),
+                                  _c.POINTER(_vp), _c.POINTER(_vp)]),
+    "hymet_paf_acc_copy": (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    "hymet_mm_map_acc": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
+    "hymet_emit_paf": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _c.POINTER(_i64), _vp]),
+    "hymet_acc_ref_counts": (_i32, [_vp, _vp, _vp]),
+    "hymet_acc_classify": (_i32, [_vp, _vp, _i32, _i32] + [_vp] * 15 + [_c.POINTER(_i32)]),
+    "hymet_emit_tsv": (_i32, [_vp, _i32, _i32] + [_vp] * 15 + [_i64, _c.POINTER(_i64)]),
     "hymet_mm_chain_dp": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _c.c_float, _c.c_float, _vp, _vp]),
     "hymet_lca_ref_counts": (_i32, [_vp, _vp, _i64, _vp]),
     "hymet_lca": (_i32, [_vp, _i32, _i32] + [_vp] * 17),

@@ -273,6 +273,7 @@ class Classifier:
         self._tax_names: List[List[int]] = []
         self._in_hier: List[int] = []
         self._tcache: Dict[str, int] = {}
+        self._dev: Dict[str, object] = {}
 
     def _taxid_index(self, tid: str) -> int:
         i = self.tax_index.get(tid)
@@ -309,6 +310,40 @@ class Classifier:
                 self._tcache[t] = v
             out[k] = v
         return out
+
+    def device_tables(self, target_names: Optional[Sequence[str]]):
+        """The integer tables in HBM for the fused path: target -> taxid index for
+        `target_names` (the index set's targets, cached per list), taxid -> 8 label ids,
+        in-hierarchy flags, the label byte pool, and for the legacy variant each taxid's raw
+        lineage and determine_taxonomic_level string (the exact-match shortcut's output).
+        Rebuilt only when a new target list or new taxids / labels appear."""
+        torch = self.gpu.torch
+
+        def dev(a):
+            return torch.from_numpy(np.ascontiguousarray(a)).to(self.gpu.dev)
+
+        def pool(strs):
+            bs = [x.encode() for x in strs]
+            off = np.zeros(len(bs) + 1, np.int64)
+            np.cumsum([len(b) for b in bs], out=off[1:])
+            return dev(np.frombuffer(b"".join(bs) or b"\0", np.uint8).copy()), dev(off)
+
+        d = self._dev
+        if target_names is not None and d.get("targets_of") is not target_names:
+            t_tax = self.target_tax(list(target_names))
+            d["t_tax"] = dev(t_tax if len(t_tax) else np.full(1, -1, np.int32))
+            d["targets_of"] = target_names
+        sizes = (len(self.taxids), len(self.labels))
+        if d.get("sizes") != sizes:
+            d["tax_names"] = dev(np.array(self._tax_names if self._tax_names else [[-1] * 8], np.int32).reshape(-1))
+            d["in_hier"] = dev(np.array(self._in_hier if self._in_hier else [0], np.uint8))
+            d["label"], d["label_off"] = pool(self.labels)
+            if self.variant == LEGACY:
+                lins = [self.hier.rows.get(t, "") if h else "" for t, h in zip(self.taxids, self._in_hier)]
+                d["taxlin"], d["taxlin_off"] = pool(lins)
+                d["taxlvl"], d["taxlvl_off"] = pool([legacy_level(x) for x in lins])
+            d["sizes"] = sizes
+        return d
 
     def run(self, paf: PafTable, ref_counts: Optional[np.ndarray] = None, comm=None) -> LcaResult:
         gpu, torch = self.gpu, self.gpu.torch

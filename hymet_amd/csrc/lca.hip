@@ -15,6 +15,10 @@
 // lca_kernel: one thread per query, lines of the query in PAF order (CSR); insertion-ordered
 // "dicts" are arrays in a per-query scratch slice sized by its line count.
 #include "common.hpp"
+#include "mm_common.hpp"
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 namespace {
 
@@ -166,9 +170,204 @@ __global__ __launch_bounds__(64) void lca_kernel(LcaParams P) {
     }
 }
 
+// ---------------------------------------------------------------- accumulator path
+// The fused path's PAF never leaves HBM (hymet_paf_acc): rows (queries with >= 1 line) are
+// ordered by first appearance = (index part of the query's first line, query index), which
+// is the insertion order of classification_cami.py's query_map (:181-208, written :333-339)
+// for minimap2's part-major, query-ordered output; each row's lines keep PAF order.
+constexpr int32_t kNoPart = 0x7fffffff;
+
+__global__ void acc_first_kernel(const int32_t *q, const int32_t *part, int64_t n, int32_t *first_part, uint32_t *cnt) {
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= n) return;
+    atomicMin(&first_part[q[l]], part[l]);
+    atomicAdd(&cnt[q[l]], 1u);
+}
+
+__global__ void acc_keys_kernel(const int32_t *first_part, int32_t n_q, uint64_t *key, int32_t *n_rows) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n_q) return;
+    const int32_t p = first_part[q];
+    const bool none = p == kNoPart || p == 0x7f7f7f7f;
+    key[q] = none ? ~0ull : ((uint64_t)(uint32_t)p << 32 | (uint32_t)q);
+    if (!none) atomicAdd(n_rows, 1);
+}
+
+__global__ void acc_rows_kernel(const uint64_t *key, int32_t n_rows, const uint32_t *cnt, int32_t *row_q, int32_t *row_part,
+                                int32_t *row_of, uint32_t *row_cnt) {
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows) return;
+    const int32_t q = (int32_t)(uint32_t)key[r];
+    row_q[r] = q;
+    row_part[r] = (int32_t)(key[r] >> 32);
+    row_of[q] = r;
+    row_cnt[r] = cnt[q];
+}
+
+__global__ void acc_line_keys_kernel(const int32_t *q, int64_t n, const int32_t *row_of, uint32_t *key, uint32_t *val) {
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= n) return;
+    key[l] = (uint32_t)row_of[q[l]];
+    val[l] = (uint32_t)l;
+}
+
+struct AccLineParams {
+    const uint32_t *perm;         // CSR position -> accumulator line
+    int64_t n;
+    const hymet_mm_reg *regs;
+    const int32_t *q, *t;
+    const int64_t *qlen;          // per query
+    int mode;
+    const uint8_t *qname_pool;    // legacy exact test: query name == target name
+    const int64_t *qname_off;
+    const uint8_t *tname_pool;
+    const int64_t *tname_off;
+    int32_t *line_t;
+    int64_t *line_blen, *line_qlen;
+    uint8_t *line_exact;
+};
+
+__global__ void acc_line_gather_kernel(AccLineParams P) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    const uint32_t l = P.perm[i];
+    const int32_t q = P.q[l], t = P.t[l];
+    const int64_t bl = P.regs[l].blen, ql = P.qlen[q];
+    P.line_t[i] = t;
+    P.line_blen[i] = bl;
+    P.line_qlen[i] = ql;
+    uint8_t ex = 0;
+    if (P.mode == 1) {  // classification.py:52-53: query_id == ref_id and coverage >= 0.99
+        const int64_t a0 = P.qname_off[q], a1 = P.qname_off[q + 1], b0 = P.tname_off[t], b1 = P.tname_off[t + 1];
+        bool same = a1 - a0 == b1 - b0;
+        for (int64_t j = 0; same && j < a1 - a0; j++) same = P.qname_pool[a0 + j] == P.tname_pool[b0 + j];
+        const double cov = ql > 0 ? (double)bl / (double)ql : 0.0;
+        ex = same && cov >= 0.99;
+    }
+    P.line_exact[i] = ex;
+}
+
 }  // namespace
 
 extern "C" {
+
+int hymet_acc_ref_counts(hymet_ctx *ctx, const hymet_paf_acc *acc, int32_t *d_counts) {
+    HY_ARG(ctx && acc && d_counts, "hymet_acc_ref_counts: null argument");
+    if (acc->n <= 0) return HYMET_OK;
+    HY_HIP(hipSetDevice(ctx->device));
+    hymet::ProfScope _ps(ctx, "lca_refcount", 8.0 * (double)acc->n);
+    hipLaunchKernelGGL(lca_refcount_kernel, dim3((unsigned)hymet::cdiv(acc->n, 256)), dim3(256), 0, ctx->stream,
+                       acc->t.as<int32_t>(), acc->n, d_counts);
+    HY_CHECK_LAUNCH("lca_refcount_kernel");
+    return HYMET_OK;
+}
+
+int hymet_acc_classify(hymet_ctx *ctx, const hymet_paf_acc *acc, int mode, int32_t n_q, const int64_t *d_qlen,
+                       const int32_t *d_ref_counts, const int32_t *d_t_tax, const int32_t *d_tax_names,
+                       const uint8_t *d_tax_in_hier, const uint8_t *d_qname_pool, const int64_t *d_qname_off,
+                       const uint8_t *d_tname_pool, const int64_t *d_tname_off, int32_t *d_row_q, int32_t *d_row_part,
+                       int32_t *d_row_depth, int32_t *d_row_names, double *d_row_conf, int32_t *d_row_tax,
+                       int32_t *n_rows) {
+    using hymet::mm::DevBuf;
+    HY_ARG(ctx && acc && n_rows && d_qlen, "hymet_acc_classify: null argument");
+    HY_ARG(mode == 0 || mode == 1, "hymet_acc_classify: mode must be 0 (classification_cami) or 1 (classification)");
+    HY_ARG(mode == 0 || (d_qname_pool && d_qname_off && d_tname_pool && d_tname_off),
+           "hymet_acc_classify: the legacy exact-match test needs the query and target name pools");
+    *n_rows = 0;
+    const int64_t n = acc->n;
+    if (n_q <= 0 || n <= 0) return HYMET_OK;
+    HY_ARG(n < (int64_t)UINT32_MAX, "hymet_acc_classify: more than 2^32 PAF lines");
+    HY_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    hymet::ProfScope _ps(ctx, "lca_rows", 40.0 * (double)n);
+    DevBuf first, cnt, key, key2, nr;
+    HY_HIP(first.alloc(4 * (size_t)n_q, st));
+    HY_HIP(cnt.alloc(4 * (size_t)n_q, st));
+    HY_HIP(key.alloc(8 * (size_t)n_q, st));
+    HY_HIP(key2.alloc(8 * (size_t)n_q, st));
+    HY_HIP(nr.alloc(4, st));
+    HY_HIP(hipMemsetAsync(first.p, 0x7f, 4 * (size_t)n_q, st));  // 0x7f7f7f7f > any part id
+    HY_HIP(hipMemsetAsync(cnt.p, 0, 4 * (size_t)n_q, st));
+    HY_HIP(hipMemsetAsync(nr.p, 0, 4, st));
+    const unsigned gl = (unsigned)hymet::cdiv(n, 256), gq = (unsigned)hymet::cdiv(n_q, 256);
+    hipLaunchKernelGGL(acc_first_kernel, dim3(gl), dim3(256), 0, st, acc->q.as<int32_t>(), acc->part.as<int32_t>(), n,
+                       first.as<int32_t>(), cnt.as<uint32_t>());
+    HY_CHECK_LAUNCH("acc_first_kernel");
+    // 0x7f7f7f7f marks "no line": normalise to kNoPart inside the key kernel
+    hipLaunchKernelGGL(acc_keys_kernel, dim3(gq), dim3(256), 0, st, first.as<int32_t>(), n_q, key.as<uint64_t>(),
+                       nr.as<int32_t>());
+    HY_CHECK_LAUNCH("acc_keys_kernel");
+    {
+        size_t tb = 0;
+        HY_HIP(rocprim::radix_sort_keys(nullptr, tb, key.as<uint64_t>(), key2.as<uint64_t>(), (size_t)n_q, 0, 64, st));
+        DevBuf tmp;
+        HY_HIP(tmp.alloc(tb, st));
+        HY_HIP(rocprim::radix_sort_keys(tmp.p, tb, key.as<uint64_t>(), key2.as<uint64_t>(), (size_t)n_q, 0, 64, st));
+    }
+    int32_t R = 0;
+    HY_HIP(hipMemcpyAsync(&R, nr.p, 4, hipMemcpyDeviceToHost, st));
+    HY_HIP(hipStreamSynchronize(st));
+    *n_rows = R;
+    if (R == 0) return HYMET_OK;
+    DevBuf row_of, row_cnt, row_off, lk, lk2, lv, lv2, lt, lb, lq, le;
+    HY_HIP(row_of.alloc(4 * (size_t)n_q, st));
+    HY_HIP(row_cnt.alloc(4 * (size_t)(R + 1), st));
+    HY_HIP(row_off.alloc(8 * (size_t)(R + 1), st));
+    hipLaunchKernelGGL(acc_rows_kernel, dim3((unsigned)hymet::cdiv(R, 256)), dim3(256), 0, st, key2.as<uint64_t>(), R,
+                       cnt.as<uint32_t>(), d_row_q, d_row_part, row_of.as<int32_t>(), row_cnt.as<uint32_t>());
+    HY_CHECK_LAUNCH("acc_rows_kernel");
+    {
+        size_t tb = 0;
+        HY_HIP(rocprim::exclusive_scan(nullptr, tb, row_cnt.as<uint32_t>(), row_off.as<int64_t>(), (int64_t)0,
+                                       (size_t)R + 1, rocprim::plus<int64_t>(), st));
+        DevBuf tmp;
+        HY_HIP(tmp.alloc(tb, st));
+        HY_HIP(hipMemsetAsync(row_cnt.as<uint32_t>() + R, 0, 4, st));
+        HY_HIP(rocprim::exclusive_scan(tmp.p, tb, row_cnt.as<uint32_t>(), row_off.as<int64_t>(), (int64_t)0,
+                                       (size_t)R + 1, rocprim::plus<int64_t>(), st));
+    }
+    // lines grouped by row, PAF order kept inside a row (stable LSD sort by row)
+    HY_HIP(lk.alloc(4 * (size_t)n, st));
+    HY_HIP(lk2.alloc(4 * (size_t)n, st));
+    HY_HIP(lv.alloc(4 * (size_t)n, st));
+    HY_HIP(lv2.alloc(4 * (size_t)n, st));
+    hipLaunchKernelGGL(acc_line_keys_kernel, dim3(gl), dim3(256), 0, st, acc->q.as<int32_t>(), n, row_of.as<int32_t>(),
+                       lk.as<uint32_t>(), lv.as<uint32_t>());
+    HY_CHECK_LAUNCH("acc_line_keys_kernel");
+    int bits = 1;
+    while ((1ll << bits) < R) bits++;
+    {
+        size_t tb = 0;
+        HY_HIP(rocprim::radix_sort_pairs(nullptr, tb, lk.as<uint32_t>(), lk2.as<uint32_t>(), lv.as<uint32_t>(),
+                                         lv2.as<uint32_t>(), (size_t)n, 0, bits, st));
+        DevBuf tmp;
+        HY_HIP(tmp.alloc(tb, st));
+        HY_HIP(rocprim::radix_sort_pairs(tmp.p, tb, lk.as<uint32_t>(), lk2.as<uint32_t>(), lv.as<uint32_t>(),
+                                         lv2.as<uint32_t>(), (size_t)n, 0, bits, st));
+    }
+    HY_HIP(lt.alloc(4 * (size_t)n, st));
+    HY_HIP(lb.alloc(8 * (size_t)n, st));
+    HY_HIP(lq.alloc(8 * (size_t)n, st));
+    HY_HIP(le.alloc((size_t)n, st));
+    AccLineParams A{lv2.as<uint32_t>(), n, acc->regs.as<hymet_mm_reg>(), acc->q.as<int32_t>(), acc->t.as<int32_t>(), d_qlen,
+                    mode, d_qname_pool, d_qname_off, d_tname_pool, d_tname_off, lt.as<int32_t>(), lb.as<int64_t>(),
+                    lq.as<int64_t>(), le.as<uint8_t>()};
+    hipLaunchKernelGGL(acc_line_gather_kernel, dim3(gl), dim3(256), 0, st, A);
+    HY_CHECK_LAUNCH("acc_line_gather_kernel");
+    DevBuf s_tid, s_w, s_nm, s_nw;
+    HY_HIP(s_tid.alloc(4 * (size_t)n, st));
+    HY_HIP(s_w.alloc(8 * (size_t)n, st));
+    HY_HIP(s_nm.alloc(4 * (size_t)n, st));
+    HY_HIP(s_nw.alloc(8 * (size_t)n, st));
+    HY_HIP(hipMemsetAsync(d_row_names, 0, 4 * 8 * (size_t)R, st));
+    LcaParams P{mode,          R,               row_off.as<int64_t>(), lt.as<int32_t>(),   lb.as<int64_t>(),
+                lq.as<int64_t>(), le.as<uint8_t>(), d_ref_counts,      d_t_tax,            d_tax_names,
+                d_tax_in_hier, s_tid.as<int32_t>(), s_w.as<double>(),  s_nm.as<int32_t>(), s_nw.as<double>(),
+                d_row_depth,   d_row_names,     d_row_conf,            d_row_tax};
+    hipLaunchKernelGGL(lca_kernel, dim3((unsigned)hymet::cdiv(R, 64)), dim3(64), 0, st, P);
+    HY_CHECK_LAUNCH("lca_kernel");
+    return HYMET_OK;
+}
 
 int hymet_lca_ref_counts(hymet_ctx *ctx, const int32_t *d_line_t, int64_t n_lines, int32_t *d_counts) {
     HY_ARG(ctx && (n_lines == 0 || (d_line_t && d_counts)), "hymet_lca_ref_counts: null argument");

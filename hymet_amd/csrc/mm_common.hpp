@@ -117,3 +117,17 @@ struct hymet_mm_index {
     std::vector<int64_t> h_len;
     int device = 0;
 };
+
+// Device-resident PAF lines of a whole run (include/hymet_gpu.h hymet_paf_acc): every
+// hymet_mm_map_acc call appends its batch's lines, so the buffer holds resultados.paf's
+// lines in minimap2's order (index part by part, queries in input order, regions by score)
+// as records -- the classifier and the PAF text writer read them in place.
+struct hymet_paf_acc {
+    int device = 0;
+    int64_t n = 0, cap = 0;
+    hymet::mm::DevBuf regs;  // hymet_mm_reg per line
+    hymet::mm::DevBuf q;     // int32 query index in the run
+    hymet::mm::DevBuf part;  // int32 index part
+    hymet::mm::DevBuf rl;    // int32 rep_len of the line's query in that part (rl:i tag)
+    hymet::mm::DevBuf t;     // int32 target index in the run (part's first target + rid)
+};

@@ -1147,6 +1147,39 @@ __global__ __launch_bounds__(256) void rechain_keys_kernel(const uint64_t *bx, c
     val[a] = (uint32_t)by[i];
 }
 
+// per query: regions kept (first-pass chains, or the long-join re-chain's for flagged queries)
+__global__ void reg_count_kernel(const uint32_t *flag, const int32_t *n1, const int32_t *n2, int n_q, uint32_t *cnt) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n_q) cnt[q] = (uint32_t)((flag && flag[q]) ? n2[q] : n1[q]);
+}
+
+// one thread per query: copy its region records to their PAF positions (+ line metadata)
+struct RegOut {
+    hymet_mm_reg *regs;
+    int32_t *q, *part, *rl, *t;  // optional (accumulator sink)
+    int32_t q_base, part_id, t_base;
+};
+__global__ void reg_gather_kernel(const uint32_t *flag, const int32_t *n1, const int32_t *n2, const int64_t *qc1,
+                                  const int64_t *qc2, const hymet_mm_reg *r1, const hymet_mm_reg *r2, const int64_t *off,
+                                  const int32_t *rep_len, int n_q, RegOut o) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n_q) return;
+    const bool use2 = flag && flag[q];
+    const hymet_mm_reg *src = use2 ? r2 + qc2[q] : r1 + qc1[q];
+    const int nr = use2 ? n2[q] : n1[q];
+    const int64_t d = off[q];
+    for (int i = 0; i < nr; i++) {
+        const hymet_mm_reg r = src[i];
+        o.regs[d + i] = r;
+        if (o.q) {
+            o.q[d + i] = o.q_base + q;
+            o.part[d + i] = o.part_id;
+            o.rl[d + i] = rep_len[q];
+            o.t[d + i] = o.t_base + r.rid;
+        }
+    }
+}
+
 __global__ void qlen_sizes_kernel(const int64_t *off, int n_q, const uint32_t *flag, uint32_t *sz) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q < n_q) sz[q] = flag[q] ? (uint32_t)(off[q + 1] - off[q]) : 0u;
@@ -1158,22 +1191,56 @@ __global__ void qlen_sizes_kernel(const int64_t *off, int n_q, const uint32_t *f
 using namespace hymet;
 using namespace hymet::mm;
 
-extern "C" {
+// where hymet_mm_map puts a batch's PAF records: host vectors (hymet_mm_result) or the
+// device-resident accumulator of a run (hymet_paf_acc)
+struct MapSink {
+    hymet_mm_result *res = nullptr;
+    hymet_paf_acc *acc = nullptr;
+    int32_t q_base = 0, part_id = 0, t_base = 0;
+};
 
-int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *opt, const uint32_t *d_2b,
-                 const uint32_t *d_mask, const int64_t *h_starts, const int64_t *h_lens, const uint32_t *h_name_hash,
-                 int32_t n_q, hymet_mm_result **out) {
+static int acc_reserve(hymet_ctx *ctx, hymet_paf_acc *a, int64_t need) {
+    if (need <= a->cap) return HYMET_OK;
+    const int64_t cap = std::max<int64_t>(need, std::max<int64_t>(a->cap * 3 / 2, 1 << 16));
+    hipStream_t st = ctx->stream;
+    DevBuf nregs, nq, npart, nrl, nt;
+    HY_HIP(nregs.alloc(sizeof(hymet_mm_reg) * (size_t)cap, st));
+    HY_HIP(nq.alloc(4 * (size_t)cap, st));
+    HY_HIP(npart.alloc(4 * (size_t)cap, st));
+    HY_HIP(nrl.alloc(4 * (size_t)cap, st));
+    HY_HIP(nt.alloc(4 * (size_t)cap, st));
+    if (a->n) {
+        HY_HIP(hipMemcpyAsync(nregs.p, a->regs.p, sizeof(hymet_mm_reg) * (size_t)a->n, hipMemcpyDeviceToDevice, st));
+        HY_HIP(hipMemcpyAsync(nq.p, a->q.p, 4 * (size_t)a->n, hipMemcpyDeviceToDevice, st));
+        HY_HIP(hipMemcpyAsync(npart.p, a->part.p, 4 * (size_t)a->n, hipMemcpyDeviceToDevice, st));
+        HY_HIP(hipMemcpyAsync(nrl.p, a->rl.p, 4 * (size_t)a->n, hipMemcpyDeviceToDevice, st));
+        HY_HIP(hipMemcpyAsync(nt.p, a->t.p, 4 * (size_t)a->n, hipMemcpyDeviceToDevice, st));
+    }
+    a->regs.swap(nregs);
+    a->q.swap(nq);
+    a->part.swap(npart);
+    a->rl.swap(nrl);
+    a->t.swap(nt);
+    a->cap = cap;
+    return HYMET_OK;
+}
+
+static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *opt, const uint32_t *d_2b,
+                       const uint32_t *d_mask, const int64_t *h_starts, const int64_t *h_lens, const uint32_t *h_name_hash,
+                       const uint32_t *d_name_hash, int32_t n_q, MapSink &sink) {
     CallTrace call_trace;
-    HY_ARG(ctx && idx && opt && d_2b && d_mask && out, "hymet_mm_map: null argument");
+    HY_ARG(ctx && idx && opt && d_2b && d_mask, "hymet_mm_map: null argument");
     HY_ARG(n_q >= 0, "hymet_mm_map: n_q < 0");
+    HY_ARG(h_name_hash || d_name_hash, "hymet_mm_map: no query name hashes");
     HY_ARG(opt->mid_occ > 0, "hymet_mm_map: opt->mid_occ must be resolved (hymet_mm_index_max_occ + clamps)");
     HY_HIP(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    hymet_mm_result *res = new hymet_mm_result();
-    res->n_q = n_q;
-    res->reg_off.assign(n_q + 1, 0);
-    res->rep_len.assign(n_q, 0);
-    *out = res;
+    hymet_mm_result *res = sink.res;
+    if (res) {
+        res->n_q = n_q;
+        res->reg_off.assign(n_q + 1, 0);
+        res->rep_len.assign(n_q, 0);
+    }
     if (n_q == 0) return HYMET_OK;
     const int k = idx->k, w = idx->w;
     const float pen_gap = (float)(opt->chain_gap_scale * 0.01 * k);
@@ -1189,7 +1256,10 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
     HY_HIP(d_qlen.alloc(8 * (size_t)n_q, st));
     HY_HIP(d_hash.alloc(4 * (size_t)n_q, st));
     HY_HIP(hipMemcpyAsync(d_qlen.p, h_lens, 8 * (size_t)n_q, hipMemcpyHostToDevice, st));
-    HY_HIP(hipMemcpyAsync(d_hash.p, h_name_hash, 4 * (size_t)n_q, hipMemcpyHostToDevice, st));
+    if (d_name_hash)
+        HY_HIP(hipMemcpyAsync(d_hash.p, d_name_hash, 4 * (size_t)n_q, hipMemcpyDeviceToDevice, st));
+    else
+        HY_HIP(hipMemcpyAsync(d_hash.p, h_name_hash, 4 * (size_t)n_q, hipMemcpyHostToDevice, st));
     std::vector<int64_t> h_qm(n_q + 1);
     HY_HIP(hipMemcpyAsync(h_qm.data(), qm_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, st));
     HY_HIP(hipStreamSynchronize(st));
@@ -1438,50 +1508,143 @@ int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *
     }
     tr.mark("long join");
     // -------------------------------------------------------------- 8 regions
-    auto run_regions = [&](ChainSet &C, std::vector<hymet_mm_reg> &regs, std::vector<int32_t> &nreg) -> int {
+    // region records stay in HBM: per chain set, records at the set's chain offsets + counts
+    auto run_regions = [&](ChainSet &C, DevBuf &rg, DevBuf &nr) -> int {
         const int64_t NC = C.n_chain;
-        DevBuf z, rg, wv, cov, tmp, nr;
+        DevBuf z, wv, cov, tmp;
         HY_HIP(z.alloc(16 * (size_t)(NC + 1), st));
         HY_HIP(rg.alloc(sizeof(hymet_mm_reg) * (size_t)(NC + 1), st));
         HY_HIP(wv.alloc(4 * (size_t)(NC + 1), st));
         HY_HIP(cov.alloc(8 * (size_t)(NC + 1), st));
         HY_HIP(tmp.alloc(4 * (size_t)(NC + 1), st));
         HY_HIP(nr.alloc(4 * (size_t)n_q, st));
-        int r2 = launch_regions(ctx, C.bx.as<uint64_t>(), C.by.as<uint64_t>(), C.cu.as<uint64_t>(), C.cboff.as<int64_t>(),
-                                C.d_qc.as<int64_t>(), C.d_qb.as<int64_t>(), mini_pos.as<uint64_t>(), mp_off.as<int64_t>(),
-                                d_qlen.as<int64_t>(), d_hash.as<uint32_t>(), rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
-                                z.p, rg.as<hymet_mm_reg>(), wv.as<int32_t>(), cov.as<uint64_t>(), tmp.as<int32_t>(),
-                                nr.as<int32_t>(), C.n_anchor, NC, NM, C.bchain.as<int32_t>(), C.cq.as<uint32_t>(),
-                                pos_tab.as<int32_t>(), d_qbase.as<int64_t>());
-        if (r2) return r2;
-        regs.resize(NC);
-        nreg.resize(n_q);
-        if (NC) HY_HIP(hipMemcpyAsync(regs.data(), rg.p, sizeof(hymet_mm_reg) * (size_t)NC, hipMemcpyDeviceToHost, st));
-        HY_HIP(hipMemcpyAsync(nreg.data(), nr.p, 4 * (size_t)n_q, hipMemcpyDeviceToHost, st));
-        HY_HIP(hipStreamSynchronize(st));
-        return HYMET_OK;
+        return launch_regions(ctx, C.bx.as<uint64_t>(), C.by.as<uint64_t>(), C.cu.as<uint64_t>(), C.cboff.as<int64_t>(),
+                              C.d_qc.as<int64_t>(), C.d_qb.as<int64_t>(), mini_pos.as<uint64_t>(), mp_off.as<int64_t>(),
+                              d_qlen.as<int64_t>(), d_hash.as<uint32_t>(), rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
+                              z.p, rg.as<hymet_mm_reg>(), wv.as<int32_t>(), cov.as<uint64_t>(), tmp.as<int32_t>(),
+                              nr.as<int32_t>(), C.n_anchor, NC, NM, C.bchain.as<int32_t>(), C.cq.as<uint32_t>(),
+                              pos_tab.as<int32_t>(), d_qbase.as<int64_t>());
     };
-    std::vector<hymet_mm_reg> r1, r2v;
-    std::vector<int32_t> n1, n2;
-    rc = run_regions(C1, r1, n1);
+    DevBuf rg1, nr1, rg2, nr2, d_flag;
+    rc = run_regions(C1, rg1, nr1);
     if (rc) return rc;
     if (!CF) {
-        rc = run_regions(C2, r2v, n2);
+        rc = run_regions(C2, rg2, nr2);
         if (rc) return rc;
+        HY_HIP(d_flag.alloc(4 * (size_t)n_q, st));
+        HY_HIP(hipMemcpyAsync(d_flag.p, h_flag.data(), 4 * (size_t)n_q, hipMemcpyHostToDevice, st));
     }
-    HY_HIP(hipMemcpyAsync(res->rep_len.data(), rep_len.p, 4 * (size_t)n_q, hipMemcpyDeviceToHost, st));
+    // PAF order within the batch: query by query, each query's regions as selected
+    DevBuf cnt, off;
+    HY_HIP(cnt.alloc(4 * (size_t)(n_q + 1), st));
+    const uint32_t *fl = CF ? nullptr : d_flag.as<uint32_t>();
+    const int32_t *n2p = CF ? nr1.as<int32_t>() : nr2.as<int32_t>();
+    const int64_t *qc2 = CF ? C1.d_qc.as<int64_t>() : C2.d_qc.as<int64_t>();
+    const hymet_mm_reg *r2p = CF ? rg1.as<hymet_mm_reg>() : rg2.as<hymet_mm_reg>();
+    LAUNCH1(reg_count_kernel, n_q, fl, nr1.as<int32_t>(), n2p, n_q, cnt.as<uint32_t>());
+    int64_t N = 0;
+    rc = scan_flags(ctx, cnt.as<uint32_t>(), n_q, off, &N);
+    if (rc) return rc;
+    HY_HIP(hipMemcpyAsync(off.as<int64_t>() + n_q, &N, 8, hipMemcpyHostToDevice, st));
+    RegOut o{};
+    DevBuf tmp_regs;
+    if (sink.acc) {
+        hymet_paf_acc *a = sink.acc;
+        rc = acc_reserve(ctx, a, a->n + N);
+        if (rc) return rc;
+        o = RegOut{a->regs.as<hymet_mm_reg>() + a->n, a->q.as<int32_t>() + a->n, a->part.as<int32_t>() + a->n,
+                   a->rl.as<int32_t>() + a->n, a->t.as<int32_t>() + a->n, sink.q_base, sink.part_id, sink.t_base};
+    } else {
+        HY_HIP(tmp_regs.alloc(sizeof(hymet_mm_reg) * (size_t)(N + 1), st));
+        o.regs = tmp_regs.as<hymet_mm_reg>();
+    }
+    {
+        ProfScope _ps(ctx, "mm_paf_records", (double)N * (2.0 * sizeof(hymet_mm_reg) + 16.0));
+        LAUNCH1(reg_gather_kernel, n_q, fl, nr1.as<int32_t>(), n2p, C1.d_qc.as<int64_t>(), qc2, rg1.as<hymet_mm_reg>(),
+                r2p, off.as<int64_t>(), rep_len.as<int32_t>(), n_q, o);
+    }
+    if (sink.acc) {
+        sink.acc->n += N;
+    } else {
+        res->regs.resize(N);
+        if (N) HY_HIP(hipMemcpyAsync(res->regs.data(), tmp_regs.p, sizeof(hymet_mm_reg) * (size_t)N, hipMemcpyDeviceToHost, st));
+        HY_HIP(hipMemcpyAsync(res->reg_off.data(), off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, st));
+        HY_HIP(hipMemcpyAsync(res->rep_len.data(), rep_len.p, 4 * (size_t)n_q, hipMemcpyDeviceToHost, st));
+    }
+    // host vectors above are async copy sources/targets
     HY_HIP(hipStreamSynchronize(st));
     tr.mark("regions");
-    for (int q = 0; q < n_q; q++) {
-        const bool use2 = !CF && h_flag[q];
-        const int nr = use2 ? n2[q] : n1[q];
-        const int64_t c0 = use2 ? C2.h_qc[q] : C1.h_qc[q];
-        const std::vector<hymet_mm_reg> &src = use2 ? r2v : r1;
-        for (int i = 0; i < nr; i++) res->regs.push_back(src[c0 + i]);
-        res->reg_off[q + 1] = (int64_t)res->regs.size();
-    }
-    tr.mark("assemble");
     return HYMET_OK;
+}
+
+extern "C" {
+
+int hymet_mm_map(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *opt, const uint32_t *d_2b,
+                 const uint32_t *d_mask, const int64_t *h_starts, const int64_t *h_lens, const uint32_t *h_name_hash,
+                 int32_t n_q, hymet_mm_result **out) {
+    HY_ARG(out != nullptr, "hymet_mm_map: null argument");
+    MapSink sink;
+    sink.res = new hymet_mm_result();
+    *out = sink.res;
+    return mm_map_impl(ctx, idx, opt, d_2b, d_mask, h_starts, h_lens, h_name_hash, nullptr, n_q, sink);
+}
+
+int hymet_paf_acc_create(hymet_ctx *ctx, hymet_paf_acc **out) {
+    HY_ARG(ctx && out, "hymet_paf_acc_create: null argument");
+    hymet_paf_acc *a = new hymet_paf_acc();
+    a->device = ctx->device;
+    *out = a;
+    return HYMET_OK;
+}
+
+int hymet_paf_acc_reset(hymet_paf_acc *acc) {
+    HY_ARG(acc, "hymet_paf_acc_reset: null argument");
+    acc->n = 0;
+    return HYMET_OK;
+}
+
+int hymet_paf_acc_destroy(hymet_paf_acc *acc) {
+    if (acc) {
+        (void)hipSetDevice(acc->device);
+        delete acc;
+    }
+    return HYMET_OK;
+}
+
+int hymet_paf_acc_info(const hymet_paf_acc *acc, int64_t *n_lines, void **d_regs, void **d_q, void **d_part, void **d_rl,
+                       void **d_t) {
+    HY_ARG(acc && n_lines, "hymet_paf_acc_info: null argument");
+    *n_lines = acc->n;
+    if (d_regs) *d_regs = acc->regs.p;
+    if (d_q) *d_q = acc->q.p;
+    if (d_part) *d_part = acc->part.p;
+    if (d_rl) *d_rl = acc->rl.p;
+    if (d_t) *d_t = acc->t.p;
+    return HYMET_OK;
+}
+
+int hymet_paf_acc_copy(hymet_ctx *ctx, const hymet_paf_acc *acc, int32_t *h_q, int32_t *h_part, int32_t *h_t) {
+    HY_ARG(ctx && acc, "hymet_paf_acc_copy: null argument");
+    if (acc->n <= 0) return HYMET_OK;
+    HY_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    if (h_q) HY_HIP(hipMemcpyAsync(h_q, acc->q.p, 4 * (size_t)acc->n, hipMemcpyDeviceToHost, st));
+    if (h_part) HY_HIP(hipMemcpyAsync(h_part, acc->part.p, 4 * (size_t)acc->n, hipMemcpyDeviceToHost, st));
+    if (h_t) HY_HIP(hipMemcpyAsync(h_t, acc->t.p, 4 * (size_t)acc->n, hipMemcpyDeviceToHost, st));
+    HY_HIP(hipStreamSynchronize(st));
+    return HYMET_OK;
+}
+
+int hymet_mm_map_acc(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *opt, const uint32_t *d_2b,
+                     const uint32_t *d_mask, const int64_t *h_starts, const int64_t *h_lens, const uint32_t *d_name_hash,
+                     int32_t n_q, int32_t q_base, int32_t part_id, int32_t t_base, hymet_paf_acc *acc) {
+    HY_ARG(acc && d_name_hash, "hymet_mm_map_acc: null argument");
+    MapSink sink;
+    sink.acc = acc;
+    sink.q_base = q_base;
+    sink.part_id = part_id;
+    sink.t_base = t_base;
+    return mm_map_impl(ctx, idx, opt, d_2b, d_mask, h_starts, h_lens, nullptr, d_name_hash, n_q, sink);
 }
 
 int hymet_mm_chain_dp(hymet_ctx *ctx, const uint64_t *h_x, const uint64_t *h_y, int64_t n, int max_dist,

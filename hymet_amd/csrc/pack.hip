@@ -81,7 +81,7 @@ extern "C" int hymet_pack(hymet_ctx *ctx, const uint8_t *d_ascii, int64_t n, int
     int rc = ensure_tables(ctx->device);
     if (rc) return rc;
     int64_t nthreads = (n + 31) / 32;
-    hymet::ProfScope _ps(ctx, "pack");
+    hymet::ProfScope _ps(ctx, "pack", 1.375 * (double)n);  // ASCII read, 2-bit + mask write
     hipLaunchKernelGGL(pack_kernel, dim3((unsigned)hymet::cdiv(nthreads, 256)), dim3(256), 0, ctx->stream, d_ascii, n,
                        alphabet, d_2b, d_mask);
     HY_CHECK_LAUNCH("pack_kernel");

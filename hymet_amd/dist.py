@@ -67,10 +67,68 @@ class Comm:
         return [np.array(sorted(b), dtype=np.int64) for b in bins]
 
     # -------------------------------------------------------------- collectives
+    def _staged(self, t):
+        """gloo works on host tensors: device tensors travel through a host copy (the
+        multi-process tests run several ranks on one GPU this way); RCCL takes them as is."""
+        return self.dist.get_backend() == "gloo" and t.is_cuda
+
     def allreduce_sum_(self, t):
         if self.world > 1:
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+            if self._staged(t):
+                h = t.cpu()
+                self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM)
+                t.copy_(h)
+            else:
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return t
+
+    def all_gather_padded(self, t, n: int):
+        """All-gather the first n rows of t (n may differ per rank): rows padded to the
+        largest n; returns the list of every rank's first-n slices."""
+        torch = self.torch
+        ns = [int(x[0]) for x in self.allgather_np(np.array([n], np.int64))]
+        m = max(ns) if ns else 0
+        pad = torch.zeros((max(m, 1),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if n:
+            pad[:n].copy_(t[:n])
+        src = pad.cpu() if self._staged(pad) else pad
+        out = [torch.empty_like(src) for _ in range(self.world)]
+        self.dist.all_gather(out, src)
+        if src is not pad:
+            out = [o.to(t.device) for o in out]
+        return [o[:k] for o, k in zip(out, ns)]
+
+    def gather_rows(self, rows, q_base: int, gpu=None):
+        """every rank's LCA rows (fixed-size records: query index in
+        the whole input, index part of its first PAF line, depth, taxid, 8 name ids,
+        confidence) are all-gathered over RCCL; rank 0 orders them like the reference's
+        output -- minimap2 prints the pooled input part by part, queries in input order
+        within a part, and classification_cami.py writes queries in first-appearance order
+        (:333-339) -- i.e. by (first part, query index).  Other ranks get empty rows."""
+        torch = self.torch
+        R = int(rows["q"].shape[0])
+        dev = rows["q"].device
+        rec = torch.zeros((max(R, 1), 12), dtype=torch.int32, device=dev)
+        if R:
+            rec[:R, 0] = rows["q"] + int(q_base)
+            rec[:R, 1] = rows["part"]
+            rec[:R, 2] = rows["depth"]
+            rec[:R, 3] = rows["tax"]
+            rec[:R, 4:] = rows["names"].view(R, 8)
+        recs = self.all_gather_padded(rec, R)
+        confs = self.all_gather_padded(rows["conf"], R)
+        if self.rank != 0:
+            e = torch.zeros(0, dtype=torch.int32, device=dev)
+            return {"q": e, "part": e, "depth": e, "tax": e, "names": e,
+                    "conf": torch.zeros(0, dtype=torch.float64, device=dev)}, 0
+        allr = torch.cat(recs)
+        allc = torch.cat(confs)
+        key = allr[:, 1].to(torch.int64) * (1 << 32) + allr[:, 0].to(torch.int64)
+        order = torch.sort(key, stable=True).indices
+        allr, allc = allr[order], allc[order]
+        n = int(allr.shape[0])
+        return {"q": allr[:, 0].contiguous(), "part": allr[:, 1].contiguous(), "depth": allr[:, 2].contiguous(),
+                "tax": allr[:, 3].contiguous(), "names": allr[:, 4:].contiguous().view(-1), "conf": allc.contiguous()}, n
 
     def allgather_np(self, arr: np.ndarray) -> List[np.ndarray]:
         if self.world <= 1:

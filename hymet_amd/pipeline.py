@@ -1,17 +1,21 @@
 """The fused, device-resident hot path of `bin/hymet run` (run_hymet_cami.sh steps 1-5):
 
-    screen (3 sketch DBs, one hash pass)  -> mash.sh selection per DB -> union (sort -u)
+    FASTA bytes (host) -> one H2D copy -> ASCII pool + packed alphabets (HBM)
+    -> screen (sketch DBs, one hash pass) -> mash.sh selection per DB -> union (sort -u)
     -> limit_candidates -> [candidate-keyed index cache, as run_hymet_cami.sh:135-171]
-    -> minimap2 asm10 mapping per -I2g part -> classification_cami weighted LCA -> TSV
+    -> minimap2 asm10 mapping per -I2g part into a device-resident PAF (hymet_paf_acc)
+    -> classification_cami weighted LCA over that PAF in HBM -> TSV (and PAF) text written
+       on the device, copied out once.
 
-Everything between the input pool and the TSV stays in HBM except the small host-side
-text steps (screen rows, candidate lists) and the region records that become PAF lines.
-Multi-GPU: every rank holds its own contig shard; the screen counts and
-the per-target PAF line counts are all-reduced; rank 0 assembles the TSV in the
-reference's query order.
+Host work per run is the short text logic of selection and a few dozen library calls; no
+per-contig or per-line Python.  Multi-GPU: every rank takes a contiguous
+record range of the same FASTA (balanced by bases); the screen hit counts and the
+per-target PAF line counts are all-reduced; fixed-size LCA row records are all-gathered and
+rank 0 writes the TSV in the reference's query order.
 """
 from __future__ import annotations
 
+import ctypes
 import hashlib
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
@@ -22,8 +26,13 @@ from . import classify as cls
 from . import mapper as mp
 from . import screen as scr
 from . import select as sel
+from ._lib import check, ptr
+from .ingest import FastaIndex, QueryShard
 from .msh import SketchDB
-from .seqio import DevicePool, SeqSet, from_records
+from .seqio import SeqSet
+
+_c = ctypes
+TSV_HEADER = b"Query\tLineage\tTaxonomic Level\tConfidence\r\n"
 
 
 @dataclass
@@ -46,6 +55,7 @@ class IndexSet:
     parts: List[mp.IndexPart]
     part_first: List[int]             # global target index of each part's rid 0
     opt: mp.MapOpt                    # asm10 options, mid_occ resolved on this set's first part
+    dev: Dict[str, object] = field(default_factory=dict)   # target name pool / lengths in HBM
 
 
 @dataclass
@@ -54,10 +64,55 @@ class RunResult:
     screen_rows: List[List[str]]      # per DB, rows after sort -u -k5,5 | sort -gr
     thresholds: List[str]
     tsv: bytes
-    n_queries: int
-    n_classified: int
-    n_paf_lines: int
-    paf: Optional[List[str]] = None
+    n_queries: int                    # TSV rows (queries with >= 1 PAF line)
+    n_classified: int                 # rows with a lineage other than Unknown
+    n_paf_lines: int                  # this rank's PAF lines
+    paf_bytes: Optional[bytes] = None  # this rank's resultados.paf text (with_paf)
+
+    @property
+    def paf(self) -> Optional[List[str]]:
+        if self.paf_bytes is None:
+            return None
+        return self.paf_bytes.decode().split("\n")[:-1] if self.paf_bytes else []
+
+
+class PafAcc:
+    """hymet_paf_acc: the run's resultados.paf as records in HBM."""
+
+    def __init__(self, gpu):
+        self.gpu = gpu
+        h = _c.c_void_p()
+        check(gpu.lib.hymet_paf_acc_create(gpu.ctx, _c.byref(h)), "hymet_paf_acc_create")
+        self.h = h
+
+    def reset(self):
+        check(self.gpu.lib.hymet_paf_acc_reset(self.h), "hymet_paf_acc_reset")
+
+    @property
+    def n(self) -> int:
+        n = _c.c_int64()
+        check(self.gpu.lib.hymet_paf_acc_info(self.h, _c.byref(n), None, None, None, None, None), "hymet_paf_acc_info")
+        return n.value
+
+    def columns(self):
+        """(query, part, target) index of every line in PAF order (host; the rare fallback)."""
+        n = self.n
+        q, part, t = (np.zeros(max(n, 1), np.int32) for _ in range(3))
+        check(self.gpu.lib.hymet_paf_acc_copy(self.gpu.ctx, self.h, q.ctypes.data_as(_c.c_void_p),
+                                              part.ctypes.data_as(_c.c_void_p), t.ctypes.data_as(_c.c_void_p)),
+              "hymet_paf_acc_copy")
+        return q[:n], part[:n], t[:n]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.gpu.lib.hymet_paf_acc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Pipeline:
@@ -79,9 +134,39 @@ class Pipeline:
             self.classifier, self.classifier_error = None, e
         self.index_cache: Dict[str, IndexSet] = {}
         self.opt: Optional[mp.MapOpt] = None
+        self.acc = PafAcc(gpu)
+        self._bufs: Dict[str, object] = {}
+
+    @property
+    def world(self) -> int:
+        return self.comm.world if self.comm is not None else 1
+
+    @property
+    def rank(self) -> int:
+        return self.comm.rank if self.comm is not None else 0
 
     # ------------------------------------------------------------------ stages
-    def screen_select(self, pool: DevicePool):
+    def ingest(self, queries) -> QueryShard:
+        """FASTA bytes / FastaIndex (this rank's contiguous record range) or a SeqSet (one
+        rank) -> QueryShard resident in HBM."""
+        if isinstance(queries, QueryShard):
+            return queries
+        if isinstance(queries, (bytes, bytearray, memoryview)):
+            queries = FastaIndex(bytes(queries))
+        if isinstance(queries, FastaIndex):
+            r0, r1 = queries.shard(self.rank, self.world)
+            sh = QueryShard.from_fasta(self.gpu, queries, r0, r1, self.cfg.map_batch_bases)
+            sh.fasta = queries
+            return sh
+        if isinstance(queries, SeqSet):
+            if self.world > 1:
+                raise ValueError("multi-rank runs take the FASTA bytes (every rank shards the same input)")
+            return QueryShard.from_seqset(self.gpu, queries, 0, self.cfg.map_batch_bases)
+        raise TypeError(f"unsupported query input {type(queries)!r}")
+
+    prepare = ingest
+
+    def screen_select(self, pool):
         res = scr.screen(self.gpu, pool, self.dbs, self.tables, self.comm)
         rows, thr, selections = [], [], []
         for r in res:
@@ -90,7 +175,7 @@ class Pipeline:
             rows.append(s)
             thr.append(t)
             selections.append(names)
-        selected = sel.union_sorted(*selections) if len(selections) > 1 else sel.union_sorted(selections[0])
+        selected = sel.union_sorted(*selections)
         scores = sel.best_scores(rows)
         limited = sel.limit(selected, scores, self.cfg.cand_max, self.cfg.dedupe)
         return limited, rows, thr
@@ -111,156 +196,178 @@ class Pipeline:
         opt = mp.MapOpt.asm10()
         opt.resolve_mid_occ(parts[0])
         ix = IndexSet(list(refs.names), np.asarray(refs.lengths, np.int64), parts, first, opt)
+        torch = self.gpu.torch
+        tb = [n.encode() for n in ix.names]
+        toff = np.zeros(len(tb) + 1, np.int64)
+        np.cumsum([len(b) for b in tb], out=toff[1:])
+        ix.dev = {"tname": torch.frombuffer(bytearray(b"".join(tb) or b"\0"), dtype=torch.uint8).to(self.gpu.dev),
+                  "tname_off": torch.from_numpy(toff).to(self.gpu.dev),
+                  "tlen": torch.from_numpy(ix.lens.copy()).to(self.gpu.dev)}
         self.index_cache = {key: ix}  # one cached candidate set, like the sha1 cache dir
         return ix
 
-    def prepare(self, queries: SeqSet) -> "Prepared":
-        """Make the query set resident in HBM: one Mash-alphabet pool for the screen and
-        minimap2-alphabet pools cut into mapping batches (sized for the anchor working set)."""
-        pq = Prepared(queries, DevicePool(self.gpu, queries, DevicePool.ALPHA_MASH), [])
-        for b0, b1 in _batches(queries.lengths, self.cfg.map_batch_bases):
-            sub = queries if (b0 == 0 and b1 == queries.n) else queries.subset(range(b0, b1))
-            names_hash = np.array([mp.x31_hash(n) for n in sub.names], np.uint32)
-            pq.batches.append((b0, DevicePool(self.gpu, sub, DevicePool.ALPHA_MINIMAP2), names_hash))
-        return pq
-
-    def map_all(self, ix: IndexSet, pq: "Prepared"):
-        """Per part, per query batch -> list of (part, query offset, MapResult)."""
+    def map_all(self, ix: IndexSet, sh: QueryShard) -> int:
+        """minimap2 -x asm10 of every query batch against every part, appended to the
+        device PAF in minimap2's order (part-major, queries in input order)."""
         self.opt = ix.opt
-        out = []
+        self.acc.reset()
+        gpu = self.gpu
+        starts = np.ascontiguousarray(sh.starts, np.int64)
+        lens = np.ascontiguousarray(sh.lengths, np.int64)
+        hbase = sh.name_hash.data_ptr()
         for pi, part in enumerate(ix.parts):
-            for b0, qp, nh in pq.batches:
-                out.append((pi, b0, mp.map_part(self.gpu, part, qp, self.opt, nh)))
-        return out
+            for b0, b1 in sh.batches:
+                n = b1 - b0
+                if n <= 0:
+                    continue
+                gpu.call("hymet_mm_map_acc", part.h, _c.byref(ix.opt), ptr(sh.mm.w2b), ptr(sh.mm.wmask),
+                         _c.c_void_p(starts.ctypes.data + 8 * b0), _c.c_void_p(lens.ctypes.data + 8 * b0),
+                         _c.c_void_p(hbase + 4 * b0), n, b0, pi, ix.part_first[pi], self.acc.h)
+        return self.acc.n
 
-    def paf_table(self, ix: IndexSet, queries: SeqSet, results, with_text=False):
-        """PAF lines in minimap2's output order (part-major, query order) as classifier arrays."""
-        qnames = queries.names
-        lq, lt, lb, lp, text = [], [], [], [], ([] if with_text else None)
-        for pi, b0, res in results:
-            first = ix.part_first[pi]
-            regs = res.regs
-            if len(regs) == 0:
+    def classify_rows(self, ix: IndexSet, sh: QueryShard):
+        """ref_counts (all-reduced) + device LCA over the accumulator -> row tensors."""
+        gpu, torch = self.gpu, self.gpu.torch
+        tabs = self.classifier.device_tables(ix.names)
+        counts = gpu.zeros(max(len(ix.names), 1), torch.int32)
+        gpu.call("hymet_acc_ref_counts", self.acc.h, ptr(counts))
+        if self.world > 1:
+            self.comm.allreduce_sum_(counts)
+        n_q = max(sh.n, 1)
+        rq, rp, rd, rt = (gpu.zeros(n_q, torch.int32) for _ in range(4))
+        rn = gpu.zeros(n_q * 8, torch.int32)
+        rc = gpu.zeros(n_q, torch.float64)
+        nr = _c.c_int32()
+        legacy = self.variant == cls.LEGACY
+        gpu.call("hymet_acc_classify", self.acc.h, self.variant, sh.n, ptr(sh.qlen), ptr(counts), ptr(tabs["t_tax"]),
+                 ptr(tabs["tax_names"]), ptr(tabs["in_hier"]), ptr(sh.qname) if legacy else None,
+                 ptr(sh.qname_off) if legacy else None, ptr(ix.dev["tname"]) if legacy else None,
+                 ptr(ix.dev["tname_off"]) if legacy else None, ptr(rq), ptr(rp), ptr(rd), ptr(rn), ptr(rc), ptr(rt),
+                 _c.byref(nr))
+        R = nr.value
+        return {"q": rq[:R], "part": rp[:R], "depth": rd[:R], "names": rn[:R * 8], "conf": rc[:R], "tax": rt[:R]}, R
+
+    def emit_tsv(self, rows, R, qname, qname_off) -> bytes:
+        gpu = self.gpu
+        tabs = self.classifier.device_tables(None)
+        legacy = self.variant == cls.LEGACY
+        nb = _c.c_int64()
+        cap = max(256 * R, 1 << 16)
+        while True:
+            out = self._dev_buf("tsv", cap)
+            rc = gpu.lib.hymet_emit_tsv(gpu.ctx, self.variant, R, ptr(rows["q"]), ptr(rows["depth"]), ptr(rows["names"]),
+                                        ptr(rows["conf"]), ptr(rows["tax"]), ptr(qname), ptr(qname_off), ptr(tabs["label"]),
+                                        ptr(tabs["label_off"]), ptr(tabs["taxlin"]) if legacy else None,
+                                        ptr(tabs["taxlin_off"]) if legacy else None,
+                                        ptr(tabs["taxlvl"]) if legacy else None,
+                                        ptr(tabs["taxlvl_off"]) if legacy else None, ptr(out), cap, _c.byref(nb))
+            if rc == -3:
+                cap = nb.value
                 continue
-            nper = np.diff(res.off)
-            lq.append(np.repeat(np.arange(len(nper), dtype=np.int64) + b0, nper))
-            lt.append(regs["rid"].astype(np.int32) + np.int32(first))
-            lb.append(regs["blen"].astype(np.int64))
-            lp.append(np.full(len(regs), pi, np.int32))
-            if with_text:
-                for q in np.flatnonzero(nper):
-                    g = int(q) + b0
-                    text.extend(mp.paf_lines(qnames[g], int(queries.lengths[g]), res.query(int(q)), int(res.rep_len[q]),
-                                             ix.names[first:], ix.lens[first:]))
-        if lq:
-            all_q = np.concatenate(lq)
-            uq, first_pos = np.unique(all_q, return_index=True)
-            order_q = uq[np.argsort(first_pos, kind="stable")]      # queries by first appearance
-            pos = np.empty(int(all_q.max()) + 1, np.int64)
-            pos[order_q] = np.arange(len(order_q))
-            line_q = pos[all_q].astype(np.int32)
-            line_t, line_b = np.concatenate(lt), np.concatenate(lb)
-            line_l = np.asarray(queries.lengths, np.int64)[all_q]
-            fp = np.sort(first_pos)
-            self.last_qkey = (np.concatenate(lp)[fp], order_q.astype(np.int64))  # (part of first line, query)
-        else:
-            self.last_qkey = (np.zeros(0, np.int32), np.zeros(0, np.int64))
-            order_q = np.zeros(0, np.int64)
-            line_q, line_t = np.zeros(0, np.int32), np.zeros(0, np.int32)
-            line_b, line_l = np.zeros(0, np.int64), np.zeros(0, np.int64)
-        exact = np.zeros(len(line_q), np.uint8)
-        if self.variant == cls.LEGACY and len(line_q):
-            # classification.py:141-151: query == target and coverage >= 0.99
-            same = np.asarray(qnames, dtype=object)[all_q] == np.asarray(ix.names, dtype=object)[line_t]
-            cov = np.where(line_l > 0, line_b / np.maximum(line_l, 1), 0.0)
-            exact = (same & (cov >= 0.99)).astype(np.uint8)
-        table = cls.PafTable([qnames[q] for q in order_q], line_q, list(ix.names), line_t, line_b, line_l, exact)
-        return table, text
+            check(rc, "hymet_emit_tsv")
+            break
+        return TSV_HEADER + self._to_host("tsv_h", out, nb.value)
+
+    def emit_paf(self, ix: IndexSet, sh: QueryShard) -> bytes:
+        """This rank's resultados.paf text (its queries' lines, part-major)."""
+        gpu = self.gpu
+        n = self.acc.n
+        if n == 0:
+            return b""
+        nb = _c.c_int64()
+        cap = 200 * n
+        while True:
+            out = self._dev_buf("paf", cap)
+            rc = gpu.lib.hymet_emit_paf(gpu.ctx, self.acc.h, ptr(sh.qname), ptr(sh.qname_off), ptr(sh.qlen),
+                                        ptr(ix.dev["tname"]), ptr(ix.dev["tname_off"]), ptr(ix.dev["tlen"]), ptr(out), cap,
+                                        _c.byref(nb), None)
+            if rc == -3:
+                cap = nb.value
+                continue
+            check(rc, "hymet_emit_paf")
+            break
+        return self._to_host("paf_h", out, nb.value)
+
+    def _dev_buf(self, key, nbytes):
+        """A reusable device byte buffer of at least nbytes."""
+        torch = self.gpu.torch
+        b = self._bufs.get(key)
+        if b is None or b.numel() < nbytes:
+            self._bufs.pop(key, None)
+            b = self.gpu.empty(max(int(nbytes), 16), torch.uint8)
+            self._bufs[key] = b
+        return b
+
+    def _to_host(self, key, dev, n) -> bytes:
+        """D2H of n bytes through a reusable pinned host buffer."""
+        torch = self.gpu.torch
+        if n == 0:
+            return b""
+        h = self._bufs.get(key)
+        if h is None or h.numel() < n:
+            h = torch.empty(int(n * 1.25) + 4096, dtype=torch.uint8, pin_memory=True)
+            self._bufs[key] = h
+        h[:n].copy_(dev[:n])
+        return h[:n].numpy().tobytes()
 
     # ------------------------------------------------------------------- run
-    def run(self, queries, with_paf=False, query_ids=None) -> RunResult:
-        """queries: a SeqSet, or a Prepared (already resident in HBM).  With several ranks,
-        query_ids gives each local query's index in the whole input (default: the shards
-        are consecutive slices in rank order); rank 0's RunResult.tsv is the whole TSV."""
-        pq = queries if isinstance(queries, Prepared) else self.prepare(queries)
-        queries = pq.queries
-        selected, rows, thr = self.screen_select(pq.mash_pool)
+    def run(self, queries, with_paf=False) -> RunResult:
+        """queries: FASTA bytes, a FastaIndex, a SeqSet, or a QueryShard already resident.
+        Rank 0's RunResult.tsv is the whole classified_sequences.tsv."""
+        sh = self.ingest(queries)
+        selected, rows, thr = self.screen_select(sh.mash)
         if not selected:
             raise RuntimeError("candidate list empty after applying limit")  # run_hymet_cami.sh:126
         ix = self.index_for(selected)
-        results = self.map_all(ix, pq)
-        table, text = self.paf_table(ix, queries, results, with_paf)
-        part, q = self.last_qkey
-        multi = self.comm is not None and self.comm.world > 1
-        gid = None
-        if multi:
-            gid = (np.asarray(query_ids, np.int64)[q] if query_ids is not None
-                   else (np.int64(self.comm.rank) << np.int64(32)) + q)
-        rws, tsv = [], b""
+        n_lines = self.map_all(ix, sh)
+        paf_bytes = self.emit_paf(ix, sh) if with_paf else None
+        tsv, n_rows, n_cls = b"", 0, 0
         if self.classifier is not None:
-            res = self.classifier.run(table, comm=self.comm)
-            rws = self.classifier.rows(res)
-            if multi:
-                rws = gather_rows(self.comm, rws, part, gid)
-            tsv = self.classifier.tsv_bytes(res, rws)
-        n_rows = len(rws)
-        if multi:
-            n_rows = self.comm.broadcast_obj(n_rows)
-        if n_rows < 1:  # fewer than 2 TSV lines: run_hymet_cami.sh:182-206
-            tsv = self._fallback(table, part, gid)
-            rws = []
-        return RunResult(selected, rows, thr, tsv, len(rws), sum(1 for r in rws if r[1] != "Unknown"), table.n_lines, text)
+            rws, R = self.classify_rows(ix, sh)
+            if self.world > 1:
+                rws, R = self.comm.gather_rows(rws, sh.q_base, self.gpu)
+                qname, qname_off = self._global_names(sh)
+            else:
+                qname, qname_off = sh.qname, sh.qname_off
+            if self.rank == 0:
+                tsv = self.emit_tsv(rws, R, qname, qname_off)
+                n_rows = R
+                n_cls = int((rws["depth"] != 0).sum().item()) if R else 0
+        total_rows = self.comm.broadcast_obj(n_rows) if self.world > 1 else n_rows
+        if total_rows < 1:  # fewer than 2 TSV lines: run_hymet_cami.sh:182-206
+            tsv = self._fallback(ix, sh)
+            n_rows = n_cls = 0
+        return RunResult(selected, rows, thr, tsv, n_rows, n_cls, n_lines, paf_bytes)
 
-    def _fallback(self, table, part, gid) -> bytes:
+    def _global_names(self, sh: QueryShard):
+        """Rank 0's name pool of the whole input (rows from every rank index into it)."""
+        fx = sh.fasta
+        if self._bufs.get("names_of") is not fx:
+            torch = self.gpu.torch
+            pool, off = fx.name_pool()
+            self._bufs["names"] = (torch.frombuffer(bytearray(pool or b"\0"), dtype=torch.uint8).to(self.gpu.dev),
+                                   torch.from_numpy(off).to(self.gpu.dev))
+            self._bufs["names_of"] = fx
+        return self._bufs["names"]
+
+    def _fallback(self, ix: IndexSet, sh: QueryShard) -> bytes:
         """build_id_map + mini_classify over the PAF lines (first mapped hit per query), then
         the awk rewrite; dies like the script when even that leaves no row."""
         from . import fallback
-        pairs = [(table.queries[int(a)], table.targets[int(b)]) for a, b in zip(table.line_q, table.line_t)]
-        if self.comm is not None and self.comm.world > 1:
+        q, part, t = self.acc.columns()
+        if sh.names_host is not None:
+            names = sh.names_host
+        else:
+            names = sh.fasta.names()[sh.q_base:sh.q_base + sh.n]
+        pairs = [(names[int(a)], ix.names[int(b)]) for a, b in zip(q, t)]
+        if self.world > 1:
             # lines of a query sit together per part; queries sort by (part, input index)
-            key = {table.queries[i]: (int(part[i]), int(gid[i])) for i in range(len(table.queries))}
-            got = self.comm.gather_obj([(key[a], j, a, b) for j, (a, b) in enumerate(pairs)])
-            if self.comm.rank != 0:
+            got = self.comm.gather_obj([(int(p_), sh.q_base + int(a), j, pa[0], pa[1])
+                                        for j, (p_, a, pa) in enumerate(zip(part, q, pairs))])
+            if self.rank != 0:
                 return b""
-            pairs = [(a, b) for _, _, a, b in sorted(x for g in got for x in g)]
+            pairs = [(x[3], x[4]) for x in sorted(y for g in got for y in g)]
         tsv = fallback.fallback_tsv(pairs, self.taxonomy)
         if tsv.count(b"\n") < 2:
             raise RuntimeError("classification still empty after fallback")  # run_hymet_cami.sh:205
         return tsv
-
-
-def gather_rows(comm, rows, part: np.ndarray, qid: np.ndarray, dst: int = 0):
-    """Rank `dst` assembles the classified_sequences.tsv rows of every contig shard
-    (SURVEY.md §8e step 7).  minimap2 prints the pooled input's PAF index part by part, and
-    within a part query by query in input order; the reference writes one row per query in
-    order of first PAF appearance.  So rows sort by (part of the query's first line, the
-    query's index in the whole input).  Other ranks get []."""
-    got = comm.gather_obj((rows, np.asarray(part, np.int64), np.asarray(qid, np.int64)), dst)
-    if comm.rank != dst:
-        return []
-    all_rows = [r for rw, _, _ in got for r in rw]
-    if not all_rows:
-        return []
-    kp = np.concatenate([p for _, p, _ in got])
-    kq = np.concatenate([q for _, _, q in got])
-    order = np.lexsort((kq, kp))
-    return [all_rows[i] for i in order]
-
-
-@dataclass
-class Prepared:
-    queries: SeqSet
-    mash_pool: DevicePool
-    batches: list
-
-
-def _batches(lengths: np.ndarray, max_bases: int):
-    out, b0, acc = [], 0, 0
-    for i, L in enumerate(lengths):
-        if acc and acc + int(L) > max_bases:
-            out.append((b0, i))
-            b0, acc = i, 0
-        acc += int(L)
-    if b0 < len(lengths) or not out:
-        out.append((b0, len(lengths)))
-    return out

@@ -68,6 +68,32 @@ int hymet_scratch_cached(hymet_ctx *ctx, int64_t *bytes);
 int hymet_pack(hymet_ctx *ctx, const uint8_t *d_ascii, int64_t n, int alphabet,
                uint32_t *d_2b, uint32_t *d_mask);
 
+/* ------------------------------------------------------------------ FASTA ingest
+ * The reference hands the pooled contigs to Mash and minimap2 as FASTA files (mash.sh:14,
+ * minimap2.sh:23; kseq: a record starts at '>' at the start of a line, the name is the
+ * header's first whitespace-delimited token, line breaks are not sequence).  Host half:
+ * the record table of a FASTA file in host memory (threads host threads, no copy).  cap =
+ * capacity of the h_* arrays; HYMET_E_CAPACITY with *n_rec set when it is too small.
+ * Offsets are byte offsets into h_buf; seq [h_seq_off, h_seq_end) includes line breaks,
+ * h_nbases excludes them. */
+int hymet_fasta_index(const char *h_buf, int64_t n, int threads, int64_t cap, int64_t *n_rec, int64_t *h_name_off,
+                      int32_t *h_name_len, int64_t *h_seq_off, int64_t *h_seq_end, int64_t *h_nbases);
+/* the names of n records (from the table above) gathered into h_pool (capacity sum of
+ * h_name_len), with n + 1 offsets into it */
+int hymet_fasta_names(const char *h_buf, const int64_t *h_name_off, const int32_t *h_name_len, int64_t n, char *h_pool,
+                      int64_t *h_pool_off);
+/* Device half: d_raw holds file bytes [raw_base, raw_base + raw_len) covering n_rec whole
+ * records (host tables of those records); writes their sequences joined by one 'N' to
+ * d_pool (pool_len = sum(nbases) + n_rec - 1, 16-byte aligned for hymet_pack) and each
+ * record's pool offset to d_pool_start.  Synchronises the context stream. */
+int hymet_fasta_compact(hymet_ctx *ctx, const uint8_t *d_raw, int64_t raw_len, int64_t raw_base, const int64_t *h_seq_off,
+                        const int64_t *h_seq_end, const int64_t *h_nbases, int64_t n_rec, uint8_t *d_pool,
+                        int64_t pool_len, int64_t *d_pool_start);
+/* khash X31 hash of every name (d_raw + d_name_off[i], d_name_len[i] bytes): the per-query
+ * seed of minimap2's hash tie-break (map.c mm_map_frag). */
+int hymet_name_hash(hymet_ctx *ctx, const uint8_t *d_raw, const int64_t *d_name_off, const int32_t *d_name_len, int64_t n,
+                    uint32_t *d_hash);
+
 /* ------------------------------------------------------------ Mash screen
  * Replaces `mash screen` (scripts/mash.sh:14): one open-addressing table of the distinct
  * sketch hashes of a DB, counts of every pooled canonical k-mer hash that hits it, and the
@@ -153,6 +179,29 @@ int hymet_mm_result_size(const hymet_mm_result *res, int64_t *n_regs);
 int hymet_mm_result_copy(const hymet_mm_result *res, int64_t *h_off, int32_t *h_rep_len,
                          hymet_mm_reg *h_regs);
 int hymet_mm_result_destroy(hymet_mm_result *res);
+/* Device-resident resultados.paf of a run: hymet_mm_map_acc appends one batch's lines
+ * (query q_base + q, index part part_id, target t_base + rid), so after every part x batch
+ * the accumulator holds minimap2's output order (part-major, queries in input order).  The
+ * classifier and the PAF text writer read it in place; nothing returns to the host. */
+typedef struct hymet_paf_acc hymet_paf_acc;
+int hymet_paf_acc_create(hymet_ctx *ctx, hymet_paf_acc **out);
+int hymet_paf_acc_reset(hymet_paf_acc *acc);
+int hymet_paf_acc_destroy(hymet_paf_acc *acc);
+/* line count and the device arrays (hymet_mm_reg, int32 query, part, rep_len, target) */
+int hymet_paf_acc_info(const hymet_paf_acc *acc, int64_t *n_lines, void **d_regs, void **d_q, void **d_part, void **d_rl,
+                       void **d_t);
+/* query, part and target index of every line, copied to host arrays of n_lines (synchronous) */
+int hymet_paf_acc_copy(hymet_ctx *ctx, const hymet_paf_acc *acc, int32_t *h_q, int32_t *h_part, int32_t *h_t);
+int hymet_mm_map_acc(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *opt, const uint32_t *d_2b,
+                     const uint32_t *d_mask, const int64_t *h_starts, const int64_t *h_lens, const uint32_t *d_name_hash,
+                     int32_t n_q, int32_t q_base, int32_t part_id, int32_t t_base, hymet_paf_acc *acc);
+/* resultados.paf text of the accumulator's lines (format.c mm_write_paf3 + write_tags, no
+ * CIGAR): query names d_qname[d_qname_off[q] .. d_qname_off[q+1]), d_qlen[q]; target names
+ * and lengths likewise.  *n_bytes = text size; HYMET_E_CAPACITY when > cap (nothing
+ * written).  d_line_off (optional, n_lines + 1): byte offset of every line. */
+int hymet_emit_paf(hymet_ctx *ctx, const hymet_paf_acc *acc, const uint8_t *d_qname, const int64_t *d_qname_off,
+                   const int64_t *d_qlen, const uint8_t *d_tname, const int64_t *d_tname_off, const int64_t *d_tlen,
+                   char *d_out, int64_t cap, int64_t *n_bytes, int64_t *d_line_off);
 /* Chaining DP alone (lchain.c mg_lchain_rmq's f[]/p[], the stage inside hymet_mm_map), for
  * parity tests and kernel timing: n anchors (x, y as minimap2 packs them) of ONE query,
  * sorted by x; groups are runs of equal x>>32.  max_dist/bw are given as mg_lchain_rmq
@@ -169,6 +218,27 @@ int hymet_mm_chain_dp(hymet_ctx *ctx, const uint64_t *h_x, const uint64_t *h_y, 
  * hymet_lca_ref_counts: d_counts[t] += #lines with target t (ref_abundance, caller-zeroed;
  * all-reduced across ranks by the caller). */
 int hymet_lca_ref_counts(hymet_ctx *ctx, const int32_t *d_line_t, int64_t n_lines, int32_t *d_counts);
+/* The same over a hymet_paf_acc (the fused path): ref_counts of its lines, then rows = the
+ * queries with >= 1 line in classification_cami.py's output order (first appearance in
+ * the PAF: by index part of the first line, then query index), each classified over its
+ * lines in PAF order.  Row outputs hold n_q entries; *n_rows is set (synchronises).  Query
+ * lengths d_qlen[q]; the legacy mode's exact-match test compares query and target names. */
+int hymet_acc_ref_counts(hymet_ctx *ctx, const hymet_paf_acc *acc, int32_t *d_counts);
+int hymet_acc_classify(hymet_ctx *ctx, const hymet_paf_acc *acc, int mode, int32_t n_q, const int64_t *d_qlen,
+                       const int32_t *d_ref_counts, const int32_t *d_t_tax, const int32_t *d_tax_names,
+                       const uint8_t *d_tax_in_hier, const uint8_t *d_qname_pool, const int64_t *d_qname_off,
+                       const uint8_t *d_tname_pool, const int64_t *d_tname_off, int32_t *d_row_q, int32_t *d_row_part,
+                       int32_t *d_row_depth, int32_t *d_row_names, double *d_row_conf, int32_t *d_row_tax,
+                       int32_t *n_rows);
+/* classified_sequences.tsv rows (no header) for LCA rows (csv.writer: tab, minimal quoting,
+ * CRLF, "%.4f"): query names by row_q from the name pool; CAMI lineages "rank:name" joined
+ * by "; " from the label pool, legacy ones ";"-joined raw parts, the legacy exact shortcut
+ * the taxid's raw lineage / level strings.  Two-call capacity protocol as hymet_emit_paf. */
+int hymet_emit_tsv(hymet_ctx *ctx, int mode, int32_t n_rows, const int32_t *d_row_q, const int32_t *d_row_depth,
+                   const int32_t *d_row_names, const double *d_row_conf, const int32_t *d_row_tax, const uint8_t *d_qname,
+                   const int64_t *d_qname_off, const uint8_t *d_label, const int64_t *d_label_off, const uint8_t *d_taxlin,
+                   const int64_t *d_taxlin_off, const uint8_t *d_taxlvl, const int64_t *d_taxlvl_off, char *d_out,
+                   int64_t cap, int64_t *n_bytes);
 int hymet_lca(hymet_ctx *ctx, int mode, int32_t n_q, const int64_t *d_q_off, const int32_t *d_line_t,
               const int64_t *d_line_blen, const int64_t *d_line_qlen, const uint8_t *d_line_exact,
               const int32_t *d_ref_counts, const int32_t *d_t_tax, const int32_t *d_tax_names,

@@ -2,8 +2,8 @@
 
   * hymet_amd.screen.reduce_partials  -- screen hit counts summed, pool bottom-s merged,
     k-mer totals added (the exchange after each rank screens its own contig shard)
-  * hymet_amd.pipeline.gather_rows    -- rank 0 assembles classified_sequences.tsv rows in
-    the reference's first-PAF-appearance order from shards of any partition
+  * hymet_amd.dist.Comm.gather_rows   -- rank 0 assembles the fixed-size LCA row records of
+    every contiguous query shard in the reference's first-PAF-appearance order
   * hymet_amd.dist.Comm collectives used by bench.py (barrier, max over ranks, gathers)
 """
 import multiprocessing as mp
@@ -93,29 +93,42 @@ def _global_rows():
     has = rng.random(n) < 0.8
     first_part = rng.integers(0, 3, size=n)
     lengths = rng.integers(1000, 100000, size=n)
-    rows = {q: (f"ctg{q}", f"lin{q % 7}", "species", round(float(rng.random()), 4)) for q in range(n)}
-    expect = [rows[q] for q in sorted(np.flatnonzero(has), key=lambda q: (first_part[q], q))]
-    return has, first_part, lengths, rows, expect
+    depth = rng.integers(0, 9, size=n)
+    names = rng.integers(-1, 50, size=(n, 8))
+    conf = rng.random(n)
+    expect = sorted(np.flatnonzero(has).tolist(), key=lambda q: (first_part[q], q))
+    return has, first_part, lengths, depth, names, conf, expect
 
 
 def _gather_fn(comm):
-    from hymet_amd.dist import Comm
-    from hymet_amd.pipeline import gather_rows
-    has, first_part, lengths, rows, _ = _global_rows()
-    shard = Comm.partition_by_length(lengths, comm.world)[comm.rank]      # non-contiguous shard
-    local = [q for q in shard if has[q]]
-    # rank-local first-appearance order: by (part of first line, local position)
-    local.sort(key=lambda q: (first_part[q], q))
-    out = gather_rows(comm, [rows[q] for q in local], np.array([first_part[q] for q in local]),
-                      np.array(local, dtype=np.int64))
-    return out
+    import torch
+    has, first_part, lengths, depth, names, conf, _ = _global_rows()
+    cuts = [0, 50, 120]                                   # contiguous shards (FastaIndex.shard)
+    b, e = cuts[comm.rank], cuts[comm.rank + 1]
+    local = [q for q in range(b, e) if has[q]]
+    local.sort(key=lambda q: (first_part[q], q))          # rank-local row order (device LCA)
+    rows = {"q": torch.tensor([q - b for q in local], dtype=torch.int32),
+            "part": torch.tensor([first_part[q] for q in local], dtype=torch.int32),
+            "depth": torch.tensor([depth[q] for q in local], dtype=torch.int32),
+            "tax": torch.tensor([q * 3 for q in local], dtype=torch.int32),
+            "names": torch.tensor(names[local].reshape(-1) if local else [], dtype=torch.int32),
+            "conf": torch.tensor([conf[q] for q in local], dtype=torch.float64)}
+    out, n = comm.gather_rows(rows, b)
+    return n, {k: v.numpy() for k, v in out.items()}
 
 
 def test_gather_rows_matches_pooled_order():
     res = _run_ranks("_gather_fn")
-    *_, expect = _global_rows()
-    assert res[0] == expect
-    assert res[1] == []
+    has, first_part, lengths, depth, names, conf, expect = _global_rows()
+    n, r = res[0]
+    assert n == len(expect)
+    assert r["q"].tolist() == expect
+    assert r["part"].tolist() == [first_part[q] for q in expect]
+    assert r["depth"].tolist() == [depth[q] for q in expect]
+    assert r["tax"].tolist() == [q * 3 for q in expect]
+    np.testing.assert_array_equal(r["names"].reshape(-1, 8), names[expect])
+    assert r["conf"].tolist() == [conf[q] for q in expect]        # doubles travel bit-exact
+    assert res[1][0] == 0
 
 
 # ------------------------------------------------------------------ collectives

@@ -59,3 +59,176 @@ def test_pipeline_matches_oracle(gpu, tmp_path):
     assert res.paf == o_paf
     assert res.tsv == o_tsv
     assert res.n_classified >= 55
+
+
+def _fasta_text(w, quote_name=True):
+    """FASTA bytes as an assembler writes them: 60-column lines, some records with CRLF, a
+    comment on the header, junk before the first record, one name holding a quote."""
+    out = [b"# assembly k141\n"]
+    for i, (n, s) in enumerate(zip(w.contig_names, w.contigs)):
+        name = n + ('"x' if quote_name and i == 3 else "")
+        eol = b"\r\n" if i % 5 == 1 else b"\n"
+        out.append(b">" + name.encode() + b" flag=1 multi=2.0 len=" + str(len(s)).encode() + eol)
+        out.append(eol.join(s[j:j + 60] for j in range(0, len(s), 60)) + eol)
+    return b"".join(out)
+
+
+def test_fasta_bytes_path_matches_oracle(gpu, tmp_path):
+    """The bench's input form: FASTA text in host memory -> native record table -> one H2D
+    copy -> device line-break compaction; and csv quoting of a query name and a lineage
+    label holding '"' (written by the GPU TSV writer)."""
+    from hymet_amd import pipeline
+    from hymet_amd.seqio import from_records, parse_fasta_bytes
+    from oracle import pipeline_oracle
+    w, db, by_name, tax, hier = _setup(gpu, tmp_path)
+    hier.write_text(hier.read_text().replace("SpeciesA synthetica", 'SpeciesA "synthetica"'))
+    data = _fasta_text(w)
+    recs = [(n, s) for n, _, s in parse_fasta_bytes(data)]
+    assert len(recs) == len(w.contigs) and recs[3][0].endswith('"x')
+
+    def ref_lookup(names):
+        return from_records([(by_name[n][0], "", by_name[n][1]) for n in names])
+
+    p = pipeline.Pipeline(gpu, [db], ref_lookup, str(tax), str(hier), pipeline.Config(map_batch_bases=400_000))
+    res = p.run(data, with_paf=True)
+    o_sel, o_paf, o_tsv = pipeline_oracle.run(recs, [db],
+                                              lambda names: ([by_name[n][0] for n in names], [by_name[n][1] for n in names]),
+                                              str(tax), str(hier))
+    assert res.selected == o_sel
+    assert res.paf == o_paf
+    assert res.tsv == o_tsv
+    assert b'"SpeciesA ""synthetica""' in res.tsv or b'""synthetica""' in res.tsv
+    assert b'"k141_3""x"' in res.tsv or not any(l.startswith('k141_3"x') for l in o_paf)
+
+
+def test_legacy_variant_fused_matches_oracle(gpu, tmp_path):
+    """main.pl's classifier (classification.py) on the device PAF: superkingdom-labelled
+    hierarchy, and one contig that IS a candidate genome (same name, full length) so the
+    exact-match shortcut (:141-151) fires."""
+    from hymet_amd import classify as cls
+    from hymet_amd import pipeline
+    from hymet_amd.seqio import from_records
+    from oracle import classify_oracle, pipeline_oracle
+    w, db, by_name, tax, hier = _setup(gpu, tmp_path)
+    hier.write_text(hier.read_text().replace("domain:", "superkingdom:"))
+    names = list(w.contig_names) + [w.ref_names[0]]
+    seqs = list(w.contigs) + [w.refs[0]]
+
+    def ref_lookup(ns):
+        return from_records([(by_name[n][0], "", by_name[n][1]) for n in ns])
+
+    p = pipeline.Pipeline(gpu, [db], ref_lookup, str(tax), str(hier), pipeline.Config(), variant=cls.LEGACY)
+    res = p.run(from_records([(n, "", s) for n, s in zip(names, seqs)]), with_paf=True)
+    sel, _ = pipeline_oracle.select(seqs, [db])
+    assert res.selected == sel
+    o_paf = pipeline_oracle.map_paf([by_name[n][0] for n in sel], [by_name[n][1] for n in sel], list(zip(names, seqs)))
+    assert res.paf == o_paf
+    pf = tmp_path / "resultados.paf"
+    pf.write_text("".join(l + "\n" for l in o_paf))
+    exp = classify_oracle.classify_legacy(str(pf), str(tax), str(hier))
+    assert res.tsv == exp
+    assert (w.ref_names[0] + "\t").encode() in exp and b"\t1.0000\r\n" in exp
+
+
+def test_emit_tsv_confidence_rounding(gpu):
+    """'%.4f' on the device == Python's correctly rounded formatting, ties to even included
+    (x/32 values are exact binary ties at 4 decimals)."""
+    import csv
+    import io
+    import ctypes
+    from hymet_amd._lib import ptr
+    torch = gpu.torch
+    rng = np.random.default_rng(4)
+    conf = [0.0, 1.0, 0.03125, 0.28125, 0.59375, 0.96875, 5e-5, 0.99995, 0.12345, 0.5, 1e-300, 0.99999999]
+    conf += [j / 32 for j in range(33)] + rng.random(2000).tolist() + (rng.random(300) ** 8).tolist()
+    R = len(conf)
+    qn = [f"q{i}" for i in range(R)]
+    pool = "".join(qn).encode()
+    off = np.zeros(R + 1, np.int64)
+    np.cumsum([len(x) for x in qn], out=off[1:])
+
+    def dev(a):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(gpu.dev)
+
+    names = np.full((R, 8), -1, np.int32)
+    names[:, 0] = 0
+    d = {"q": dev(np.arange(R, dtype=np.int32)), "depth": dev(np.ones(R, np.int32)), "names": dev(names.reshape(-1)),
+         "conf": dev(np.array(conf, np.float64)), "tax": dev(np.zeros(R, np.int32))}
+    lab, lab_off = dev(np.frombuffer(b"Bacteria", np.uint8).copy()), dev(np.array([0, 8], np.int64))
+    out = gpu.empty(1 << 20, torch.uint8)
+    nb = ctypes.c_int64()
+    gpu.call("hymet_emit_tsv", 0, R, ptr(d["q"]), ptr(d["depth"]), ptr(d["names"]), ptr(d["conf"]), ptr(d["tax"]),
+             ptr(dev(np.frombuffer(pool, np.uint8).copy())), ptr(dev(off)), ptr(lab), ptr(lab_off), None, None, None, None,
+             ptr(out), 1 << 20, ctypes.byref(nb))
+    got = out[:nb.value].cpu().numpy().tobytes()
+    buf = io.StringIO(newline="")
+    wr = csv.writer(buf, delimiter="\t")
+    wr.writerows([q, "superkingdom:Bacteria", "superkingdom", f"{c:.4f}"] for q, c in zip(qn, conf))
+    assert got == buf.getvalue().encode()
+
+
+def _world2_worker(rank, port, data_path, tax, hier, q):
+    import os
+    import traceback
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        from hymet_amd import pipeline
+        from hymet_amd._lib import Gpu
+        from hymet_amd.dist import Comm
+        gpu = Gpu(0)
+        comm = Comm(rank, 2).init_backend(gpu, "gloo")
+        w, db, by_name = _w2_setup(gpu)
+        from hymet_amd.seqio import from_records
+        p = pipeline.Pipeline(gpu, [db], lambda ns: from_records([(by_name[n][0], "", by_name[n][1]) for n in ns]),
+                              tax, hier, pipeline.Config(map_batch_bases=300_000), comm)
+        data = open(data_path, "rb").read()
+        res = p.run(data, with_paf=True)
+        comm.close()
+        q.put((rank, "ok", (res.tsv, res.paf_bytes, res.selected)))
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def _w2_setup(gpu):
+    import tempfile
+    from pathlib import Path
+    w, db, by_name, _, _ = _setup(gpu, Path(tempfile.mkdtemp()))
+    return w, db, by_name
+
+
+@pytest.mark.timeout(300)
+def test_world2_pipeline_equals_world1(gpu, tmp_path):
+    """Two ranks (two processes on this GPU, gloo staging the collectives through the host):
+    each takes a contiguous half of the same FASTA; rank 0's TSV equals the one-rank TSV and
+    the ranks' PAF texts concatenate to the one-rank PAF (one index part)."""
+    import multiprocessing as mpc
+    import socket
+    from hymet_amd import pipeline
+    from hymet_amd.seqio import from_records
+    w, db, by_name, tax, hier = _setup(gpu, tmp_path)
+    data = _fasta_text(w, quote_name=False)
+    dp = tmp_path / "pool.fna"
+    dp.write_bytes(data)
+    p = pipeline.Pipeline(gpu, [db], lambda ns: from_records([(by_name[n][0], "", by_name[n][1]) for n in ns]),
+                          str(tax), str(hier), pipeline.Config(map_batch_bases=300_000))
+    one = p.run(data, with_paf=True)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mpc.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_world2_worker, args=(r, port, str(dp), str(tax), str(hier), q)) for r in range(2)]
+    for x in ps:
+        x.start()
+    got = {}
+    for _ in range(2):
+        r, st, out = q.get(timeout=240)
+        assert st == "ok", out
+        got[r] = out
+    for x in ps:
+        x.join(timeout=60)
+    assert got[0][2] == one.selected == got[1][2]
+    assert got[0][0] == one.tsv
+    assert got[1][0] == b""
+    assert got[0][1] + got[1][1] == one.paf_bytes
