@@ -58,7 +58,7 @@ _SIGS = {
     "hymet_emit_paf": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _c.POINTER(_i64), _vp]),
     "hymet_acc_ref_counts": (_i32, [_vp, _vp, _vp]),
     "hymet_acc_classify": (_i32, [_vp, _vp, _i32, _i32] + [_vp] * 15 + [_c.POINTER(_i32)]),
-    "hymet_emit_tsv": (_i32, [_vp, _i32, _i32] + [_vp] * 15 + [_i64, _c.POINTER(_i64)]),
+    "hymet_emit_tsv": (_i32, [_vp, _i32, _i32] + [_vp] * 14 + [_i64, _c.POINTER(_i64)]),
     "hymet_mm_chain_dp": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _c.c_float, _c.c_float, _vp, _vp]),
     "hymet_lca_ref_counts": (_i32, [_vp, _vp, _i64, _vp]),
     "hymet_lca": (_i32, [_vp, _i32, _i32] + [_vp] * 17),

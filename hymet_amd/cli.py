@@ -126,7 +126,7 @@ def map_paf(gpu, refs, queries, split_idx: str = "2g", mini_batch: float = 50e6,
     """minimap2 -I<split_idx> index of `refs` + `-x asm10` mapping of `queries` -> PAF lines
     in minimap2's order (index part by part; queries in input order within a part)."""
     from . import mapper as mp
-    from .pipeline import _batches
+    from .ingest import _batches
     from .seqio import DevicePool
     parts = mp.split_parts(refs.lengths, float(mp.parse_num(split_idx)), mini_batch)
     batches = []

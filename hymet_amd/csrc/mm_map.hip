@@ -1451,6 +1451,29 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
         if (rc) return rc;
     }
     tr.mark("anchors+sort");
+    // HYMET_DUMP_ANCHORS=path (profiling, tools/chain_prof): the first call's sorted first-pass
+    // anchors as (x, y) pairs with x>>32 replaced by the (query, strand, target) group ordinal
+    if (const char *dump = getenv("HYMET_DUMP_ANCHORS")) {
+        static bool dumped = false;
+        if (!dumped && S1.n > 0) {
+            dumped = true;
+            const int64_t nd = std::min<int64_t>(S1.n, 1 << 24);
+            std::vector<uint64_t> hx(nd), hy(nd), hk(nd);
+            HY_HIP(hipMemcpyAsync(hx.data(), S1.ax.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
+            HY_HIP(hipMemcpyAsync(hy.data(), S1.ay.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
+            HY_HIP(hipMemcpyAsync(hk.data(), S1.k1.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
+            HY_HIP(hipStreamSynchronize(st));
+            if (FILE *fp = fopen(dump, "wb")) {
+                uint64_t gid = 0;
+                for (int64_t a = 0; a < nd; a++) {
+                    if (a && (hk[a] >> S1.gshift) != (hk[a - 1] >> S1.gshift)) gid++;
+                    const uint64_t v[2] = {gid << 32 | (uint32_t)hx[a], hy[a]};
+                    fwrite(v, 8, 2, fp);
+                }
+                fclose(fp);
+            }
+        }
+    }
     // ------------------------------------------------ 6 chain (+ 7 long join)
     ChainSet C1;
     rc = chain_set(ctx, opt, pen_gap, pen_skip, opt->bw, S1, n_q, C1);

@@ -47,3 +47,19 @@ def test_library_is_built_from_these_sources():
     on the build host and on the GPU box alike."""
     from hymet_amd import build
     assert build.is_current(), "libhymet_gpu.so is stale: run python -m hymet_amd.build"
+
+
+def test_binding_arity_matches_header():
+    """Every ctypes signature in hymet_amd/_lib.py has the parameter count its prototype in
+    include/hymet_gpu.h declares (a mismatch would pass garbage through the boundary)."""
+    from hymet_amd._lib import _SIGS
+    txt = re.sub(r"/\*.*?\*/", "", (ROOT / "include" / "hymet_gpu.h").read_text(), flags=re.S)
+    bad = []
+    for name, (_, args) in _SIGS.items():
+        m = re.search(r"\b" + name + r"\s*\((.*?)\);", txt, re.S)
+        assert m, name
+        body = m.group(1).strip()
+        n = 0 if body in ("", "void") else len(body.split(","))
+        if n != len(args):
+            bad.append((name, n, len(args)))
+    assert not bad, bad
