@@ -43,6 +43,8 @@ _SIGS = {
     "hymet_mm_index_destroy": (_i32, [_vp]),
     "hymet_mm_index_info": (_i32, [_vp, _c.POINTER(_i32), _c.POINTER(_i32), _c.POINTER(_i32), _c.POINTER(_i64)]),
     "hymet_mm_index_max_occ": (_i32, [_vp, _vp, _c.c_float, _c.POINTER(_i32)]),
+    "hymet_mm_index_save": (_i32, [_vp, _vp, _c.c_char_p, _i32, _c.POINTER(_i64)]),
+    "hymet_mm_index_load": (_i32, [_vp, _c.c_char_p, _i64, _c.POINTER(_vp), _c.POINTER(_i64)]),
     "hymet_mm_index_export": (_i32, [_vp, _vp, _vp, _vp]),
     "hymet_mm_map": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _c.POINTER(_vp)]),
     "hymet_mm_result_size": (_i32, [_vp, _c.POINTER(_i64)]),

@@ -23,7 +23,6 @@ from __future__ import annotations
 
 import argparse
 import glob
-import json
 import logging
 import os
 import sys
@@ -118,66 +117,88 @@ def cmd_limit(argv: Sequence[str]) -> int:
 
 
 # ------------------------------------------------------------------ map (minimap2.sh)
-INDEX_MAGIC = "hymet-amd-mm-index/1"
-
-
-def map_paf(gpu, refs, queries, split_idx: str = "2g", mini_batch: float = 50e6, batch_bases: int = 40_000_000,
-            w: int = 10, k: int = 15) -> List[str]:
-    """minimap2 -I<split_idx> index of `refs` + `-x asm10` mapping of `queries` -> PAF lines
-    in minimap2's order (index part by part; queries in input order within a part)."""
+def build_parts(gpu, refs, split_idx: str = "2g", mini_batch: float = 50e6, w: int = 10, k: int = 15):
+    """minimap2 -I<split_idx> -d: the device index, one part per <= split_idx bases."""
     from . import mapper as mp
-    from .ingest import _batches
-    from .seqio import DevicePool
-    parts = mp.split_parts(refs.lengths, float(mp.parse_num(split_idx)), mini_batch)
-    batches = []
-    for b0, b1 in _batches(queries.lengths, batch_bases):
-        sub = queries if (b0 == 0 and b1 == queries.n) else queries.subset(range(b0, b1))
-        batches.append((b0, sub, DevicePool(gpu, sub, DevicePool.ALPHA_MINIMAP2)))
-    out: List[str] = []
-    opt = None
-    for p in parts:
-        sub = refs.subset(p) if len(parts) > 1 else refs
-        part = mp.IndexPart(gpu, sub, w, k)
-        if opt is None:
-            opt = mp.MapOpt.asm10()
-            opt.resolve_mid_occ(part)          # mm_mapopt_update on the first part
-        for b0, qs, qp in batches:
-            res = mp.map_part(gpu, part, qp, opt)
-            for q in np.flatnonzero(np.diff(res.off)):
-                q = int(q)
-                out.extend(mp.paf_lines(qs.names[q], int(qs.lengths[q]), res.query(q), int(res.rep_len[q]),
-                                        part.names, part.lens))
-        part.close()
-    return out
+    parts_idx = mp.split_parts(refs.lengths, float(mp.parse_num(split_idx)), mini_batch)
+    parts, first = [], []
+    for p in parts_idx:
+        sub = refs.subset(p) if len(parts_idx) > 1 else refs
+        parts.append(mp.IndexPart(gpu, sub, w, k))
+        first.append(int(p[0]))
+    return parts, list(refs.names), refs.lengths, first
+
+
+def read_query_files(paths: Sequence[str]) -> bytes:
+    """The pooled input/*.fna as one FASTA text, file order kept; bytes before a file's
+    first record are skipped (kseq does) and files are joined on a line break."""
+    out = []
+    for p in paths:
+        with open(p, "rb") as f:
+            d = f.read()
+        if p.endswith(".gz") or d[:2] == b"\x1f\x8b":
+            import gzip
+            d = gzip.decompress(d)
+        if not d.startswith(b">"):
+            i = d.find(b"\n>")
+            d = d[i + 1:] if i >= 0 else b""
+        if d and not d.endswith(b"\n"):
+            d += b"\n"
+        out.append(d)
+    return b"".join(out)
+
+
+def map_paf(gpu, parts, names, lens, first, query_fasta: bytes, batch_bases: int = 40_000_000) -> bytes:
+    """`-x asm10` mapping of the pooled queries against the index parts -> resultados.paf
+    bytes in minimap2's order (part by part; queries in input order within a part), through
+    the fused path's device kernels (records accumulated in HBM, text written on the GPU)."""
+    from . import pipeline
+    from .ingest import FastaIndex, QueryShard
+    ix = pipeline.make_index_set(gpu, names, lens, parts, first)
+    fx = FastaIndex(query_fasta)
+    sh = QueryShard.from_fasta(gpu, fx, 0, fx.n, batch_bases)
+    acc = pipeline.PafAcc(gpu)
+    pipeline.map_shard(gpu, ix, sh, acc)
+    return pipeline.emit_paf_bytes(gpu, ix, sh, acc, {})
 
 
 def cmd_map(argv: Sequence[str]) -> int:
+    """scripts/minimap2.sh: build the index unless INDEX_PATH is non-empty (:10-19), then map
+    input/*.fna with asm10 (:23).  The device index is persisted as INDEX_PATH.hymet beside a
+    manifest in INDEX_PATH, so a warm call only loads it (no sketching, no sorting)."""
     if len(argv) != 4:
         print("usage: map INPUT_DIR REFERENCE_FASTA INDEX_PATH PAF_OUT", file=sys.stderr)
         return 2
     input_dir, ref_fasta, index_path, paf_out = argv
+    from . import mapper as mp
     from ._lib import Gpu
     from .seqio import read_fasta
     split = os.environ.get("SPLIT_IDX", "2g")
+    cached = os.path.exists(index_path) and os.path.getsize(index_path) > 0
     try:
-        if not (os.path.exists(index_path) and os.path.getsize(index_path) > 0):
+        gpu = Gpu(int(os.environ.get("HYMET_DEVICE", "0")))
+        loaded = None
+        if not cached:
             print("Creating index with minimap2...")
-            # The device index is rebuilt from the reference FASTA on every run (seconds
-            # on the GPU); the file records what it was built from, so the reference's
-            # "[ -s reference.mmi ]" cache test keeps its meaning.
-            st = os.stat(ref_fasta)
-            with open(index_path, "w") as f:
-                json.dump({"format": INDEX_MAGIC, "reference": os.path.abspath(ref_fasta), "size": st.st_size,
-                           "split_idx": split, "k": 15, "w": 10}, f)
-                f.write("\n")
         else:
             print(f"Using cached minimap2 index: {index_path}")
-        print("Running alignment with minimap2...")
-        gpu = Gpu(int(os.environ.get("HYMET_DEVICE", "0")))
-        refs = read_fasta([ref_fasta])
-        queries = read_fasta(_fna_files(input_dir))
-        lines = map_paf(gpu, refs, queries, split)
-        _write_lines(paf_out, lines)
+            loaded = mp.load_index(gpu, index_path)
+        if loaded is None:   # fresh, or a CPU minimap2 .mmi we keep untouched: build in HBM
+            # HYMET_INDEX_MINI_BATCH: the index reader's mini-batch (minimap2's 50 Mbp chunking)
+            mini = float(os.environ.get("HYMET_INDEX_MINI_BATCH", "50e6"))
+            parts, names, lens, first = build_parts(gpu, read_fasta([ref_fasta]), split, mini)
+            if not cached:
+                mp.save_index(index_path, parts, names, lens, first, ref_fasta, split)
+        else:
+            parts, names, lens, first = loaded
+    except Exception as e:  # minimap2.sh:13-16
+        print(f"Error creating index with minimap2. ({e})")
+        return 1
+    print("Running alignment with minimap2...")
+    try:
+        data = map_paf(gpu, parts, names, lens, first, read_query_files(_fna_files(input_dir)))
+        with open(paf_out, "wb") as f:
+            f.write(data)
     except Exception as e:  # minimap2.sh:25-29
         print(f"Error running alignment with minimap2. ({e})")
         return 1

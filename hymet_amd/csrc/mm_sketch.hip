@@ -18,6 +18,9 @@
 // two adjacent loads instead of a hash-table probe chain.
 #include "mm_common.hpp"
 
+#include <cstdio>
+#include <cstring>
+
 namespace hymet {
 namespace mm {
 namespace {
@@ -387,6 +390,115 @@ int hymet_mm_index_max_occ(hymet_ctx *ctx, const hymet_mm_index *idx, float frac
     }
     HY_ARG(val < cap, "hymet_mm_index_max_occ: occurrence above histogram range");
     *out = val + 1;
+    return HYMET_OK;
+}
+
+// ------------------------------------------------------- persisted index (minimap2.sh:10)
+// A part on disk: "HYMETIX1", int32 w, k, n_seq, pad, int64 n_pos, int64 len[n_seq],
+// uint32 bucket[n_pos], uint64 pos[n_pos] (sorted by (bucket, pos) as in HBM).  The direct-
+// address offsets are rebuilt on load from the sorted buckets (no sort, no sketch).
+static const char kIxMagic[8] = {'H', 'Y', 'M', 'E', 'T', 'I', 'X', '1'};
+
+int hymet_mm_index_save(hymet_ctx *ctx, const hymet_mm_index *idx, const char *path, int append, int64_t *end_offset) {
+    HY_ARG(ctx && idx && path, "hymet_mm_index_save: null argument");
+    HY_HIP(hipSetDevice(ctx->device));
+    FILE *fp = fopen(path, append ? "ab" : "wb");
+    if (!fp) return fail(HYMET_E_ARG, std::string("hymet_mm_index_save: cannot open ") + path);
+    const int32_t hdr[4] = {idx->w, idx->k, idx->n_seq, 0};
+    const int64_t n = idx->n_pos;
+    bool ok = fwrite(kIxMagic, 1, 8, fp) == 8 && fwrite(hdr, 4, 4, fp) == 4 && fwrite(&n, 8, 1, fp) == 1 &&
+              (idx->n_seq == 0 || fwrite(idx->h_len.data(), 8, (size_t)idx->n_seq, fp) == (size_t)idx->n_seq);
+    const int64_t chunk = 1 << 24;
+    std::vector<uint64_t> buf;
+    for (int pass = 0; ok && pass < 2; pass++) {  // buckets, then positions, streamed in chunks
+        const size_t es = pass == 0 ? 4 : 8;
+        buf.resize((size_t)std::min<int64_t>(n, chunk) + 1);
+        for (int64_t a = 0; ok && a < n; a += chunk) {
+            const int64_t m = std::min<int64_t>(chunk, n - a);
+            const void *src = pass == 0 ? (const void *)(idx->d_hash + a) : (const void *)(idx->d_pos + a);
+            if (hipMemcpy(buf.data(), src, es * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess) {
+                fclose(fp);
+                return fail(HYMET_E_HIP, "hymet_mm_index_save: copy");
+            }
+            ok = fwrite(buf.data(), es, (size_t)m, fp) == (size_t)m;
+        }
+    }
+    if (end_offset) *end_offset = (int64_t)ftell(fp);
+    if (fclose(fp) != 0 || !ok) return fail(HYMET_E_ARG, std::string("hymet_mm_index_save: write failed: ") + path);
+    return HYMET_OK;
+}
+
+__global__ void koff_gap_kernel(const uint32_t *__restrict__ hash, int64_t n, uint32_t *__restrict__ koff) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t prev = i ? (int64_t)hash[i - 1] : -1;
+    for (int64_t b = prev + 1; b <= (int64_t)hash[i]; b++) koff[b] = (uint32_t)i;  // first entry of buckets (prev, h]
+}
+
+__global__ void koff_tail_kernel(int64_t from, int64_t to, uint32_t v, uint32_t *__restrict__ koff) {
+    for (int64_t b = from + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b <= to; b += (int64_t)gridDim.x * blockDim.x)
+        koff[b] = v;
+}
+
+int hymet_mm_index_load(hymet_ctx *ctx, const char *path, int64_t offset, hymet_mm_index **out, int64_t *end_offset) {
+    HY_ARG(ctx && path && out, "hymet_mm_index_load: null argument");
+    HY_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    FILE *fp = fopen(path, "rb");
+    if (!fp) return fail(HYMET_E_ARG, std::string("hymet_mm_index_load: cannot open ") + path);
+    char mg[8];
+    int32_t hdr[4];
+    int64_t n = 0;
+    if (fseeko(fp, offset, SEEK_SET) != 0 || fread(mg, 1, 8, fp) != 8 || memcmp(mg, kIxMagic, 8) != 0 ||
+        fread(hdr, 4, 4, fp) != 4 || fread(&n, 8, 1, fp) != 1 || hdr[1] < 1 || hdr[1] > 15 || hdr[2] < 0 || n < 0 ||
+        n >= (1ll << 32)) {
+        fclose(fp);
+        return fail(HYMET_E_ARG, std::string("hymet_mm_index_load: not a hymet index part: ") + path);
+    }
+    hymet_mm_index *idx = new hymet_mm_index();
+    idx->w = hdr[0], idx->k = hdr[1], idx->n_seq = hdr[2], idx->n_pos = n, idx->n_buckets = 1ll << (2 * hdr[1]);
+    idx->device = ctx->device;
+    idx->h_len.resize(idx->n_seq);
+    auto bad = [&](int code, const char *what) {
+        fclose(fp);
+        hymet_mm_index_destroy(idx);
+        return fail(code, std::string("hymet_mm_index_load: ") + what);
+    };
+    if (idx->n_seq && fread(idx->h_len.data(), 8, (size_t)idx->n_seq, fp) != (size_t)idx->n_seq) return bad(HYMET_E_ARG, "truncated");
+    const int64_t nb = idx->n_buckets;
+    if (hipMalloc(&idx->d_koff, 4 * (size_t)(nb + 1)) != hipSuccess || hipMalloc(&idx->d_pos, 8 * (size_t)(n + 1)) != hipSuccess ||
+        hipMalloc(&idx->d_hash, 4 * (size_t)(n + 1)) != hipSuccess || hipMalloc(&idx->d_len, 8 * (size_t)(idx->n_seq + 1)) != hipSuccess)
+        return bad(HYMET_E_HIP, "out of device memory");
+    if (idx->n_seq && hipMemcpy(idx->d_len, idx->h_len.data(), 8 * (size_t)idx->n_seq, hipMemcpyHostToDevice) != hipSuccess)
+        return bad(HYMET_E_HIP, "copy lengths");
+    const int64_t chunk = 1 << 24;
+    std::vector<uint64_t> buf((size_t)std::min<int64_t>(std::max<int64_t>(n, 1), chunk));
+    for (int pass = 0; pass < 2; pass++) {
+        const size_t es = pass == 0 ? 4 : 8;
+        for (int64_t a = 0; a < n; a += chunk) {
+            const int64_t m = std::min<int64_t>(chunk, n - a);
+            if (fread(buf.data(), es, (size_t)m, fp) != (size_t)m) return bad(HYMET_E_ARG, "truncated");
+            void *dst = pass == 0 ? (void *)(idx->d_hash + a) : (void *)(idx->d_pos + a);
+            if (hipMemcpy(dst, buf.data(), es * (size_t)m, hipMemcpyHostToDevice) != hipSuccess) return bad(HYMET_E_HIP, "copy");
+        }
+    }
+    if (end_offset) *end_offset = (int64_t)ftello(fp);
+    fclose(fp);
+    // offsets: koff[b] = first entry of bucket >= b; koff[nb] = n
+    if (n > 0) {
+        uint32_t last = 0;
+        if (hipMemcpy(&last, idx->d_hash + n - 1, 4, hipMemcpyDeviceToHost) != hipSuccess) return bad(HYMET_E_HIP, "copy");
+        hipLaunchKernelGGL(koff_gap_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, idx->d_hash, n, idx->d_koff);
+        hipLaunchKernelGGL(koff_tail_kernel, dim3(ctx->n_cu * 8), dim3(256), 0, st, (int64_t)last + 1, nb, (uint32_t)n,
+                           idx->d_koff);
+    } else {
+        hipLaunchKernelGGL(koff_tail_kernel, dim3(ctx->n_cu * 8), dim3(256), 0, st, (int64_t)0, nb, 0u, idx->d_koff);
+    }
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+        hymet_mm_index_destroy(idx);
+        return fail(HYMET_E_HIP, "hymet_mm_index_load: offsets kernel");
+    }
+    *out = idx;
     return HYMET_OK;
 }
 

@@ -140,6 +140,32 @@ class IndexPart:
         check(gpu.lib.hymet_mm_index_info(self.h, None, None, None, _c.byref(n_pos)), "hymet_mm_index_info")
         self.n_pos = n_pos.value
 
+    @classmethod
+    def load(cls, gpu, path: str, offset: int, names, lens, w: int = 10, k: int = 15):
+        """A part persisted by save() (hymet_mm_index_load: no sketch, no sort)."""
+        self = cls.__new__(cls)
+        self.gpu, self.w, self.k = gpu, w, k
+        self.names = list(names)
+        self.lens = np.ascontiguousarray(lens, dtype=np.int64)
+        h = _c.c_void_p()
+        end = _c.c_int64()
+        gpu.call("hymet_mm_index_load", str(path).encode(), int(offset), _c.byref(h), _c.byref(end))
+        self.h = h
+        n_pos, n_seq = _c.c_int64(), _c.c_int32()
+        check(gpu.lib.hymet_mm_index_info(self.h, None, None, _c.byref(n_seq), _c.byref(n_pos)), "hymet_mm_index_info")
+        if n_seq.value != len(self.names):
+            self.close()
+            raise ValueError(f"{path}: index part has {n_seq.value} sequences, manifest lists {len(self.names)}")
+        self.n_pos = n_pos.value
+        self.end_offset = end.value
+        return self
+
+    def save(self, path: str, append: bool) -> int:
+        """Append (or write) this part to a persisted index file; returns the end offset."""
+        end = _c.c_int64()
+        self.gpu.call("hymet_mm_index_save", self.h, str(path).encode(), int(append), _c.byref(end))
+        return end.value
+
     def max_occ(self, frac: float = 2e-4) -> int:
         out = _c.c_int32()
         self.gpu.call("hymet_mm_index_max_occ", self.h, _c.c_float(frac), _c.byref(out))
@@ -161,6 +187,57 @@ class IndexPart:
             self.close()
         except Exception:
             pass
+
+
+INDEX_FORMAT = "hymet-amd-gpu-index/2"
+
+
+def save_index(path_mmi: str, parts: List["IndexPart"], names, lens, part_first, ref_fasta: str, split: str):
+    """Persist the device index beside reference.mmi (minimap2.sh:10-19 caches the index):
+    the binary parts go to PATH.hymet (a distinct name, so a CPU minimap2 .mmi is never
+    clobbered) and PATH itself holds the manifest -- non-empty, so the script's `[ -s ]`
+    cache test keeps its meaning."""
+    import json
+    import os
+    data = str(path_mmi) + ".hymet"
+    offs = [0]
+    for i, p in enumerate(parts):
+        offs.append(p.save(data, append=i > 0))
+    st = os.stat(ref_fasta) if ref_fasta and os.path.exists(ref_fasta) else None
+    man = {"format": INDEX_FORMAT, "data": os.path.basename(data), "part_offsets": offs[:-1], "part_first": list(part_first),
+           "names": list(names), "lens": [int(x) for x in lens], "w": parts[0].w if parts else 10,
+           "k": parts[0].k if parts else 15, "split_idx": split,
+           "reference": os.path.abspath(ref_fasta) if ref_fasta else None,
+           "reference_size": st.st_size if st else None, "reference_mtime": st.st_mtime if st else None}
+    tmp = str(path_mmi) + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(man, f)
+        f.write("\n")
+    os.replace(tmp, path_mmi)
+
+
+def load_index(gpu, path_mmi: str):
+    """(parts, names, lens, part_first) of a persisted index, or None when PATH is not one
+    of ours (e.g. a real minimap2 .mmi) or its data file is missing."""
+    import json
+    import os
+    try:
+        with open(path_mmi, "r") as f:
+            man = json.loads(f.readline())
+    except (OSError, ValueError, UnicodeDecodeError):
+        return None
+    if not isinstance(man, dict) or man.get("format") != INDEX_FORMAT:
+        return None
+    data = os.path.join(os.path.dirname(os.path.abspath(path_mmi)), man["data"])
+    if not os.path.exists(data):
+        return None
+    names, lens, first = man["names"], np.asarray(man["lens"], np.int64), man["part_first"]
+    parts = []
+    for i, off in enumerate(man["part_offsets"]):
+        b = first[i]
+        e = first[i + 1] if i + 1 < len(first) else len(names)
+        parts.append(IndexPart.load(gpu, data, off, names[b:e], lens[b:e], man["w"], man["k"]))
+    return parts, names, lens, first
 
 
 def sketch(gpu, pool: DevicePool, w: int = 10, k: int = 15, rid_mode: int = 0):

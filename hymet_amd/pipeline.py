@@ -115,6 +115,82 @@ class PafAcc:
             pass
 
 
+def make_index_set(gpu, names, lens, parts, first) -> IndexSet:
+    """An index set ready to map: a fresh `minimap2 -x asm10` process per run resolves
+    mid_occ from the first part of THIS index (options.c mm_mapopt_update), so the options
+    live with the set; target names and lengths go to HBM for the PAF writer."""
+    torch = gpu.torch
+    opt = mp.MapOpt.asm10()
+    opt.resolve_mid_occ(parts[0])
+    ix = IndexSet(list(names), np.asarray(lens, np.int64), list(parts), list(first), opt)
+    tb = [n.encode() for n in ix.names]
+    toff = np.zeros(len(tb) + 1, np.int64)
+    np.cumsum([len(b) for b in tb], out=toff[1:])
+    ix.dev = {"tname": torch.frombuffer(bytearray(b"".join(tb) or b"\0"), dtype=torch.uint8).to(gpu.dev),
+              "tname_off": torch.from_numpy(toff).to(gpu.dev),
+              "tlen": torch.from_numpy(ix.lens.copy()).to(gpu.dev)}
+    return ix
+
+
+def map_shard(gpu, ix: IndexSet, sh: QueryShard, acc: PafAcc) -> int:
+    """minimap2 -x asm10 of every query batch against every part, appended to the device
+    PAF in minimap2's order (part-major, queries in input order)."""
+    acc.reset()
+    starts = np.ascontiguousarray(sh.starts, np.int64)
+    lens = np.ascontiguousarray(sh.lengths, np.int64)
+    hbase = sh.name_hash.data_ptr()
+    for pi, part in enumerate(ix.parts):
+        for b0, b1 in sh.batches:
+            n = b1 - b0
+            if n <= 0:
+                continue
+            gpu.call("hymet_mm_map_acc", part.h, _c.byref(ix.opt), ptr(sh.mm.w2b), ptr(sh.mm.wmask),
+                     _c.c_void_p(starts.ctypes.data + 8 * b0), _c.c_void_p(lens.ctypes.data + 8 * b0),
+                     _c.c_void_p(hbase + 4 * b0), n, b0, pi, ix.part_first[pi], acc.h)
+    return acc.n
+
+
+def _dev_buf(gpu, bufs, key, nbytes):
+    """A reusable device byte buffer of at least nbytes."""
+    b = bufs.get(key)
+    if b is None or b.numel() < nbytes:
+        bufs.pop(key, None)
+        b = gpu.empty(max(int(nbytes), 16), gpu.torch.uint8)
+        bufs[key] = b
+    return b
+
+
+def _to_host(gpu, bufs, key, dev, n) -> bytes:
+    """D2H of n bytes through a reusable pinned host buffer."""
+    if n == 0:
+        return b""
+    h = bufs.get(key)
+    if h is None or h.numel() < n:
+        h = gpu.torch.empty(int(n * 1.25) + 4096, dtype=gpu.torch.uint8, pin_memory=True)
+        bufs[key] = h
+    h[:n].copy_(dev[:n])
+    return h[:n].numpy().tobytes()
+
+
+def emit_paf_bytes(gpu, ix: IndexSet, sh: QueryShard, acc: PafAcc, bufs) -> bytes:
+    """resultados.paf text of the accumulator (written on the device, copied out once)."""
+    n = acc.n
+    if n == 0:
+        return b""
+    nb = _c.c_int64()
+    cap = 200 * n
+    while True:
+        out = _dev_buf(gpu, bufs, "paf", cap)
+        rc = gpu.lib.hymet_emit_paf(gpu.ctx, acc.h, ptr(sh.qname), ptr(sh.qname_off), ptr(sh.qlen), ptr(ix.dev["tname"]),
+                                    ptr(ix.dev["tname_off"]), ptr(ix.dev["tlen"]), ptr(out), cap, _c.byref(nb), None)
+        if rc == -3:
+            cap = nb.value
+            continue
+        check(rc, "hymet_emit_paf")
+        break
+    return _to_host(gpu, bufs, "paf_h", out, nb.value)
+
+
 class Pipeline:
     def __init__(self, gpu, dbs: Sequence[SketchDB], ref_lookup, taxonomy, hierarchy, cfg: Config = None, comm=None,
                  variant: int = cls.CAMI):
@@ -191,39 +267,13 @@ class Pipeline:
             sub = refs.subset(p) if len(parts_idx) > 1 else refs
             parts.append(mp.IndexPart(self.gpu, sub, self.cfg.w, self.cfg.k))
             first.append(int(p[0]))
-        # a fresh `minimap2 -x asm10` process per run: mm_mapopt_update resolves mid_occ from
-        # the first part of THIS index (options.c), so the options live with the index set
-        opt = mp.MapOpt.asm10()
-        opt.resolve_mid_occ(parts[0])
-        ix = IndexSet(list(refs.names), np.asarray(refs.lengths, np.int64), parts, first, opt)
-        torch = self.gpu.torch
-        tb = [n.encode() for n in ix.names]
-        toff = np.zeros(len(tb) + 1, np.int64)
-        np.cumsum([len(b) for b in tb], out=toff[1:])
-        ix.dev = {"tname": torch.frombuffer(bytearray(b"".join(tb) or b"\0"), dtype=torch.uint8).to(self.gpu.dev),
-                  "tname_off": torch.from_numpy(toff).to(self.gpu.dev),
-                  "tlen": torch.from_numpy(ix.lens.copy()).to(self.gpu.dev)}
+        ix = make_index_set(self.gpu, list(refs.names), refs.lengths, parts, first)
         self.index_cache = {key: ix}  # one cached candidate set, like the sha1 cache dir
         return ix
 
     def map_all(self, ix: IndexSet, sh: QueryShard) -> int:
-        """minimap2 -x asm10 of every query batch against every part, appended to the
-        device PAF in minimap2's order (part-major, queries in input order)."""
         self.opt = ix.opt
-        self.acc.reset()
-        gpu = self.gpu
-        starts = np.ascontiguousarray(sh.starts, np.int64)
-        lens = np.ascontiguousarray(sh.lengths, np.int64)
-        hbase = sh.name_hash.data_ptr()
-        for pi, part in enumerate(ix.parts):
-            for b0, b1 in sh.batches:
-                n = b1 - b0
-                if n <= 0:
-                    continue
-                gpu.call("hymet_mm_map_acc", part.h, _c.byref(ix.opt), ptr(sh.mm.w2b), ptr(sh.mm.wmask),
-                         _c.c_void_p(starts.ctypes.data + 8 * b0), _c.c_void_p(lens.ctypes.data + 8 * b0),
-                         _c.c_void_p(hbase + 4 * b0), n, b0, pi, ix.part_first[pi], self.acc.h)
-        return self.acc.n
+        return map_shard(self.gpu, ix, sh, self.acc)
 
     def classify_rows(self, ix: IndexSet, sh: QueryShard):
         """ref_counts (all-reduced) + device LCA over the accumulator -> row tensors."""
@@ -270,45 +320,13 @@ class Pipeline:
 
     def emit_paf(self, ix: IndexSet, sh: QueryShard) -> bytes:
         """This rank's resultados.paf text (its queries' lines, part-major)."""
-        gpu = self.gpu
-        n = self.acc.n
-        if n == 0:
-            return b""
-        nb = _c.c_int64()
-        cap = 200 * n
-        while True:
-            out = self._dev_buf("paf", cap)
-            rc = gpu.lib.hymet_emit_paf(gpu.ctx, self.acc.h, ptr(sh.qname), ptr(sh.qname_off), ptr(sh.qlen),
-                                        ptr(ix.dev["tname"]), ptr(ix.dev["tname_off"]), ptr(ix.dev["tlen"]), ptr(out), cap,
-                                        _c.byref(nb), None)
-            if rc == -3:
-                cap = nb.value
-                continue
-            check(rc, "hymet_emit_paf")
-            break
-        return self._to_host("paf_h", out, nb.value)
+        return emit_paf_bytes(self.gpu, ix, sh, self.acc, self._bufs)
 
     def _dev_buf(self, key, nbytes):
-        """A reusable device byte buffer of at least nbytes."""
-        torch = self.gpu.torch
-        b = self._bufs.get(key)
-        if b is None or b.numel() < nbytes:
-            self._bufs.pop(key, None)
-            b = self.gpu.empty(max(int(nbytes), 16), torch.uint8)
-            self._bufs[key] = b
-        return b
+        return _dev_buf(self.gpu, self._bufs, key, nbytes)
 
     def _to_host(self, key, dev, n) -> bytes:
-        """D2H of n bytes through a reusable pinned host buffer."""
-        torch = self.gpu.torch
-        if n == 0:
-            return b""
-        h = self._bufs.get(key)
-        if h is None or h.numel() < n:
-            h = torch.empty(int(n * 1.25) + 4096, dtype=torch.uint8, pin_memory=True)
-            self._bufs[key] = h
-        h[:n].copy_(dev[:n])
-        return h[:n].numpy().tobytes()
+        return _to_host(self.gpu, self._bufs, key, dev, n)
 
     # ------------------------------------------------------------------- run
     def run(self, queries, with_paf=False) -> RunResult:
@@ -345,7 +363,7 @@ class Pipeline:
         if self._bufs.get("names_of") is not fx:
             torch = self.gpu.torch
             pool, off = fx.name_pool()
-            self._bufs["names"] = (torch.frombuffer(bytearray(pool or b"\0"), dtype=torch.uint8).to(self.gpu.dev),
+            self._bufs["names"] = (torch.from_numpy(pool.copy() if len(pool) else np.zeros(1, np.uint8)).to(self.gpu.dev),
                                    torch.from_numpy(off).to(self.gpu.dev))
             self._bufs["names_of"] = fx
         return self._bufs["names"]

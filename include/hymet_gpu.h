@@ -137,6 +137,12 @@ int hymet_mm_index_destroy(hymet_mm_index *idx);
 int hymet_mm_index_info(const hymet_mm_index *idx, int32_t *w, int32_t *k, int32_t *n_seq, int64_t *n_pos);
 /* index.c mm_idx_cal_max_occ: the occurrence threshold for a fraction f (-f 2e-4) */
 int hymet_mm_index_max_occ(hymet_ctx *ctx, const hymet_mm_index *idx, float frac, int32_t *out);
+/* The GPU index persisted beside reference.mmi (minimap2.sh:10 reuses a non-empty index):
+ * save writes (append != 0: appends) one part -- header, sequence lengths, the sorted
+ * (bucket, y) arrays -- and reports the file offset after it; load reads the part at
+ * `offset` and rebuilds the direct-address offsets on the device (no sketching, no sort). */
+int hymet_mm_index_save(hymet_ctx *ctx, const hymet_mm_index *idx, const char *path, int append, int64_t *end_offset);
+int hymet_mm_index_load(hymet_ctx *ctx, const char *path, int64_t offset, hymet_mm_index **out, int64_t *end_offset);
 /* sorted (bucket = minimizer hash, y) arrays, n_pos entries each (tests / persistence) */
 int hymet_mm_index_export(hymet_ctx *ctx, const hymet_mm_index *idx, uint32_t *h_hash, uint64_t *h_pos);
 

@@ -131,9 +131,14 @@ def test_screen_map_classify_dropins_match_oracle(tmp_path, capsys):
     assert "Creating index with minimap2..." in capsys.readouterr().out and mmi.stat().st_size > 0
     o_paf = pipeline_oracle.map_paf([n for n, _ in chosen], [s for _, s in chosen], recs)
     assert paf.read_text().splitlines() == o_paf
+    assert (tmp_path / "reference.mmi.hymet").stat().st_size > 0
+    # warm call: the persisted device index is loaded; like minimap2 with a prebuilt .mmi it
+    # never reads the reference FASTA again (moved away here)
+    ref_fa.rename(tmp_path / "moved.fasta")
     assert cli(["map", str(inp), str(ref_fa), str(mmi), str(paf)]) == 0
     assert "Using cached minimap2 index" in capsys.readouterr().out
     assert paf.read_text().splitlines() == o_paf
+    (tmp_path / "moved.fasta").rename(ref_fa)
     # ---- classification_cami.py / classification.py
     tax = tmp_path / "detailed_taxonomy.tsv"
     tax.write_text(w.taxonomy_tsv())
@@ -144,3 +149,34 @@ def test_screen_map_classify_dropins_match_oracle(tmp_path, capsys):
         assert cli([sub, "--paf", str(paf), "--taxonomy", str(tax), "--hierarchy", str(hier), "--output", str(out),
                     "--processes", "2"]) == 0
         assert out.read_bytes() == fn(str(paf), str(tax), str(hier))
+
+
+@pytest.mark.gpu
+def test_persisted_multipart_index_round_trip(tmp_path, capsys, monkeypatch):
+    """SPLIT_IDX small enough for three -I parts: the persisted parts reload to the same
+    PAF as the fresh build and as the oracle (minimap2 -I300k -d ; -x asm10)."""
+    from hymet_amd.cli import main as cli
+    from hymet_amd import synth
+    from oracle import pipeline_oracle
+    w = synth.make_cami(np.random.default_rng(31), n_taxa=3, per_taxon=2, genome_mbp=(0.15, 0.25), contig_gbp=0.0003,
+                        max_contigs=30, name="parts")
+    inp = tmp_path / "input"
+    inp.mkdir()
+    recs = list(zip(w.contig_names, w.contigs))
+    _fasta(inp / "a.fna", recs[:12])
+    _fasta(inp / "b.fna", recs[12:])
+    chosen = list(zip(w.ref_names, w.refs))
+    ref_fa = tmp_path / "combined_genomes.fasta"
+    _fasta(ref_fa, chosen)
+    monkeypatch.setenv("SPLIT_IDX", "300k")
+    monkeypatch.setenv("HYMET_INDEX_MINI_BATCH", "1e5")
+    paf, mmi = tmp_path / "resultados.paf", tmp_path / "reference.mmi"
+    assert cli(["map", str(inp), str(ref_fa), str(mmi), str(paf)]) == 0
+    cold = paf.read_bytes()
+    assert cli(["map", str(inp), str(ref_fa), str(mmi), str(paf)]) == 0
+    assert "Using cached minimap2 index" in capsys.readouterr().out
+    assert paf.read_bytes() == cold
+    o_paf = pipeline_oracle.map_paf([n for n, _ in chosen], [s for _, s in chosen], recs, part_bases=3e5, mini_batch=1e5)
+    assert cold.decode().splitlines() == o_paf
+    import json
+    assert len(json.loads(mmi.read_text())["part_offsets"]) >= 3

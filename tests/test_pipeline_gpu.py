@@ -157,9 +157,9 @@ def test_emit_tsv_confidence_rounding(gpu):
     lab, lab_off = dev(np.frombuffer(b"Bacteria", np.uint8).copy()), dev(np.array([0, 8], np.int64))
     out = gpu.empty(1 << 20, torch.uint8)
     nb = ctypes.c_int64()
+    d_pool, d_off = dev(np.frombuffer(pool, np.uint8).copy()), dev(off)   # kept alive across the call
     gpu.call("hymet_emit_tsv", 0, R, ptr(d["q"]), ptr(d["depth"]), ptr(d["names"]), ptr(d["conf"]), ptr(d["tax"]),
-             ptr(dev(np.frombuffer(pool, np.uint8).copy())), ptr(dev(off)), ptr(lab), ptr(lab_off), None, None, None, None,
-             ptr(out), 1 << 20, ctypes.byref(nb))
+             ptr(d_pool), ptr(d_off), ptr(lab), ptr(lab_off), None, None, None, None, ptr(out), 1 << 20, ctypes.byref(nb))
     got = out[:nb.value].cpu().numpy().tobytes()
     buf = io.StringIO(newline="")
     wr = csv.writer(buf, delimiter="\t")
