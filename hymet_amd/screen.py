@@ -106,14 +106,24 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
     return counts, bottom, n_kmers
 
 
-def reduce_partials(comm, counts, bottom: np.ndarray, nk: int, s: int):
+def reduce_partials(comm, counts, bottom: np.ndarray, nk: int, s: int, tables=None):
     """Combine the ranks' partial screens of one pool: hit counts are
     summed (all-reduce, RCCL on the device tensors), the pool bottom-s sketch is the bottom
-    s of the union of the ranks' candidates, and the k-mer totals add up."""
+    s of the union of the ranks' candidates, and the k-mer totals add up.
+
+    Every rank builds its own open-addressing table and parallel insertion makes slot
+    positions rank-specific, so counts are exchanged in the DB's hash order (gathered
+    through slot_of, summed, scattered back), never by slot."""
     if comm is None or comm.world <= 1:
         return counts, bottom, nk
-    for c in counts:
-        comm.allreduce_sum_(c)
+    for i, c in enumerate(counts):
+        if tables is None:
+            comm.allreduce_sum_(c)          # slot-aligned partials (tests)
+            continue
+        so = tables[i].slot_of[:tables[i].n_hashes]
+        by_hash = c[so]
+        comm.allreduce_sum_(by_hash)
+        c[so] = by_hash
     bottom = _bottom_s(np.concatenate(comm.allgather_np(np.asarray(bottom, np.uint64))), s)
     nk = int(sum(int(x[0]) for x in comm.allgather_np(np.array([nk], dtype=np.int64))))
     return counts, bottom, nk
@@ -157,7 +167,7 @@ def screen(gpu, pool, dbs: Sequence[SketchDB], tables: Optional[Sequence[ScreenT
             else:
                 b, e = 0, n_pos                  # the pool is this rank's contig shard
             counts, bottom, nk = count_pool(gpu, pool, [tables[i] for i in chunk], k, seed, s, b, e)
-            counts, bottom, nk = reduce_partials(comm, counts, bottom, nk, s)
+            counts, bottom, nk = reduce_partials(comm, counts, bottom, nk, s, [tables[i] for i in chunk])
             for ci, i in enumerate(chunk):
                 sh, md = table_stats(gpu, tables[i], counts[ci])
                 b_i = bottom[:dbs[i].sketch_size]

@@ -84,6 +84,30 @@ def test_screen_partials_reduce_like_one_pool():
         assert nk == sum(nks)
 
 
+def _screen_perm_fn(comm):
+    """Each rank's table puts the same hashes in different slots (parallel insertion order):
+    the exchange must line counts up by hash, not by slot."""
+    import types
+    import torch
+    from hymet_amd.screen import reduce_partials
+    rng = np.random.default_rng(21)
+    H, S = 300, 1024
+    per_hash = [rng.integers(0, 4, size=H).astype(np.int32) for _ in range(2)]      # [rank] hits per hash
+    slot_of = np.random.default_rng(100 + comm.rank).permutation(S)[:H].astype(np.int64)
+    c = torch.zeros(S + 1, dtype=torch.int32)
+    c[torch.from_numpy(slot_of)] = torch.from_numpy(per_hash[comm.rank])
+    tab = types.SimpleNamespace(slot_of=torch.from_numpy(slot_of), n_hashes=H)
+    out, _, _ = reduce_partials(comm, [c], np.zeros(0, np.uint64), 0, 10, [tab])
+    return out[0][torch.from_numpy(slot_of)].numpy(), per_hash[0] + per_hash[1]
+
+
+def test_screen_counts_reduce_by_hash_not_slot():
+    res = _run_ranks("_screen_perm_fn")
+    for r in (0, 1):
+        got, exp = res[r]
+        np.testing.assert_array_equal(got, exp)
+
+
 # ---------------------------------------------------------------- TSV row gather
 def _global_rows():
     """120 queries of a pooled input; queries with hits get the index part of their first

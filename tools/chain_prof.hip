@@ -60,6 +60,19 @@ int main(int argc, char **argv) {
         if (i == 0 || (hx[i] >> 32) != (hx[i - 1] >> 32)) h_gs.push_back(i);
     const int G = (int)h_gs.size();
     h_gs.push_back(n);
+    {  // group-size distribution: groups and anchors per size class
+        const int64_t lim[] = {3, 8, 16, 32, 64, 128, 256, 1024, 4096, 16384, INT64_MAX};
+        int64_t ng[11] = {0}, na[11] = {0};
+        for (int g = 0; g < G; g++) {
+            const int64_t s = h_gs[g + 1] - h_gs[g];
+            int c = 0;
+            while (s > lim[c]) c++;
+            ng[c]++, na[c] += s;
+        }
+        for (int c = 0; c < 11; c++)
+            printf("groups <= %6lld: %8lld groups (%5.1f%%), %10lld anchors (%5.1f%%)\n", (long long)(c < 10 ? lim[c] : -1),
+                   (long long)ng[c], 100.0 * ng[c] / G, (long long)na[c], 100.0 * na[c] / n);
+    }
     std::vector<int32_t> h_order(G);
     for (int g = 0; g < G; g++) h_order[g] = g;
     std::sort(h_order.begin(), h_order.end(), [&](int a, int b) { return h_gs[a + 1] - h_gs[a] > h_gs[b + 1] - h_gs[b]; });
