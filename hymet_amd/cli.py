@@ -14,6 +14,10 @@
         == tools/build_id_map.py (classification fallback, run_hymet_cami.sh:191)
     python -m hymet_amd.cli mini-classify input.paf id_to_taxid.tsv out.tsv
         == tools/mini_classify.py (classification fallback, run_hymet_cami.sh:192)
+    python -m hymet_amd.cli hymet2cami classified_sequences.tsv
+        == tools/hymet2cami.py (CAMI profile export, run_hymet_cami.sh:214-218)
+    python -m hymet_amd.cli taxonomy-hierarchy [NAMES_DMP NODES_DMP OUT]
+        == scripts/taxonomy_hierarchy.py (taxdump -> taxonomy_hierarchy.tsv)
 
 The thin wrappers under scripts/ call these, so run_hymet_cami.sh / main.pl can use them
 in place of the reference stage scripts unchanged.  All device work goes through
@@ -235,6 +239,47 @@ def cmd_classify(argv: Sequence[str], legacy: bool = False) -> int:
     return 0
 
 
+# ------------------------------------------- CAMI export / taxdump
+def cmd_hymet2cami(argv: Sequence[str]) -> int:
+    """tools/hymet2cami.py <classified_sequences.tsv>: CAMI profile on stdout, progress on
+    stderr; names.dmp / nodes.dmp from TAXONKIT_DB (default <repo>/taxonomy_files)."""
+    from pathlib import Path
+    from .taxonomy import hymet2cami
+    if len(argv) != 1:
+        print("Usage: hymet2cami.py <classified_sequences.tsv>", file=sys.stderr)
+        return 1
+    path = Path(argv[0]).resolve()
+    if not path.is_file():
+        print(f"Missing classified_sequences TSV: {path}", file=sys.stderr)
+        return 1
+    taxdb = os.environ.get("TAXONKIT_DB", str(Path(__file__).resolve().parents[1] / "taxonomy_files"))
+    sys.stdout.write(hymet2cami(str(path), taxdb))
+    return 0
+
+
+def cmd_taxonomy_hierarchy(argv: Sequence[str]) -> int:
+    """scripts/taxonomy_hierarchy.py: taxonomy_files/{names,nodes}.dmp -> data/taxonomy_hierarchy.tsv
+    (paths relative to the working directory, as the reference; or NAMES NODES OUT)."""
+    from .taxonomy import hierarchy_tsv
+    if argv and len(argv) != 3:
+        print("usage: taxonomy-hierarchy [NAMES_DMP NODES_DMP OUT_TSV]", file=sys.stderr)
+        return 2
+    names, nodes, out = argv if argv else (os.path.join(".", "taxonomy_files", "names.dmp"),
+                                           os.path.join(".", "taxonomy_files", "nodes.dmp"),
+                                           os.path.join(".", "data", "taxonomy_hierarchy.tsv"))
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    for p in (names, nodes):
+        if not os.path.exists(p):
+            raise FileNotFoundError(f"File {p} not found.")
+    print("Loading data from files...")
+    data = hierarchy_tsv(names, nodes)
+    print("Generating taxonomy_hierarchy.tsv...")
+    with open(out, "wb") as f:
+        f.write(data)
+    print(f"File generated successfully: {out}")
+    return 0
+
+
 def main(argv: Optional[Sequence[str]] = None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     if not argv:
@@ -257,6 +302,10 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     if cmd == "mini-classify":
         from .fallback import main_mini_classify
         return main_mini_classify(rest)
+    if cmd == "hymet2cami":
+        return cmd_hymet2cami(rest)
+    if cmd == "taxonomy-hierarchy":
+        return cmd_taxonomy_hierarchy(rest)
     print(f"unknown subcommand {cmd!r}", file=sys.stderr)
     return 2
 
