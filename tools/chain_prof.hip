@@ -120,9 +120,9 @@ int main(int argc, char **argv) {
         const char *cn[8] = {"global fetch", "list ins general", "list erase general", "rmq full path", "walk",
                              "head suffix", "cert y-fail", "batches"};
         for (int k = 0; k < 8; k++) printf("  %-20s %8.4f per anchor\n", cn[k], (double)z[8 + k] / n);
-        const char *cn2[11] = {"batch attempts", "pre: cert", "pre: b0 != prev", "pre: walk", "fail: x same", "fail: y range",
-                               "fail: gap/width", "fail: cand", "fail: walk", "fail: list", "accepted"};
-        for (int k = 0; k < 11; k++) printf("  %-20s %8.4f per anchor\n", cn2[k], (double)z[16 + k] / n);
+        const char *cn2[12] = {"batch attempts", "pre: cert", "pre: b0 != prev", "pre: walk", "fail: x same", "fail: y range",
+                               "fail: gap/width", "fail: cand", "fail: walk", "fail: list", "accepted", "st_in pop prefix"};
+        for (int k = 0; k < 12; k++) printf("  %-20s %8.4f per anchor\n", cn2[k], (double)z[16 + k] / n);
     }
     return 0;
 }
