@@ -55,6 +55,7 @@ _SIGS = {
     "hymet_paf_acc_destroy": (_i32, [_vp]),
     "hymet_paf_acc_info": (_i32, [_vp, _c.POINTER(_i64), _c.POINTER(_vp), _c.POINTER(_vp), _c.POINTER(_vp),
                                   _c.POINTER(_vp), _c.POINTER(_vp)]),
+    "hymet_paf_acc_append": (_i32, [_vp, _vp, _vp, _i64, _i64]),
     "hymet_paf_acc_copy": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "hymet_mm_map_acc": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
     "hymet_emit_paf": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _c.POINTER(_i64), _vp]),
@@ -105,7 +106,7 @@ def check(rc: int, what: str):
 class Gpu:
     """One libhymet context bound to a torch CUDA(HIP) device and its current stream."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, stream=None):
         import torch
 
         if not torch.cuda.is_available():
@@ -118,7 +119,16 @@ class Gpu:
         h = _vp()
         check(self.lib.hymet_init(device, _c.byref(h)), "hymet_init")
         self.ctx = h
-        self.bind_stream()
+        self.stream = stream
+        self.children = []
+        self.bind_stream(stream)
+
+    def fork(self) -> "Gpu":
+        """A second library context on its own HIP stream, for work that runs concurrently
+        with this context's (mapping batches on two streams); profiled with its parent."""
+        child = Gpu(self.device, stream=self.torch.cuda.Stream(device=self.device))
+        self.children.append(child)
+        return child
 
     def bind_stream(self, stream=None):
         s = stream if stream is not None else self.torch.cuda.current_stream(self.device)
@@ -129,15 +139,22 @@ class Gpu:
 
     def sync(self):
         check(self.lib.hymet_sync(self.ctx), "hymet_sync")
+        for ch in self.children:
+            ch.sync()
 
     def prof(self, on: bool = True):
         check(self.lib.hymet_prof_enable(self.ctx, int(on)), "hymet_prof_enable")
+        for ch in self.children:
+            ch.prof(on)
 
     def prof_reset(self):
         check(self.lib.hymet_prof_reset(self.ctx), "hymet_prof_reset")
+        for ch in self.children:
+            ch.prof_reset()
 
     def prof_table(self):
-        """{kernel name: (total ms, launches, algorithmic bytes)} since the last reset."""
+        """{kernel name: (total ms, launches, algorithmic bytes)} since the last reset, summed
+        over this context and its forks."""
         buf = _c.create_string_buffer(1 << 16)
         check(self.lib.hymet_prof_names(self.ctx, buf, 1 << 16), "hymet_prof_names")
         out = {}
@@ -145,6 +162,10 @@ class Gpu:
             ms, n, b = _c.c_double(), _i64(), _c.c_double()
             check(self.lib.hymet_prof_query(self.ctx, name.encode(), _c.byref(ms), _c.byref(n), _c.byref(b)), "hymet_prof_query")
             out[name] = (ms.value, n.value, b.value)
+        for ch in self.children:
+            for name, (ms, n, b) in ch.prof_table().items():
+                m0, n0, b0 = out.get(name, (0.0, 0, 0.0))
+                out[name] = (m0 + ms, n0 + n, b0 + b)
         return out
 
     def trim(self) -> int:

@@ -65,9 +65,6 @@ namespace {
 #ifndef HYMET_CHAIN_IDQ
 #define HYMET_CHAIN_IDQ 64
 #endif
-#ifndef HYMET_CHAIN_STIN_FAST  // inner-window start: pop a leaving list prefix instead of compacting
-#define HYMET_CHAIN_STIN_FAST 1
-#endif
 #ifndef HYMET_CHAIN_WPE  // waves per SIMD the register allocation targets (0: compiler's choice)
 #define HYMET_CHAIN_WPE 4
 #endif
@@ -667,29 +664,8 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     const uint64_t m = __ballot(adv);
                     const int t = ~m ? __ffsll((unsigned long long)~m) - 1 : 64;
                     if (t > 1 && !overflow && ni > 0) {
-                        const int32_t lim = st_in + t;
-#if HYMET_CHAIN_STIN_FAST
-                        // colinear common case: the d leaving entries (indices [st_in, min(lim, i0))
-                        // are all in the list) are exactly its first d slots -- pop the front
-                        const int d = min(lim, i0) - st_in;
-                        if (d > 0 && d <= ni) {
-                            bool front = true;
-                            if (lane < d) front = L(lane).y < lim;
-                            if (__ballot(!front) == 0) {
-                                CCOUNT(19);
-                                lh = (lh + d) & (kInnerCap - 1);
-                                ni -= d;
-                                if (ni > 0) {
-                                    const int2 a = L(0);
-                                    lfy = a.x, lfj = a.y;
-                                }
-                                st_in += t;
-                                if (t < 64) break;
-                                continue;
-                            }
-                        }
-#endif
                         // several entries leave: stable compaction of the list keeps j >= st_in + t
+                        const int32_t lim = st_in + t;
                         int kept = 0;
                         for (int base = 0; base < ni; base += 64) {
                             const int kk = base + lane;

@@ -1646,6 +1646,27 @@ int hymet_paf_acc_info(const hymet_paf_acc *acc, int64_t *n_lines, void **d_regs
     return HYMET_OK;
 }
 
+int hymet_paf_acc_append(hymet_ctx *ctx, hymet_paf_acc *dst, const hymet_paf_acc *src, int64_t begin, int64_t end) {
+    HY_ARG(ctx && dst && src && dst != src, "hymet_paf_acc_append: null or aliased argument");
+    HY_ARG(begin >= 0 && end >= begin && end <= src->n, "hymet_paf_acc_append: line range outside the source");
+    const int64_t m = end - begin;
+    if (m == 0) return HYMET_OK;
+    HY_HIP(hipSetDevice(ctx->device));
+    int rc = acc_reserve(ctx, dst, dst->n + m);
+    if (rc) return rc;
+    hipStream_t st = ctx->stream;
+    const int64_t d = dst->n;
+    HY_HIP(hipMemcpyAsync(dst->regs.as<hymet_mm_reg>() + d, src->regs.as<hymet_mm_reg>() + begin, sizeof(hymet_mm_reg) * (size_t)m,
+                          hipMemcpyDeviceToDevice, st));
+    HY_HIP(hipMemcpyAsync(dst->q.as<int32_t>() + d, src->q.as<int32_t>() + begin, 4 * (size_t)m, hipMemcpyDeviceToDevice, st));
+    HY_HIP(hipMemcpyAsync(dst->part.as<int32_t>() + d, src->part.as<int32_t>() + begin, 4 * (size_t)m, hipMemcpyDeviceToDevice,
+                          st));
+    HY_HIP(hipMemcpyAsync(dst->rl.as<int32_t>() + d, src->rl.as<int32_t>() + begin, 4 * (size_t)m, hipMemcpyDeviceToDevice, st));
+    HY_HIP(hipMemcpyAsync(dst->t.as<int32_t>() + d, src->t.as<int32_t>() + begin, 4 * (size_t)m, hipMemcpyDeviceToDevice, st));
+    dst->n += m;
+    return HYMET_OK;
+}
+
 int hymet_paf_acc_copy(hymet_ctx *ctx, const hymet_paf_acc *acc, int32_t *h_q, int32_t *h_part, int32_t *h_t) {
     HY_ARG(ctx && acc, "hymet_paf_acc_copy: null argument");
     if (acc->n <= 0) return HYMET_OK;

@@ -45,6 +45,7 @@ class Config:
     w: int = 10                       # minimap2 -d defaults
     k: int = 15
     map_batch_bases: int = 40_000_000  # query bases per device mapping batch (HBM budget)
+    map_streams: int = 2              # concurrent mapping batches (library contexts / HIP streams)
     n_input_files: int = 1            # run_hymet_cami.sh copies one FASTA into input/
 
 
@@ -150,6 +151,48 @@ def map_shard(gpu, ix: IndexSet, sh: QueryShard, acc: PafAcc) -> int:
     return acc.n
 
 
+def map_shard_streams(gpus, accs, ix: IndexSet, sh: QueryShard, acc: PafAcc) -> int:
+    """map_shard with the part x batch calls spread over several library contexts, each on
+    its own HIP stream and host thread (ctypes releases the GIL): one batch's host
+    synchronisations, small kernels and chaining tail overlap another batch's kernels.  Each
+    worker appends to its own accumulator; the segments are then concatenated into `acc`
+    in minimap2's order (part-major, batch order)."""
+    import threading
+    tasks = [(pi, b0, b1) for pi in range(len(ix.parts)) for b0, b1 in sh.batches if b1 > b0]
+    segs = [None] * len(tasks)
+    errs = []
+    starts = np.ascontiguousarray(sh.starts, np.int64)
+    lens = np.ascontiguousarray(sh.lengths, np.int64)
+    hbase = sh.name_hash.data_ptr()
+
+    def work(w):
+        g, a = gpus[w], accs[w]
+        try:
+            a.reset()
+            for ti in range(w, len(tasks), len(gpus)):
+                pi, b0, b1 = tasks[ti]
+                before = a.n
+                g.call("hymet_mm_map_acc", ix.parts[pi].h, _c.byref(ix.opt), ptr(sh.mm.w2b), ptr(sh.mm.wmask),
+                       _c.c_void_p(starts.ctypes.data + 8 * b0), _c.c_void_p(lens.ctypes.data + 8 * b0),
+                       _c.c_void_p(hbase + 4 * b0), b1 - b0, b0, pi, ix.part_first[pi], a.h)
+                segs[ti] = (w, before, a.n)
+        except Exception as e:  # noqa: BLE001 -- re-raised on the calling thread
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(w,)) for w in range(len(gpus))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    acc.reset()
+    g0 = acc.gpu
+    for w, b, e in segs:
+        g0.call("hymet_paf_acc_append", acc.h, accs[w].h, b, e)
+    return acc.n
+
+
 def _dev_buf(gpu, bufs, key, nbytes):
     """A reusable device byte buffer of at least nbytes."""
     b = bufs.get(key)
@@ -211,6 +254,8 @@ class Pipeline:
         self.index_cache: Dict[str, IndexSet] = {}
         self.opt: Optional[mp.MapOpt] = None
         self.acc = PafAcc(gpu)
+        self.map_gpus = [gpu.fork() for _ in range(self.cfg.map_streams)] if self.cfg.map_streams > 1 else []
+        self.map_accs = [PafAcc(g) for g in self.map_gpus]
         self._bufs: Dict[str, object] = {}
 
     @property
@@ -273,6 +318,9 @@ class Pipeline:
 
     def map_all(self, ix: IndexSet, sh: QueryShard) -> int:
         self.opt = ix.opt
+        if self.map_gpus:
+            self.gpu.sync()  # the shard's pools were written on this context's stream
+            return map_shard_streams(self.map_gpus, self.map_accs, ix, sh, self.acc)
         return map_shard(self.gpu, ix, sh, self.acc)
 
     def classify_rows(self, ix: IndexSet, sh: QueryShard):

@@ -196,6 +196,9 @@ int hymet_paf_acc_destroy(hymet_paf_acc *acc);
 /* line count and the device arrays (hymet_mm_reg, int32 query, part, rep_len, target) */
 int hymet_paf_acc_info(const hymet_paf_acc *acc, int64_t *n_lines, void **d_regs, void **d_q, void **d_part, void **d_rl,
                        void **d_t);
+/* append lines [begin, end) of src to dst (device copies on ctx's stream; src's producing
+ * work must be complete -- hymet_mm_map_acc returns synchronised) */
+int hymet_paf_acc_append(hymet_ctx *ctx, hymet_paf_acc *dst, const hymet_paf_acc *src, int64_t begin, int64_t end);
 /* query, part and target index of every line, copied to host arrays of n_lines (synchronous) */
 int hymet_paf_acc_copy(hymet_ctx *ctx, const hymet_paf_acc *acc, int32_t *h_q, int32_t *h_part, int32_t *h_t);
 int hymet_mm_map_acc(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *opt, const uint32_t *d_2b,
