@@ -139,7 +139,7 @@ def build_cami(args, comm, gpu):
     def ref_lookup(sel):
         return refs_ss.subset([by_name[n] for n in sel])
 
-    cfg = pipeline.Config(map_batch_bases=int(args.batch_mbp * 1e6))
+    cfg = pipeline.Config(map_batch_bases=int(args.batch_mbp * 1e6), map_streams=args.map_streams)
     pipe = pipeline.Pipeline(gpu, [db], ref_lookup, tax, hier, cfg, comm)
     return w, db, pipe, fasta, refs_ss, tax, hier, td
 
@@ -376,6 +376,7 @@ def main():
     ap.add_argument("--taxa", type=int, default=12)
     ap.add_argument("--per-taxon", type=int, default=62)
     ap.add_argument("--batch-mbp", type=float, default=40.0)
+    ap.add_argument("--map-streams", type=int, default=1, help="concurrent mapping batches (library contexts)")
     ap.add_argument("--fasta-width", type=int, default=0, help="FASTA line width (0: one line per contig, as MEGAHIT)")
     ap.add_argument("--screen-refs", type=int, default=100_000)
     ap.add_argument("--no-cpu", action="store_true")
