@@ -88,6 +88,17 @@ def path_roofline(prof, steps, step_s, L, K, P, n_parts, world, w=10):
             "peak": HBM_PEAK_GBS * world, "unit": "GB/s", "frac": ach / (HBM_PEAK_GBS * world)}
 
 
+def gpu_scratch_gb(gpu):
+    """Bytes held by the library's scratch cache (all contexts), GB."""
+    import ctypes
+    tot = 0
+    for g in [gpu] + list(gpu.children):
+        v = ctypes.c_int64()
+        if g.lib.hymet_scratch_cached(g.ctx, ctypes.byref(v)) == 0:
+            tot = max(tot, v.value)   # the cache is process-wide: every context reports the same
+    return tot / 1e9
+
+
 def cpu_info():
     model = ""
     try:
@@ -205,6 +216,7 @@ def bench_cami(args, comm, gpu, torch):
                    "window": "FASTA bytes in host memory -> classified_sequences.tsv written + resultados.paf text in host "
                              "memory (ingest, H2D, screen, select, limit, map, LCA, text emit inside every step)"},
         "cold_run_s": cold,
+        "scratch_cached_gb": gpu_scratch_gb(gpu),
         "paf_lines": n_lines,
         "kernel_ms_per_step_rank0": kern_ms,
         "stage_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
@@ -376,7 +388,7 @@ def main():
     ap.add_argument("--taxa", type=int, default=12)
     ap.add_argument("--per-taxon", type=int, default=62)
     ap.add_argument("--batch-mbp", type=float, default=40.0)
-    ap.add_argument("--map-streams", type=int, default=1, help="concurrent mapping batches (library contexts)")
+    ap.add_argument("--map-streams", type=int, default=2, help="concurrent mapping batches (library contexts)")
     ap.add_argument("--fasta-width", type=int, default=0, help="FASTA line width (0: one line per contig, as MEGAHIT)")
     ap.add_argument("--screen-refs", type=int, default=100_000)
     ap.add_argument("--no-cpu", action="store_true")

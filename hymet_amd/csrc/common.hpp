@@ -47,7 +47,8 @@ int hip_fail(hipError_t e, const char *what);
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // Caching device allocator for kernel scratch, keyed by (device, stream, size class): a
 // block released on a stream is reissued only to work queued behind it on the same stream.
-// Cached bytes are capped (HYMET_SCRATCH_CAP_GB, default 96); hymet_scratch_trim frees them.
+// A request takes the best-fitting cached block of at most twice its size.  Cached bytes
+// are capped (HYMET_SCRATCH_CAP_GB, default 160); hymet_scratch_trim frees them.
 // (hipMalloc/hipFree and the stream-ordered pool cost 0.1-0.4 s per large block on this
 // stack, at every mapping batch, hence the cache.)
 hipError_t scratch_alloc(size_t bytes, hipStream_t stream, void **p, size_t *cls);

@@ -35,7 +35,7 @@ static size_t g_cached = 0;                                // bytes held in g_ca
 static size_t cache_cap() {
     static const size_t cap = [] {
         const char *e = getenv("HYMET_SCRATCH_CAP_GB");
-        const double gb = e ? atof(e) : 96.0;
+        const double gb = e ? atof(e) : 160.0;
         return (size_t)(gb * 1073741824.0);
     }();
     return cap;
@@ -66,11 +66,15 @@ hipError_t scratch_alloc(size_t bytes, hipStream_t stream, void **p, size_t *cls
     if (e != hipSuccess) return e;
     *cls = size_class(bytes);
     {
+        // best fit among this stream's cached blocks of at most twice the request: batches
+        // of varying sizes then reuse blocks instead of piling up one class per size
         std::lock_guard<std::mutex> lk(g_cache_mu);
-        auto it = g_cache.find({dev, stream, *cls});
-        if (it != g_cache.end() && !it->second.empty()) {
+        for (auto it = g_cache.lower_bound({dev, stream, *cls});
+             it != g_cache.end() && it->first.dev == dev && it->first.stream == stream && it->first.cls <= 2 * *cls; ++it) {
+            if (it->second.empty()) continue;
             *p = it->second.back();
             it->second.pop_back();
+            *cls = it->first.cls;
             g_cached -= *cls;
             return hipSuccess;
         }

@@ -45,7 +45,7 @@ class Config:
     w: int = 10                       # minimap2 -d defaults
     k: int = 15
     map_batch_bases: int = 40_000_000  # query bases per device mapping batch (HBM budget)
-    map_streams: int = 1              # concurrent mapping batches (library contexts / HIP streams)
+    map_streams: int = 2              # concurrent mapping batches (library contexts / HIP streams)
     n_input_files: int = 1            # run_hymet_cami.sh copies one FASTA into input/
 
 

@@ -54,7 +54,8 @@ int hymet_prof_query(hymet_ctx *ctx, const char *name, double *total_ms, int64_t
 /* newline-separated names of every timed kernel */
 int hymet_prof_names(hymet_ctx *ctx, char *buf, int64_t cap);
 /* The library's kernel scratch is a caching allocator keyed by (device, stream, size class)
- * and capped at HYMET_SCRATCH_CAP_GB (default 96) of cached blocks.  trim synchronises the
+ * (best fit up to twice the request) and capped at HYMET_SCRATCH_CAP_GB (default 160) of
+ * cached blocks.  trim synchronises the
  * context stream and returns every cached block of the device to HIP (e.g. before torch
  * allocates large tensors); cached reports the bytes held. */
 int hymet_scratch_trim(hymet_ctx *ctx, int64_t *freed_bytes);
