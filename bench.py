@@ -130,16 +130,27 @@ def build_cami(args, comm, gpu):
     db_names = [n + ".fna.gz" for n in w.ref_names]
     refs_ss = from_records([(n, "", s) for n, s in zip(w.ref_names, w.refs)])
     sk = scr.sketch_sequences(gpu, DevicePool(gpu, refs_ss, DevicePool.ALPHA_MASH), 21, 42, 1000)
-    n_dec = max(0, args.screen_refs - len(sk))
-    dec = synth.decoy_sketches(np.random.default_rng(99), n_dec, 1000)
-    lens = [len(h) for h in sk] + [1000] * n_dec
-    off = np.zeros(len(lens) + 1, np.int64)
-    off[1:] = np.cumsum(lens)
-    hashes = np.concatenate(sk + [dec.reshape(-1)])
-    names = db_names + [f"GCF_{900000000 + i:09d}.1_decoy_genomic.fna.gz" for i in range(n_dec)]
-    db = SketchDB(names=names, comments=[f"[1 seqs] {n}" for n in names], lengths=np.full(len(names), 4_000_000, np.int64),
-                  offsets=off, hashes=hashes)
-    log(f"sketch DB: {db.n_refs} refs, {len(db.hashes)/1e6:.0f}M hashes ({time.time()-t0:.1f}s)")
+    # sketch DBs of H hashes each (sketch1, and for CAMI-high GTDB/custom-sized sketch2/3):
+    # the candidates' own sketches split over the DBs by share, decoy references fill up
+    sizes = [int(float(x)) for x in args.db_hashes.split(",")]
+    shares = np.array(sizes, np.float64) / sum(sizes)
+    cut = np.r_[0, np.round(np.cumsum(shares) * len(sk)).astype(int)]
+    dbs = []
+    for d, H in enumerate(sizes):
+        mine = list(range(cut[d], cut[d + 1]))
+        n_dec = max(0, H // 1000 - len(mine))
+        dec = synth.decoy_sketches(np.random.default_rng(99 + d), n_dec, 1000)
+        lens = [len(sk[i]) for i in mine] + [1000] * n_dec
+        off = np.zeros(len(lens) + 1, np.int64)
+        off[1:] = np.cumsum(lens)
+        hashes = np.concatenate([sk[i] for i in mine] + [dec.reshape(-1)])
+        names = [db_names[i] for i in mine] + [f"GCF_{900000000 + d * 10**7 + i:09d}.1_decoy_genomic.fna.gz"
+                                               for i in range(n_dec)]
+        dbs.append(SketchDB(names=names, comments=[f"[1 seqs] {n}" for n in names],
+                            lengths=np.full(len(names), 4_000_000, np.int64), offsets=off, hashes=hashes))
+    db = dbs[0]
+    log(f"sketch DBs: " + ", ".join(f"{x.n_refs} refs / {len(x.hashes)/1e6:.0f}M hashes" for x in dbs) +
+        f" ({time.time()-t0:.1f}s)")
     td = tempfile.mkdtemp(prefix="hymet_bench_")
     tax = os.path.join(td, "detailed_taxonomy.tsv")
     hier = os.path.join(td, "taxonomy_hierarchy.tsv")
@@ -150,8 +161,9 @@ def build_cami(args, comm, gpu):
     def ref_lookup(sel):
         return refs_ss.subset([by_name[n] for n in sel])
 
-    cfg = pipeline.Config(map_batch_bases=int(args.batch_mbp * 1e6), map_streams=args.map_streams)
-    pipe = pipeline.Pipeline(gpu, [db], ref_lookup, tax, hier, cfg, comm)
+    cfg = pipeline.Config(map_batch_bases=int(args.batch_mbp * 1e6), map_streams=args.map_streams,
+                          cand_max=args.cand_max)
+    pipe = pipeline.Pipeline(gpu, dbs, ref_lookup, tax, hier, cfg, comm)
     return w, db, pipe, fasta, refs_ss, tax, hier, td
 
 
@@ -209,9 +221,10 @@ def bench_cami(args, comm, gpu, torch):
         "warmup": args.warmup, "ms_per_step": step * 1e3, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic",
         "mbp_per_s": total_bases / 1e6 / step,
-        "config": {"workload": f"CAMI-medium (C4): {args.taxa} taxa, {n_contigs} contigs / {total_bases/1e6:.0f} Mbp FASTA "
+        "config": {"workload": f"{args.workload_name}: {args.taxa} taxa, {n_contigs} contigs / {total_bases/1e6:.0f} Mbp FASTA "
                                f"({len(fasta)/1e6:.0f} MB) sharded over {comm.world} GPU(s); {len(res.selected)} candidates / "
-                               f"{refs_ss.total_bases/1e9:.2f} Gbp in {len(ix.parts)} -I2g parts; sketch DB {db.n_refs} refs x 1000",
+                               f"{refs_ss.total_bases/1e9:.2f} Gbp in {len(ix.parts)} -I2g parts; sketch DBs "
+                               + " + ".join(f"{d.n_refs} refs" for d in pipe.dbs) + " x 1000",
                    "global_contigs": n_contigs, "parallelism": f"contig-shard x{comm.world}",
                    "window": "FASTA bytes in host memory -> classified_sequences.tsv written + resultados.paf text in host "
                              "memory (ingest, H2D, screen, select, limit, map, LCA, text emit inside every step)"},
@@ -383,24 +396,38 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="cami-medium", choices=["cami-medium", "screen"])
+    ap.add_argument("--workload", default="cami-medium", choices=["cami-medium", "cami-high", "screen"])
     ap.add_argument("--contig-gbp", type=float, default=1.0)
     ap.add_argument("--taxa", type=int, default=12)
     ap.add_argument("--per-taxon", type=int, default=62)
     ap.add_argument("--batch-mbp", type=float, default=40.0)
     ap.add_argument("--map-streams", type=int, default=2, help="concurrent mapping batches (library contexts)")
     ap.add_argument("--fasta-width", type=int, default=0, help="FASTA line width (0: one line per contig, as MEGAHIT)")
-    ap.add_argument("--screen-refs", type=int, default=100_000)
+    ap.add_argument("--screen-refs", type=int, default=100_000, help="screen-only workload: references in the DB")
+    ap.add_argument("--db-hashes", default=None, help="hashes per sketch DB, comma-separated (C4: 1e8; C5: 1e8,5e7,1e7)")
+    ap.add_argument("--cand-max", type=int, default=5000, help="CAND_MAX (run_hymet_cami.sh:26)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16, help="CPU baseline threads (the GPU box's CPU share is 16)")
     args = ap.parse_args()
+    # CAMI-high (C5, BASELINE.json configs[4]): 14 taxa (tools/generate_cami_subsets.py:343),
+    # the full CAND_MAX of 5000 candidates (~20 Gbp, ten -I2g parts), ~2 Gbp of contigs,
+    # three sketch DBs of 1e8 / 5e7 / 1e7 hashes
+    if args.workload == "cami-high":
+        args.taxa = 14
+        args.per_taxon = [358] * 2 + [357] * 12
+        args.contig_gbp = 2.0
+        args.db_hashes = args.db_hashes or "1e8,5e7,1e7"
+        args.workload_name = "CAMI-high (C5)"
+    else:
+        args.db_hashes = args.db_hashes or "1e8"
+        args.workload_name = "CAMI-medium (C4)"
     import torch
     from hymet_amd._lib import Gpu
     from hymet_amd.dist import Comm
     comm = Comm.from_env()
     gpu = Gpu(int(os.environ.get("LOCAL_RANK", "0")))
     comm.init_backend(gpu)
-    res = bench_cami(args, comm, gpu, torch) if args.workload == "cami-medium" else bench_screen(args, comm, gpu, torch)
+    res = bench_screen(args, comm, gpu, torch) if args.workload == "screen" else bench_cami(args, comm, gpu, torch)
     if comm.rank == 0:
         print(json.dumps(res), flush=True)
     comm.close()
