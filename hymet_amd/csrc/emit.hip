@@ -250,13 +250,9 @@ int scan_lengths(hymet_ctx *ctx, hymet::mm::DevBuf &len, int64_t n, hymet::mm::D
     hipStream_t st = ctx->stream;
     HY_HIP(off.alloc(8 * (size_t)(n + 1), st));
     HY_HIP(hipMemsetAsync(len.as<uint32_t>() + n, 0, 4, st));
-    size_t tb = 0;
-    HY_HIP(rocprim::exclusive_scan(nullptr, tb, len.as<uint32_t>(), off.as<int64_t>(), (int64_t)0, (size_t)(n + 1),
-                                   rocprim::plus<int64_t>(), st));
     hymet::mm::DevBuf tmp;
-    HY_HIP(tmp.alloc(tb, st));
-    HY_HIP(rocprim::exclusive_scan(tmp.p, tb, len.as<uint32_t>(), off.as<int64_t>(), (int64_t)0, (size_t)(n + 1),
-                                   rocprim::plus<int64_t>(), st));
+    const int rc = hymet::mm::scan_u32_i64(ctx, len.as<uint32_t>(), off.as<int64_t>(), n + 1, tmp);
+    if (rc) return rc;
     HY_HIP(hipMemcpyAsync(total, off.as<int64_t>() + n, 8, hipMemcpyDeviceToHost, st));
     HY_HIP(hipStreamSynchronize(st));
     return HYMET_OK;

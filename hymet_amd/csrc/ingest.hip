@@ -133,12 +133,8 @@ extern "C" int hymet_fasta_compact(hymet_ctx *ctx, const uint8_t *d_raw, int64_t
         hipLaunchKernelGGL(chunk_count_kernel, dim3((unsigned)C), dim3(kThreads), 0, st, d_raw, d_ch.as<ChunkRef>(), C,
                            d_cnt.as<uint32_t>());
         HY_CHECK_LAUNCH("chunk_count_kernel");
-        size_t tb = 0;
-        HY_HIP(rocprim::exclusive_scan(nullptr, tb, d_cnt.as<uint32_t>(), d_pref.as<int64_t>(), (int64_t)0, (size_t)C,
-                                       rocprim::plus<int64_t>(), st));
-        HY_HIP(tmp.alloc(tb, st));
-        HY_HIP(rocprim::exclusive_scan(tmp.p, tb, d_cnt.as<uint32_t>(), d_pref.as<int64_t>(), (int64_t)0, (size_t)C,
-                                       rocprim::plus<int64_t>(), st));
+        const int rc = hymet::mm::scan_u32_i64(ctx, d_cnt.as<uint32_t>(), d_pref.as<int64_t>(), C, tmp);
+        if (rc) return rc;
         hipLaunchKernelGGL(chunk_write_kernel, dim3((unsigned)C), dim3(kThreads), 0, st, d_raw, d_ch.as<ChunkRef>(), C,
                            d_pref.as<int64_t>(), d_pool_start, d_pool);
         HY_CHECK_LAUNCH("chunk_write_kernel");

@@ -317,14 +317,10 @@ int hymet_acc_classify(hymet_ctx *ctx, const hymet_paf_acc *acc, int mode, int32
                        cnt.as<uint32_t>(), d_row_q, d_row_part, row_of.as<int32_t>(), row_cnt.as<uint32_t>());
     HY_CHECK_LAUNCH("acc_rows_kernel");
     {
-        size_t tb = 0;
-        HY_HIP(rocprim::exclusive_scan(nullptr, tb, row_cnt.as<uint32_t>(), row_off.as<int64_t>(), (int64_t)0,
-                                       (size_t)R + 1, rocprim::plus<int64_t>(), st));
-        DevBuf tmp;
-        HY_HIP(tmp.alloc(tb, st));
+        DevBuf part;
         HY_HIP(hipMemsetAsync(row_cnt.as<uint32_t>() + R, 0, 4, st));
-        HY_HIP(rocprim::exclusive_scan(tmp.p, tb, row_cnt.as<uint32_t>(), row_off.as<int64_t>(), (int64_t)0,
-                                       (size_t)R + 1, rocprim::plus<int64_t>(), st));
+        const int rc = hymet::mm::scan_u32_i64(ctx, row_cnt.as<uint32_t>(), row_off.as<int64_t>(), R + 1, part);
+        if (rc) return rc;
     }
     // lines grouped by row, PAF order kept inside a row (stable LSD sort by row)
     HY_HIP(lk.alloc(4 * (size_t)n, st));

@@ -1,0 +1,586 @@
+// Grouped anchor sort: the anchor keys of a mapping batch (q | rev | rid | rpos, value y;
+// write_anchor_keys_kernel / rechain_keys_kernel) into (key, y) order -- minimap2's radix
+// sort of a query's anchors by x (map.c collect_seed_hits -> radix_sort_128x), with the
+// canonical full (x, y) tie order T1 -- written out directly as the anchor
+// set (x, y, key), so no unpack pass follows.
+//
+// The keys arrive query-major (one query's anchors are contiguous), so the global LSD sort
+// over ~47 key bits (six 8-bit passes over 12 B per anchor) is replaced by work local to a
+// query:
+//   * a query of <= 4096 anchors is sorted whole in one block;
+//   * a larger query is cut into tiles of 4096 anchors; every tile counts its anchors per
+//     bin = (rev, rid) in LDS; a per-query scan turns the counts into each (tile, bin) run's
+//     position and lists the non-empty bins -- the (query, strand, target) groups; the tiles
+//     scatter their anchors to their runs; every group of <= 4096 anchors is then sorted by
+//     (rpos, y) in one block, and the larger groups (a query against its own genome) by one
+//     device radix sort over all of them together (key = group rank | rpos).
+// A block sort packs (the key's bits below q or below rid, y) into one 64-bit word, sorts it
+// in registers (bitonic, ITEMS per thread) and merges the runs in LDS (merge path); segments
+// of <= 64 anchors take a wave bitonic sort on (key, y).  Equal keys after the device radix
+// sort (one target position hit by several query minimizers) are put in y order on write.
+// The caller falls back to the device sort of the whole batch (return 1) when a large query
+// meets more than 4096 bins (index parts of > 2047 targets) or the packed words would not
+// fit 64 bits.
+#include "mm_common.hpp"
+
+namespace hymet {
+namespace mm {
+namespace {
+
+constexpr int kTile = 4096;     // anchors per tile of a large query
+constexpr int kMaxBins = 4096;  // (rev, rid) bins held in LDS
+
+struct Seg {
+    int64_t s;  // first anchor
+    int32_t n;  // anchors
+    int32_t q;  // query
+};
+
+// segment classes: thread (<= 8), wave (<= 64), blocks of 256 / 512 / 1024 / 2048 / 4096, large
+enum { kThread = 0, kWave, kB256, kB512, kB1K, kB2K, kB4K, kLarge, kClasses };
+
+__device__ __forceinline__ int seg_class(int64_t n) {
+    return n <= 8 ? kThread : n <= 64 ? kWave : n <= 256 ? kB256 : n <= 512 ? kB512 : n <= 1024 ? kB1K : n <= 2048 ? kB2K
+         : n <= kTile ? kB4K : kLarge;
+}
+
+// the anchor set written for sorted position i: key (k1), x, y
+struct AnchorOut {
+    uint64_t *key, *ax, *ay;
+    int rb, pb;
+    uint64_t yhi;
+    __device__ __forceinline__ void put(int64_t i, uint64_t k, uint32_t y) const {
+        key[i] = k;
+        const uint64_t rev = k >> (rb + pb) & 1, rid = k >> pb & ((1ull << rb) - 1), rpos = k & ((1ull << pb) - 1);
+        ax[i] = rev << 63 | rid << 32 | rpos;
+        ay[i] = yhi << 32 | y;
+    }
+};
+
+// one slot per lane with `pred` in list cnt's range: one atomic per wave (every lane calls)
+__device__ __forceinline__ int wave_append(int32_t *cnt, bool pred) {
+    const uint64_t m = __ballot(pred);
+    if (m == 0) return -1;
+    const int lane = threadIdx.x & 63, leader = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(cnt, __popcll(m));
+    base = __shfl(base, leader, 64);
+    return pred ? base + __popcll(m & ((1ull << lane) - 1)) : -1;
+}
+
+// Append the block's segments to their class lists: LDS counts per class, then one global
+// atomic per class and block (a global atomic per item serialises on the 8 counters).
+// ITEMS segments per thread; cls < 0: none.
+template <int ITEMS>
+__device__ __forceinline__ void block_append(const Seg (&sg)[ITEMS], const int (&cls)[ITEMS], Seg *lists, int64_t cap,
+                                             int32_t *cnt) {
+    __shared__ int32_t lc[kClasses], gb[kClasses];
+    if (threadIdx.x < kClasses) lc[threadIdx.x] = 0;
+    __syncthreads();
+    int slot[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) {
+        slot[j] = -1;
+        for (int k = 0; k < kClasses; k++) {
+            const int sl = wave_append(&lc[k], cls[j] == k);
+            if (sl >= 0) slot[j] = sl;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kClasses) gb[threadIdx.x] = lc[threadIdx.x] ? atomicAdd(&cnt[threadIdx.x], lc[threadIdx.x]) : 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++)
+        if (cls[j] >= 0) lists[cls[j] * cap + gb[cls[j]] + slot[j]] = sg[j];
+}
+
+// queries by size class (large: tiles counted)
+__global__ __launch_bounds__(256) void query_class_kernel(const int64_t *qoff, int n_q, Seg *lists, int64_t cap, int32_t *cnt,
+                                                          uint32_t *nt) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool ok = q < n_q;
+    const int64_t s = ok ? qoff[q] : 0, n = ok ? qoff[q + 1] - s : 0;
+    if (ok) nt[q] = n > kTile ? (uint32_t)((n + kTile - 1) / kTile) : 0;
+    const Seg sg[1] = {Seg{s, (int32_t)n, q}};
+    const int cls[1] = {n > 0 ? seg_class(n) : -1};
+    block_append<1>(sg, cls, lists, cap, cnt);
+}
+
+// LDS atomicAdd(&h[bin], 1) for the active lanes, returning the old values: the lanes of up
+// to two bins shared by many lanes (a query's anchors crowd into its genome's bins) take one
+// atomic per bin, the rest one each
+__device__ __forceinline__ uint32_t lds_rank(uint32_t *h, int bin, bool active) {
+    const int lane = threadIdx.x & 63;
+    uint64_t pending = __ballot(active);
+    uint32_t r = 0;
+    for (int it = 0; it < 2 && pending; it++) {
+        const int leader = __ffsll((unsigned long long)pending) - 1;
+        const int lb = __shfl(bin, leader, 64);
+        const uint64_t m = __ballot(active && bin == lb) & pending;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&h[lb], (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, leader, 64);
+        if (m >> lane & 1) r = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+        pending &= ~m;
+    }
+    if (pending >> lane & 1) r = atomicAdd(&h[bin], 1u);
+    return r;
+}
+
+__global__ void tile_map_kernel(const Seg *large, int n_large, const int64_t *tpos, int64_t *tile_a0, int32_t *tile_q,
+                                int32_t *tile_n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_large) return;
+    const Seg S = large[i];
+    int64_t t = tpos[S.q];
+    for (int64_t a = 0; a < S.n; a += kTile, t++) {
+        tile_a0[t] = S.s + a;
+        tile_q[t] = S.q;
+        tile_n[t] = (int32_t)min((int64_t)kTile, (int64_t)S.n - a);
+    }
+}
+
+__global__ __launch_bounds__(256) void tile_hist_kernel(const uint64_t *__restrict__ key, const int64_t *__restrict__ tile_a0,
+                                                        const int32_t *__restrict__ tile_n, int pb, int nbins,
+                                                        uint32_t *__restrict__ H) {
+    __shared__ uint32_t h[kMaxBins];
+    const int64_t a0 = tile_a0[blockIdx.x];
+    const int n = tile_n[blockIdx.x];
+    for (int b = threadIdx.x; b < nbins; b += 256) h[b] = 0;
+    __syncthreads();
+    for (int e0 = 0; e0 < n; e0 += 256) {  // every lane runs the loop (wave-level ballots inside)
+        const int e = e0 + threadIdx.x;
+        const bool act = e < n;
+        (void)lds_rank(h, act ? (int)((key[a0 + e] >> pb) & (nbins - 1)) : 0, act);
+    }
+    __syncthreads();
+    uint32_t *row = H + (int64_t)blockIdx.x * nbins;
+    for (int b = threadIdx.x; b < nbins; b += 256) row[b] = h[b];
+}
+
+// one block per large query: H[t][b] <- offset (within the query) of tile t's bin-b run;
+// every non-empty bin appended to the group list
+__global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const int64_t *tpos, int nbins,
+                                                         uint32_t *__restrict__ H, Seg *groups, int32_t *n_groups) {
+    __shared__ uint32_t part[256];
+    __shared__ uint32_t carry;
+    const Seg S = large[blockIdx.x];
+    const int64_t t0 = tpos[S.q], t1 = t0 + (S.n + kTile - 1) / kTile;
+    if (threadIdx.x == 0) carry = 0;
+    for (int r = 0; r < nbins; r += 256) {  // bins r + tid, in bin order across rows
+        const int b = r + threadIdx.x;
+        uint32_t run = 0;
+        if (b < nbins)
+            for (int64_t t = t0; t < t1; t += 8) {  // 8 loads in flight
+                uint32_t v[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) v[j] = t + j < t1 ? H[(t + j) * nbins + b] : 0u;
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (t + j < t1) {
+                        H[(t + j) * nbins + b] = run;  // exclusive within the bin, across tiles
+                        run += v[j];
+                    }
+            }
+        part[threadIdx.x] = run;
+        __syncthreads();
+        for (int d = 1; d < 256; d <<= 1) {  // inclusive scan over the row's bins
+            const uint32_t o = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+            __syncthreads();
+            part[threadIdx.x] += o;
+            __syncthreads();
+        }
+        const uint32_t base = carry + part[threadIdx.x] - run;
+        if (b < nbins && run > 0)
+            for (int64_t t = t0; t < t1; t++) H[t * nbins + b] += base;
+        const int slot = wave_append(n_groups, b < nbins && run > 0);
+        if (slot >= 0) groups[slot] = Seg{S.s + base, (int32_t)run, S.q};
+        __syncthreads();
+        if (threadIdx.x == 255) carry += part[255];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void tile_scatter_kernel(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
+                                                           const int64_t *__restrict__ tile_a0, const int32_t *__restrict__ tile_q,
+                                                           const int32_t *__restrict__ tile_n, const int64_t *__restrict__ qoff,
+                                                           int pb, int nbins, const uint32_t *__restrict__ H,
+                                                           uint64_t *__restrict__ okey, uint32_t *__restrict__ oval) {
+    __shared__ uint32_t c[kMaxBins];
+    const int64_t a0 = tile_a0[blockIdx.x];
+    const int n = tile_n[blockIdx.x];
+    const uint32_t *row = H + (int64_t)blockIdx.x * nbins;
+    for (int b = threadIdx.x; b < nbins; b += 256) c[b] = row[b];
+    __syncthreads();
+    const int64_t base = qoff[tile_q[blockIdx.x]];
+    for (int e0 = 0; e0 < n; e0 += 256) {
+        const int e = e0 + threadIdx.x;
+        const bool act = e < n;
+        const uint64_t k = act ? key[a0 + e] : 0;
+        const int64_t pos = base + lds_rank(c, (int)((k >> pb) & (nbins - 1)), act);
+        if (act) {
+            okey[pos] = k;
+            oval[pos] = val[a0 + e];
+        }
+    }
+}
+
+// groups by size class, 4 per thread; a single-anchor group is final where the scatter put it
+__global__ __launch_bounds__(256) void group_class_kernel(const Seg *groups, int64_t G, Seg *lists, int64_t cap, int32_t *cnt,
+                                                          const uint64_t *key, const uint32_t *val, AnchorOut out) {
+    Seg sg[4];
+    int cls[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int64_t g = (int64_t)blockIdx.x * 1024 + j * 256 + threadIdx.x;
+        sg[j] = g < G ? groups[g] : Seg{0, 0, 0};
+        if (sg[j].n == 1) out.put(sg[j].s, key[sg[j].s], val[sg[j].s]);
+        cls[j] = sg[j].n > 1 ? seg_class(sg[j].n) : -1;
+    }
+    block_append<4>(sg, cls, lists, cap, cnt);
+}
+
+// one thread per segment of <= 8 anchors: sorting network on (key, y) in registers
+__global__ __launch_bounds__(256) void thread_seg_sort_kernel(const Seg *list, int n_seg, const uint64_t *key,
+                                                              const uint32_t *val, AnchorOut out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_seg) return;
+    const Seg S = list[i];
+    uint64_t k[8];
+    uint32_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        k[j] = j < S.n ? key[S.s + j] : ~0ull;
+        v[j] = j < S.n ? val[S.s + j] : ~0u;
+    }
+#pragma unroll
+    for (int w = 2; w <= 8; w <<= 1)
+#pragma unroll
+        for (int d = w >> 1; d > 0; d >>= 1)
+#pragma unroll
+            for (int a = 0; a < 8; a++) {
+                const int b = a ^ d;
+                if (b > a) {
+                    const bool up = (a & w) == 0;
+                    const bool gt = k[a] > k[b] || (k[a] == k[b] && v[a] > v[b]);
+                    if (gt == up) {
+                        const uint64_t tk = k[a];
+                        k[a] = k[b];
+                        k[b] = tk;
+                        const uint32_t tv = v[a];
+                        v[a] = v[b];
+                        v[b] = tv;
+                    }
+                }
+            }
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+        if (j < S.n) out.put(S.s + j, k[j], v[j]);
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return (uint64_t)(uint32_t)hi << 32 | (uint32_t)lo;
+}
+
+// one wave per segment of <= 64 anchors: bitonic sort on (key, y) in registers
+__global__ __launch_bounds__(64) void wave_seg_sort_kernel(const Seg *list, const uint64_t *key, const uint32_t *val,
+                                                           AnchorOut out) {
+    const Seg S = list[blockIdx.x];
+    const int lane = threadIdx.x;
+    uint64_t k = ~0ull;
+    uint32_t v = ~0u;
+    if (lane < S.n) {
+        k = key[S.s + lane];
+        v = val[S.s + lane];
+    }
+    for (int w = 2; w <= 64; w <<= 1)
+        for (int j = w >> 1; j > 0; j >>= 1) {
+            const uint64_t ok = shfl_xor64(k, j);
+            const uint32_t ov = (uint32_t)__shfl_xor((int)v, j, 64);
+            const bool up = (lane & w) == 0, lower = (lane & j) == 0;
+            const bool other_less = ok < k || (ok == k && ov < v);
+            if ((lower == up) == other_less) {  // the lower lane of an ascending pair keeps the min
+                k = ok;
+                v = ov;
+            }
+        }
+    if (lane < S.n) out.put(S.s + lane, k, v);
+}
+
+__device__ __forceinline__ int lds_ix(int e) { return e + (e >> 4); }  // one pad word per 16: blocked access without bank conflicts
+
+// ascending bitonic network over a thread's N words (unrolled: registers only)
+template <int N>
+__device__ __forceinline__ void reg_sort(uint64_t (&k)[N]) {
+#pragma unroll
+    for (int w = 2; w <= N; w <<= 1)
+#pragma unroll
+        for (int j = w >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; i++) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = k[i], b = k[l];
+                    const bool up = (i & w) == 0;
+                    k[i] = up ? min(a, b) : max(a, b);
+                    k[l] = up ? max(a, b) : min(a, b);
+                }
+            }
+}
+
+// one block of BLOCK threads per segment of <= BLOCK * ITEMS anchors: packed words
+// w = (key bits [0, nbits)) << ybits | y sorted by register networks + LDS merge path
+template <int BLOCK, int ITEMS>
+__global__ __launch_bounds__(BLOCK) void block_seg_sort_kernel(const Seg *list, const uint64_t *key, const uint32_t *val,
+                                                               int nbits, int ybits, AnchorOut out) {
+    constexpr int CAP = BLOCK * ITEMS;
+    __shared__ uint64_t sm[CAP + CAP / 16];
+    const Seg S = list[blockIdx.x];
+    const int tid = threadIdx.x;
+    const uint64_t lm = (1ull << nbits) - 1, ym = (1ull << ybits) - 1;
+    const uint64_t hi_bits = key[S.s] & ~lm;
+    for (int e = tid; e < CAP; e += BLOCK)  // coalesced load, striped
+        sm[lds_ix(e)] = e < S.n ? ((key[S.s + e] & lm) << ybits | val[S.s + e]) : ~0ull;
+    __syncthreads();
+    uint64_t k[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) k[j] = sm[lds_ix(tid * ITEMS + j)];
+    reg_sort<ITEMS>(k);
+    for (int run = ITEMS; run < CAP; run <<= 1) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) sm[lds_ix(tid * ITEMS + j)] = k[j];
+        __syncthreads();
+        const int o = tid * ITEMS, base = o & ~(2 * run - 1), diag = o - base;
+        const int a0 = base, b0 = base + run;
+        int lo = max(0, diag - run), hi = min(diag, run);
+        while (lo < hi) {  // merge path: first lo with A[lo] > B[diag - 1 - lo]
+            const int mid = (lo + hi) >> 1;
+            if (sm[lds_ix(a0 + mid)] <= sm[lds_ix(b0 + diag - 1 - mid)]) lo = mid + 1;
+            else hi = mid;
+        }
+        // the thread's ITEMS outputs are the ITEMS smallest of A[ai..] and B[bi..]: min(A[ai + j],
+        // B[bi + ITEMS-1-j]) holds exactly those as a bitonic sequence -- independent LDS
+        // loads and a half-cleaner network instead of a serial merge
+        const int ai = a0 + lo, bi = b0 + diag - lo;
+        const int ae = a0 + run, be = b0 + run;
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const int ia = ai + j, ib = bi + ITEMS - 1 - j;
+            const uint64_t va = ia < ae ? sm[lds_ix(ia)] : ~0ull, vb = ib < be ? sm[lds_ix(ib)] : ~0ull;
+            k[j] = min(va, vb);
+        }
+#pragma unroll
+        for (int d = ITEMS >> 1; d > 0; d >>= 1)
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++)
+                if ((i & d) == 0) {
+                    const uint64_t x = k[i], y = k[i + d];
+                    k[i] = min(x, y);
+                    k[i + d] = max(x, y);
+                }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; j++) sm[lds_ix(tid * ITEMS + j)] = k[j];
+    __syncthreads();
+    for (int e = tid; e < S.n; e += BLOCK) {  // coalesced write
+        const uint64_t w = sm[lds_ix(e)];
+        out.put(S.s + e, hi_bits | w >> ybits, (uint32_t)(w & ym));
+    }
+}
+
+// groups above 4096 anchors: gathered as (rank << pb | rpos, y), sorted together, put back
+__global__ __launch_bounds__(256) void big_gather_kernel(const Seg *list, const int64_t *dst, int pb, const uint64_t *key,
+                                                         const uint32_t *val, uint64_t *tk, uint32_t *tv) {
+    const Seg S = list[blockIdx.x];
+    const int64_t d = dst[blockIdx.x];
+    const uint64_t pm = (1ull << pb) - 1;
+    for (int e = threadIdx.x; e < S.n; e += 256) {
+        tk[d + e] = (uint64_t)blockIdx.x << pb | (key[S.s + e] & pm);
+        tv[d + e] = val[S.s + e];
+    }
+}
+
+// sorted big groups back into place; runs of equal key take their y values in order
+// (insertion sort by the run's first lane; such runs are short and rare)
+__global__ __launch_bounds__(256) void big_put_kernel(const Seg *list, const int64_t *dst, int pb, const uint64_t *key,
+                                                      const uint64_t *tk, const uint32_t *tv, AnchorOut out) {
+    const Seg S = list[blockIdx.x];
+    const int64_t d = dst[blockIdx.x];
+    const uint64_t pm = (1ull << pb) - 1;
+    const uint64_t hi_bits = key[S.s] & ~pm;
+    for (int e = threadIdx.x; e < S.n; e += 256) {
+        const uint64_t k = tk[d + e];
+        const bool prev_eq = e > 0 && tk[d + e - 1] == k;
+        if (prev_eq) continue;
+        int f = e;
+        while (f + 1 < S.n && tk[d + f + 1] == k) f++;
+        if (f == e) {
+            out.put(S.s + e, hi_bits | (k & pm), tv[d + e]);
+            continue;
+        }
+        uint32_t ys[64];
+        const int m = min(f - e + 1, 64);
+        for (int a = 0; a < m; a++) {
+            const uint32_t v = tv[d + e + a];
+            int b = a;
+            while (b > 0 && ys[b - 1] > v) {
+                ys[b] = ys[b - 1];
+                b--;
+            }
+            ys[b] = v;
+        }
+        for (int a = 0; a < m; a++) out.put(S.s + e + a, hi_bits | (k & pm), ys[a]);
+        for (int a = m; a <= f - e; a++) out.put(S.s + e + a, hi_bits | (k & pm), tv[d + e + a]);  // > 64 equal keys: input order
+    }
+}
+
+__global__ void seg_len_kernel(const Seg *list, int n, uint32_t *len) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) len[i] = (uint32_t)list[i].n;
+}
+
+int bits_of(int64_t v) {
+    int b = 1;
+    while ((1ll << b) <= v) b++;
+    return b;
+}
+
+// sort the segments of `lists` (class-major, capacity cap; counts hc), all but the large class
+int sort_segments(hymet_ctx *ctx, const Seg *lists, int64_t cap, const int32_t *hc, const uint64_t *key,
+                  const uint32_t *val, int nbits, int ybits, const AnchorOut &out) {
+    hipStream_t st = ctx->stream;
+#define HY_SEG_LAUNCH(cls, kern, block)                                                                                     \
+    if (hc[cls] > 0) {                                                                                                      \
+        hipLaunchKernelGGL(kern, dim3((unsigned)hc[cls]), dim3(block), 0, st, lists + cls * cap, key, val, nbits, ybits, out); \
+        HY_CHECK_LAUNCH(#kern);                                                                                             \
+    }
+    if (hc[kThread] > 0) {
+        hipLaunchKernelGGL(thread_seg_sort_kernel, dim3((unsigned)cdiv(hc[kThread], 256)), dim3(256), 0, st, lists + kThread * cap,
+                           hc[kThread], key, val, out);
+        HY_CHECK_LAUNCH("thread_seg_sort_kernel");
+    }
+    if (hc[kWave] > 0) {
+        hipLaunchKernelGGL(wave_seg_sort_kernel, dim3((unsigned)hc[kWave]), dim3(64), 0, st, lists + kWave * cap, key, val, out);
+        HY_CHECK_LAUNCH("wave_seg_sort_kernel");
+    }
+    HY_SEG_LAUNCH(kB256, (block_seg_sort_kernel<64, 4>), 64)
+    HY_SEG_LAUNCH(kB512, (block_seg_sort_kernel<64, 8>), 64)
+    HY_SEG_LAUNCH(kB1K, (block_seg_sort_kernel<64, 16>), 64)
+    HY_SEG_LAUNCH(kB2K, (block_seg_sort_kernel<128, 16>), 128)
+    HY_SEG_LAUNCH(kB4K, (block_seg_sort_kernel<256, 16>), 256)
+#undef HY_SEG_LAUNCH
+    return HYMET_OK;
+}
+
+}  // namespace
+
+int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val, int64_t n, const int64_t *d_qoff, int n_q,
+                        int rb, int pb, uint64_t yhi, int64_t max_qlen, uint64_t *okey, uint32_t *oval, uint64_t *ax,
+                        uint64_t *ay) {
+    const int nbins = 1 << (1 + rb);
+    const int ybits = bits_of(max_qlen);
+    if (n <= 0 || n_q <= 0 || 1 + rb + pb + ybits > 63) return 1;
+    hipStream_t st = ctx->stream;
+    const AnchorOut out{okey, ax, ay, rb, pb, yhi};
+    // 1 queries by size
+    DevBuf qlists, qcnt, nt;
+    HY_HIP(qlists.alloc(sizeof(Seg) * kClasses * (size_t)n_q, st));
+    HY_HIP(qcnt.alloc(4 * kClasses, st));
+    HY_HIP(nt.alloc(4 * (size_t)(n_q + 1), st));
+    HY_HIP(hipMemsetAsync(qcnt.p, 0, 4 * kClasses, st));
+    hipLaunchKernelGGL(query_class_kernel, dim3((unsigned)cdiv(n_q, 256)), dim3(256), 0, st, d_qoff, n_q, qlists.as<Seg>(),
+                       (int64_t)n_q, qcnt.as<int32_t>(), nt.as<uint32_t>());
+    HY_CHECK_LAUNCH("query_class_kernel");
+    int32_t hq[kClasses] = {};
+    HY_HIP(hipMemcpyAsync(hq, qcnt.p, 4 * kClasses, hipMemcpyDeviceToHost, st));
+    HY_HIP(hipStreamSynchronize(st));
+    if (hq[kLarge] > 0 && nbins > kMaxBins) return 1;
+    ProfScope _ps(ctx, "mm_anchor_gsort", 60.0 * (double)n);  // key+y read, scatter write, sort read, key+x+y write
+    // 2 small queries: sorted whole
+    int rc = sort_segments(ctx, qlists.as<Seg>(), n_q, hq, key, val, 1 + rb + pb, ybits, out);
+    if (rc || hq[kLarge] == 0) return rc;
+    // 3 large queries: tiles, bin histograms, per-query scan, scatter
+    const int nl = hq[kLarge];
+    const Seg *large = qlists.as<Seg>() + kLarge * (size_t)n_q;
+    DevBuf tpos;
+    HY_HIP(tpos.alloc(8 * (size_t)(n_q + 1), st));
+    int64_t NT = 0;
+    rc = exclusive_scan_u32_i64(ctx, nt.as<uint32_t>(), tpos.as<int64_t>(), n_q, &NT);
+    if (rc) return rc;
+    DevBuf ta0, tq, tn, H;
+    HY_HIP(ta0.alloc(8 * (size_t)NT, st));
+    HY_HIP(tq.alloc(4 * (size_t)NT, st));
+    HY_HIP(tn.alloc(4 * (size_t)NT, st));
+    HY_HIP(H.alloc(4 * (size_t)NT * nbins, st));
+    hipLaunchKernelGGL(tile_map_kernel, dim3((unsigned)cdiv(nl, 256)), dim3(256), 0, st, large, nl, tpos.as<int64_t>(),
+                       ta0.as<int64_t>(), tq.as<int32_t>(), tn.as<int32_t>());
+    HY_CHECK_LAUNCH("tile_map_kernel");
+    hipLaunchKernelGGL(tile_hist_kernel, dim3((unsigned)NT), dim3(256), 0, st, key, ta0.as<int64_t>(), tn.as<int32_t>(), pb,
+                       nbins, H.as<uint32_t>());
+    HY_CHECK_LAUNCH("tile_hist_kernel");
+    const int64_t gcap = std::min<int64_t>(n, NT * (int64_t)nbins);  // a group holds >= 1 anchor
+    HY_ARG(gcap < INT32_MAX, "grouped_anchor_sort: too many groups in one batch");
+    DevBuf groups, ng;
+    HY_HIP(groups.alloc(sizeof(Seg) * (size_t)(gcap + 1), st));
+    HY_HIP(ng.alloc(4, st));
+    HY_HIP(hipMemsetAsync(ng.p, 0, 4, st));
+    hipLaunchKernelGGL(query_scan_kernel, dim3((unsigned)nl), dim3(256), 0, st, large, tpos.as<int64_t>(), nbins,
+                       H.as<uint32_t>(), groups.as<Seg>(), ng.as<int32_t>());
+    HY_CHECK_LAUNCH("query_scan_kernel");
+    hipLaunchKernelGGL(tile_scatter_kernel, dim3((unsigned)NT), dim3(256), 0, st, key, val, ta0.as<int64_t>(), tq.as<int32_t>(),
+                       tn.as<int32_t>(), d_qoff, pb, nbins, H.as<uint32_t>(), okey, oval);
+    HY_CHECK_LAUNCH("tile_scatter_kernel");
+    // 4 groups of the large queries, sorted in place by (rpos, y)
+    int32_t G = 0;
+    HY_HIP(hipMemcpyAsync(&G, ng.p, 4, hipMemcpyDeviceToHost, st));
+    HY_HIP(hipStreamSynchronize(st));
+    if (G == 0) return HYMET_OK;
+    DevBuf glists, gcnt;
+    HY_HIP(glists.alloc(sizeof(Seg) * kClasses * (size_t)G, st));
+    HY_HIP(gcnt.alloc(4 * kClasses, st));
+    HY_HIP(hipMemsetAsync(gcnt.p, 0, 4 * kClasses, st));
+    hipLaunchKernelGGL(group_class_kernel, dim3((unsigned)cdiv(G, 1024)), dim3(256), 0, st, groups.as<Seg>(), (int64_t)G,
+                       glists.as<Seg>(), (int64_t)G, gcnt.as<int32_t>(), okey, oval, out);
+    HY_CHECK_LAUNCH("group_class_kernel");
+    int32_t hg[kClasses] = {};
+    HY_HIP(hipMemcpyAsync(hg, gcnt.p, 4 * kClasses, hipMemcpyDeviceToHost, st));
+    HY_HIP(hipStreamSynchronize(st));
+    rc = sort_segments(ctx, glists.as<Seg>(), (int64_t)G, hg, okey, oval, pb, ybits, out);
+    if (rc) return rc;
+    if (hg[kLarge] > 0) {
+        const int nbig = hg[kLarge];
+        const Seg *big = glists.as<Seg>() + kLarge * (size_t)G;
+        DevBuf blen, bdst, tk, tk2, tv, tv2, tmp;
+        HY_HIP(blen.alloc(4 * (size_t)(nbig + 1), st));
+        HY_HIP(bdst.alloc(8 * (size_t)(nbig + 1), st));
+        hipLaunchKernelGGL(seg_len_kernel, dim3((unsigned)cdiv(nbig, 256)), dim3(256), 0, st, big, nbig, blen.as<uint32_t>());
+        HY_CHECK_LAUNCH("seg_len_kernel");
+        int64_t NB = 0;
+        rc = exclusive_scan_u32_i64(ctx, blen.as<uint32_t>(), bdst.as<int64_t>(), nbig, &NB);
+        if (rc) return rc;
+        HY_HIP(tk.alloc(8 * (size_t)NB, st));
+        HY_HIP(tk2.alloc(8 * (size_t)NB, st));
+        HY_HIP(tv.alloc(4 * (size_t)NB, st));
+        HY_HIP(tv2.alloc(4 * (size_t)NB, st));
+        hipLaunchKernelGGL(big_gather_kernel, dim3((unsigned)nbig), dim3(256), 0, st, big, bdst.as<int64_t>(), pb, okey, oval,
+                           tk.as<uint64_t>(), tv.as<uint32_t>());
+        HY_CHECK_LAUNCH("big_gather_kernel");
+        const int end_bit = pb + bits_of(nbig);
+        size_t tb = 0;
+        HY_HIP(rocprim::radix_sort_pairs(nullptr, tb, tk.as<uint64_t>(), tk2.as<uint64_t>(), tv.as<uint32_t>(), tv2.as<uint32_t>(),
+                                         (size_t)NB, 0, end_bit, st));
+        HY_HIP(tmp.alloc(tb, st));
+        HY_HIP(rocprim::radix_sort_pairs(tmp.p, tb, tk.as<uint64_t>(), tk2.as<uint64_t>(), tv.as<uint32_t>(), tv2.as<uint32_t>(),
+                                         (size_t)NB, 0, end_bit, st));
+        hipLaunchKernelGGL(big_put_kernel, dim3((unsigned)nbig), dim3(256), 0, st, big, bdst.as<int64_t>(), pb, okey,
+                           tk2.as<uint64_t>(), tv2.as<uint32_t>(), out);
+        HY_CHECK_LAUNCH("big_put_kernel");
+    }
+    return HYMET_OK;
+}
+
+}  // namespace mm
+}  // namespace hymet

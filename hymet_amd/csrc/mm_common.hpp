@@ -92,8 +92,19 @@ struct SketchParams {
 // mm_sketch.hip and used by the index builder and the mapper.
 int launch_sketch(hymet_ctx *ctx, int w, bool write, const SketchParams &P);
 
-// exclusive scan of n uint32 counts into int64 offsets; returns the total through *total
+// exclusive scan of n uint32 counts into int64 offsets (scan.hip); returns the total through
+// *total (synchronises the stream)
 int exclusive_scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, int64_t *total);
+// the same, asynchronous: `part` (scratch, kept alive by the caller) ends with the total at
+// index ceil(n / 4096)
+int scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, DevBuf &part);
+
+// Per-query grouped sort of anchor keys (mm_asort.hip): key/val (n, query-major, query offsets
+// d_qoff[n_q + 1]) into the sorted anchor set okey (k1) / ax / ay (oval: scratch).  Returns 1
+// with nothing written where it does not apply (the caller's device sort then runs).
+int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val, int64_t n, const int64_t *d_qoff, int n_q,
+                        int rb, int pb, uint64_t yhi, int64_t max_qlen, uint64_t *okey, uint32_t *oval, uint64_t *ax,
+                        uint64_t *ay);
 
 // Minimizers of a packed set of sequences: host-side chunk bookkeeping + both passes.
 // On success d_x / d_y hold *n_out minimizers in sequence order (sequence-major); if

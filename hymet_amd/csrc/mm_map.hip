@@ -813,27 +813,41 @@ static int sort_anchor_set(hymet_ctx *ctx, DevBuf &x, DevBuf &y, DevBuf &k1, Dev
     return HYMET_OK;
 }
 
-// sort anchor keys (write_anchor_keys_kernel / rechain_keys_kernel) into an AnchorSet: one
-// LSD radix sort over the key's significant bits, then unpack to (x, y)
+// sort anchor keys (write_anchor_keys_kernel / rechain_keys_kernel) into an AnchorSet: the
+// per-query grouped sort (mm_asort.hip), or one LSD radix sort over the key's significant
+// bits where that does not apply (HYMET_ANCHOR_GSORT=0 forces it), then unpack to (x, y)
 static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n, int end_bit, int rb, int pb, int yhi,
-                            AnchorSet &out) {
+                            const int64_t *d_qoff, int n_q, int64_t max_qlen, AnchorSet &out) {
     DevBuf kb, vb;
     HY_HIP(kb.alloc(8 * (size_t)n, ctx->stream));
     HY_HIP(vb.alloc(4 * (size_t)n, ctx->stream));
-    uint64_t *kk = key.as<uint64_t>(), *kka = kb.as<uint64_t>();
-    uint32_t *vv = val.as<uint32_t>(), *vva = vb.as<uint32_t>();
-    int rc = sort_pairs<uint64_t, uint32_t, HYMET_ANCHOR_RB>(ctx, kk, kka, vv, vva, n, 0, end_bit, "radix_sort_anchors");
-    if (rc) return rc;
     HY_HIP(out.ax.alloc(8 * (size_t)n, ctx->stream));
     HY_HIP(out.ay.alloc(8 * (size_t)n, ctx->stream));
+    out.gshift = pb;
+    out.n = n;
+    uint64_t *kk = key.as<uint64_t>(), *kka = kb.as<uint64_t>();
+    uint32_t *vv = val.as<uint32_t>(), *vva = vb.as<uint32_t>();
+    static const bool gsort = [] {
+        const char *e = getenv("HYMET_ANCHOR_GSORT");
+        return !(e && e[0] == '0');
+    }();
+    if (gsort) {
+        const int rc = grouped_anchor_sort(ctx, kk, vv, n, d_qoff, n_q, rb, pb, (uint64_t)yhi, max_qlen, kka, vva,
+                                           out.ax.as<uint64_t>(), out.ay.as<uint64_t>());
+        if (rc == HYMET_OK) {
+            out.k1.swap(kb);
+            return HYMET_OK;
+        }
+        if (rc != 1) return rc;
+    }
+    int rc = sort_pairs<uint64_t, uint32_t, HYMET_ANCHOR_RB>(ctx, kk, kka, vv, vva, n, 0, end_bit, "radix_sort_anchors");
+    if (rc) return rc;
     {
         ProfScope _ps(ctx, "mm_anchor_unpack", 28.0 * (double)n);  // key + value read, x + y write
         LAUNCH1(anchor_unpack_kernel, n, kk, vv, n, rb, pb, (uint64_t)yhi, out.ax.as<uint64_t>(), out.ay.as<uint64_t>());
     }
     if (kk == kb.as<uint64_t>()) out.k1.swap(kb);
     else out.k1.swap(key);
-    out.gshift = pb;
-    out.n = n;
     return HYMET_OK;
 }
 
@@ -1395,8 +1409,12 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     // mm_est_err's minimizer lookup table (filled once seed_n is final, below)
     DevBuf d_qbase, pos_tab;
     std::vector<int64_t> qbase(n_q + 1, 0);  // lives until the call returns (async H2D source)
+    int64_t max_qlen = 1;
     {
-        for (int q = 0; q < n_q; q++) qbase[q + 1] = qbase[q] + h_lens[q];
+        for (int q = 0; q < n_q; q++) {
+            qbase[q + 1] = qbase[q] + h_lens[q];
+            max_qlen = std::max<int64_t>(max_qlen, h_lens[q]);
+        }
         HY_HIP(d_qbase.alloc(8 * (size_t)(n_q + 1), st));
         HY_HIP(hipMemcpyAsync(d_qbase.p, qbase.data(), 8 * (size_t)(n_q + 1), hipMemcpyHostToDevice, st));
         HY_HIP(pos_tab.alloc(4 * (size_t)(qbase[n_q] + 1), st));
@@ -1432,7 +1450,7 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                 HY_CHECK_LAUNCH("write_anchor_keys_kernel");
             }
         }
-        rc = sort_anchor_keys(ctx, key, val, A, key1_bits + pb, rb, pb, k, S1);
+        rc = sort_anchor_keys(ctx, key, val, A, key1_bits + pb, rb, pb, k, S1.d_off.as<int64_t>(), n_q, max_qlen, S1);
         if (rc) return rc;
     } else {
         DevBuf x, y, k1, k2, val;
@@ -1507,7 +1525,7 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                 HY_HIP(val.alloc(4 * (size_t)(A2 + 1), st));
                 LAUNCH1(rechain_keys_kernel, A2, C1.bx.as<uint64_t>(), C1.by.as<uint64_t>(), C1.d_qb.as<int64_t>(),
                         S2.d_off.as<int64_t>(), n_q, A2, rb, pb, key.as<uint64_t>(), val.as<uint32_t>());
-                rc = sort_anchor_keys(ctx, key, val, A2, key1_bits + pb, rb, pb, k, S2);
+                rc = sort_anchor_keys(ctx, key, val, A2, key1_bits + pb, rb, pb, k, S2.d_off.as<int64_t>(), n_q, max_qlen, S2);
                 if (rc) return rc;
             } else {
                 DevBuf x, y, k1, k2, val;

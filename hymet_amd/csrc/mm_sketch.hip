@@ -164,23 +164,6 @@ int launch_sketch(hymet_ctx *ctx, int w, bool write, const SketchParams &P) {
     return HYMET_OK;
 }
 
-int exclusive_scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, int64_t *total) {
-    *total = 0;
-    if (n <= 0) return HYMET_OK;
-    size_t tmp = 0;
-    HY_HIP(rocprim::exclusive_scan(nullptr, tmp, in, out, (int64_t)0, (size_t)n, rocprim::plus<int64_t>(), ctx->stream));
-    DevBuf t;
-    HY_HIP(t.alloc(tmp, ctx->stream));
-    HY_HIP(rocprim::exclusive_scan(t.p, tmp, in, out, (int64_t)0, (size_t)n, rocprim::plus<int64_t>(), ctx->stream));
-    int64_t last_off = 0;
-    uint32_t last_cnt = 0;
-    HY_HIP(hipMemcpyAsync(&last_off, out + n - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
-    HY_HIP(hipMemcpyAsync(&last_cnt, in + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HY_HIP(hipStreamSynchronize(ctx->stream));
-    *total = last_off + last_cnt;
-    return HYMET_OK;
-}
-
 int sketch_sequences(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask, const int64_t *h_starts,
                      const int64_t *h_lens, int n_seq, int w, int k, int rid_mode, DevBuf &d_x, DevBuf &d_y,
                      int64_t *n_out, DevBuf *d_seq_off) {

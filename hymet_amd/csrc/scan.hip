@@ -1,0 +1,148 @@
+// Exclusive prefix sum of uint32 counts into int64 offsets -- the scan behind every
+// count-then-write pass of the library (seed and anchor offsets, group starts, region and
+// text offsets).  Reduce-then-scan over tiles of 4096 counts: per-tile sums, one block
+// scanning the tile sums, then every tile re-read and scanned in LDS with its offset.
+// 16 B of HBM traffic per count (4 + 4 read, 8 written), no per-call state to initialise.
+#include "mm_common.hpp"
+
+namespace hymet {
+namespace mm {
+namespace {
+
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kScanBlock * kScanItems;
+
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
+    const int lo = __shfl_up((int)(uint32_t)v, d, 64), hi = __shfl_up((int)(uint32_t)(v >> 32), d, 64);
+    return (uint64_t)(uint32_t)hi << 32 | (uint32_t)lo;
+}
+
+// inclusive scan across the 64 lanes of a wave
+__device__ __forceinline__ uint64_t wave_incl(uint64_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = shfl_up64(v, d);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+// exclusive scan of one value per thread over a block of NW waves; *total gets the sum
+template <int NW>
+__device__ __forceinline__ uint64_t block_excl(uint64_t v, uint64_t *ws, uint64_t *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t inc = wave_incl(v);
+    if (lane == 63) ws[w] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        if (i < w) before += ws[i];
+        all += ws[i];
+    }
+    __syncthreads();
+    *total = all;
+    return before + inc - v;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint32_t *__restrict__ in, int64_t n,
+                                                                 uint64_t *__restrict__ part) {
+    __shared__ uint64_t ws[kScanBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        const int64_t i = base + j * kScanBlock + threadIdx.x;
+        if (i < n) s += in[i];
+    }
+    uint64_t total;
+    (void)block_excl<kScanBlock / 64>(s, ws, &total);
+    if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+// one block of 1024: tile sums -> exclusive tile offsets; part[nb] = grand total
+__global__ __launch_bounds__(1024) void scan_parts_kernel(uint64_t *part, int64_t nb) {
+    __shared__ uint64_t ws[16];
+    uint64_t carry = 0;
+    for (int64_t b0 = 0; b0 < nb; b0 += 1024) {
+        const int64_t b = b0 + threadIdx.x;
+        const uint64_t v = b < nb ? part[b] : 0;
+        uint64_t total;
+        const uint64_t ex = block_excl<16>(v, ws, &total);
+        if (b < nb) part[b] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) part[nb] = carry;
+}
+
+__device__ __forceinline__ int pad16(int e) { return e + (e >> 4); }
+
+__global__ __launch_bounds__(kScanBlock) void scan_down_kernel(const uint32_t *__restrict__ in, int64_t n,
+                                                               const uint64_t *__restrict__ part, int64_t *__restrict__ out) {
+    __shared__ uint32_t sv[kScanTile + kScanTile / 16];
+    __shared__ int64_t so[kScanTile + kScanTile / 16];
+    __shared__ uint64_t ws[kScanBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {  // coalesced, striped
+        const int e = j * kScanBlock + t;
+        sv[pad16(e)] = base + e < n ? in[base + e] : 0u;
+    }
+    __syncthreads();
+    uint32_t v[kScanItems];
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {  // thread t owns counts t*16 .. t*16+15
+        v[j] = sv[pad16(t * kScanItems + j)];
+        s += v[j];
+    }
+    uint64_t total;
+    uint64_t run = part[blockIdx.x] + block_excl<kScanBlock / 64>(s, ws, &total);
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        so[pad16(t * kScanItems + j)] = (int64_t)run;
+        run += v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        const int e = j * kScanBlock + t;
+        if (base + e < n) out[base + e] = so[pad16(e)];
+    }
+}
+
+}  // namespace
+
+int scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, DevBuf &part) {
+    if (n <= 0) return HYMET_OK;
+    hipStream_t st = ctx->stream;
+    const int64_t nb = cdiv(n, kScanTile);
+    HY_HIP(part.alloc(8 * (size_t)(nb + 1), st));
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>());
+    HY_CHECK_LAUNCH("scan_reduce_kernel");
+    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<uint64_t>(), nb);
+    HY_CHECK_LAUNCH("scan_parts_kernel");
+    hipLaunchKernelGGL(scan_down_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(), out);
+    HY_CHECK_LAUNCH("scan_down_kernel");
+    return HYMET_OK;
+}
+
+int exclusive_scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, int64_t *total) {
+    *total = 0;
+    if (n <= 0) return HYMET_OK;
+    DevBuf part;
+    int rc = scan_u32_i64(ctx, in, out, n, part);
+    if (rc) return rc;
+    const int64_t nb = cdiv(n, kScanTile);
+    uint64_t t = 0;
+    HY_HIP(hipMemcpyAsync(&t, part.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HY_HIP(hipStreamSynchronize(ctx->stream));
+    *total = (int64_t)t;
+    return HYMET_OK;
+}
+
+}  // namespace mm
+}  // namespace hymet
