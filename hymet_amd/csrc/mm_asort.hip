@@ -15,8 +15,11 @@
 //     (rpos, y) in one block, and the larger groups (a query against its own genome) by one
 //     device radix sort over all of them together (key = group rank | rpos).
 // A block sort packs (the key's bits below q or below rid, y) into one 64-bit word, sorts it
-// in registers (bitonic, ITEMS per thread) and merges the runs in LDS (merge path); segments
-// of <= 64 anchors take a wave bitonic sort on (key, y).  Equal keys after the device radix
+// in registers (bitonic, ITEMS per thread) and merges the runs in LDS: merge path splits,
+// then each thread's outputs by a bitonic half-cleaner over two windows of ITEMS words
+// (independent LDS loads instead of a serial merge).  Segments of <= 64 anchors take a wave
+// bitonic sort on (key, y), those of <= 8 a register network in one thread; class lists
+// are filled with one global atomic per class and block.  Equal keys after the device radix
 // sort (one target position hit by several query minimizers) are put in y order on write.
 // The caller falls back to the device sort of the whole batch (return 1) when a large query
 // meets more than 4096 bins (index parts of > 2047 targets) or the packed words would not

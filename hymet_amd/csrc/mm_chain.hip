@@ -65,6 +65,12 @@ namespace {
 #ifndef HYMET_CHAIN_IDQ
 #define HYMET_CHAIN_IDQ 64
 #endif
+// Three anchor chunks in registers (current, next, after next): a colinear batch reads the
+// next chunk, which was then loaded one chunk earlier instead of just now.  On real C4
+// anchors (tools/chain_prof, 16.8M anchors) 97 -> 61 ms, despite 24 B/lane more spill.
+#ifndef HYMET_CHAIN_PF3
+#define HYMET_CHAIN_PF3 1
+#endif
 #ifndef HYMET_CHAIN_WPE  // waves per SIMD the register allocation targets (0: compiler's choice)
 #define HYMET_CHAIN_WPE 4
 #endif
@@ -102,6 +108,19 @@ __device__ unsigned long long g_chain_prof[32];
 #define CPROF(k)
 #define CPROF_FLUSH
 #endif
+// Per-group wall cycles for tools/chain_prof (-DHYMET_CHAIN_GTIME): two clock reads per group,
+// cheap enough not to change the schedule (the section counters above do: ~10x slower).
+#ifdef HYMET_CHAIN_GTIME
+__device__ uint64_t *g_chain_gtime;
+#define GTIME_START const uint64_t _gt0 = wall_clock64();
+#define GTIME_STOP                                                         \
+    do {                                                                   \
+        if (lane == 0 && g_chain_gtime) g_chain_gtime[g] = wall_clock64() - _gt0; \
+    } while (0)
+#else
+#define GTIME_START
+#define GTIME_STOP
+#endif
 
 struct ChainParams {
     const uint64_t *ax;
@@ -117,6 +136,7 @@ struct ChainParams {
     int4 *sum;                // block summaries of every group (group g at ((g_start[g] >> 6) + g) * kSumInts)
     int max_dist, max_dist_inner, bw, max_chn_skip, cap_rmq_size;
     float pen_gap, pen_skip;
+    const int32_t *work_end;  // device: the wave kernel takes work items [0, *work_end) (null: n_work)
 };
 
 __device__ __forceinline__ float mg_log2(float x) {
@@ -327,12 +347,14 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
     sp += kIdq * sizeof(int2);
     int32_t *stamp = reinterpret_cast<int32_t *>(sp);
     const double c = 0.5 * (double)P.pen_gap;
+    const int32_t n_work = P.work_end ? min(P.n_work, *P.work_end) : P.n_work;
     for (;;) {
         int w = 0;
         if (lane == 0) w = atomicAdd(P.work_counter, 1);
         w = __shfl(w, 0, 64);
-        if (w >= P.n_work) break;
+        if (w >= n_work) break;
         const int g = P.order[w];
+        GTIME_START
         const int64_t g0 = P.g_start[g];
         const int32_t n = (int32_t)(P.g_start[g + 1] - g0);
         const bool qfirst = P.g_qfirst[g] != 0;
@@ -445,6 +467,9 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         __builtin_amdgcn_wave_barrier();
         // double-buffered anchor chunks: lane l holds anchor (chunk base + l)
         uint64_t nx = 0, ny = 0, cx = 0, cy = 0;
+#if HYMET_CHAIN_PF3
+        uint64_t nnx = 0, nny = 0;
+#endif
         Ent prev{0, 0, 0, 0};  // anchor i-1
         // block b complete: staircase summary -- S1 = argmin, S(k+1) = argmin over y < y(Sk),
         // i.e. the entries better than every entry with y <= theirs, by y descending; the
@@ -572,6 +597,22 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         for (; i < n;) {
             CPROF(7);
             if ((i >> 6) != (cb >> 6)) {
+#if HYMET_CHAIN_PF3
+                // three chunks in registers: the batch reads chunk c+1, loaded a chunk earlier
+                if ((i >> 6) == (cb >> 6) + 1) {
+                    cx = nx, cy = ny, nx = nnx, ny = nny;
+                } else {
+                    const int32_t b = (i & ~63) + lane;
+                    cx = b < n ? P.ax[g0 + b] : 0;
+                    cy = b < n ? P.ay[g0 + b] : 0;
+                    nx = b + 64 < n ? P.ax[g0 + b + 64] : 0;
+                    ny = b + 64 < n ? P.ay[g0 + b + 64] : 0;
+                }
+                cb = i & ~63;
+                const int32_t b = cb + 128 + lane;
+                nnx = b < n ? P.ax[g0 + b] : 0;
+                nny = b < n ? P.ay[g0 + b] : 0;
+#else
                 if ((i >> 6) == (cb >> 6) + 1) {
                     cx = nx, cy = ny;
                 } else {
@@ -583,6 +624,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 const int32_t b = cb + 64 + lane;
                 nx = b < n ? P.ax[g0 + b] : 0;
                 ny = b < n ? P.ay[g0 + b] : 0;
+#endif
             }
             const int32_t xi = rl((int32_t)cx, i & 63);
             const int32_t yi = rl((int32_t)cy, i & 63);
@@ -1080,6 +1122,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             ++i;
         }
         CPROF_FLUSH;
+        GTIME_STOP;
     }
 }
 
@@ -1402,19 +1445,150 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
 
 }  // namespace
 
+
+// ---- small groups: one LANE per group of <= kSmall anchors
+// A wave spends ~30 us of fixed latency on every group it takes (work-list atomic, group
+// bounds, the chunk loads, f/p stores), which made groups of 3-16 anchors more than half of
+// the kernel's wave time on C4 anchors.  Here 64 such groups run side by side, each lane
+// replaying mg_lchain_rmq (lchain.c; oracle/mm_oracle.c chain_group) on its group with the
+// group in registers: the window trees become bit masks and brute-force scans over <= 16
+// entries, the inner walk a scan of the (y, idx) order.  Same decisions, same f/p.
+#ifndef HYMET_CHAIN_SMALL
+#define HYMET_CHAIN_SMALL 16
+#endif
+constexpr int kSmall = HYMET_CHAIN_SMALL;  // <= 32 (window sets are 32-bit masks)
+
+// first work item whose group has <= kSmall anchors (the list is size-descending)
+__global__ void chain_small_split_kernel(const int64_t *g_start, const int32_t *order, int32_t n_work, int32_t *split) {
+    if (threadIdx.x != 0) return;
+    int32_t lo = 0, hi = n_work;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        const int g = order[mid];
+        if (g_start[g + 1] - g_start[g] <= kSmall) hi = mid;
+        else lo = mid + 1;
+    }
+    *split = lo;
+}
+
+__global__ __launch_bounds__(64) void chain_small_kernel(ChainParams P, const int32_t *split) {
+    const int32_t w = *split + (int32_t)(blockIdx.x * 64 + threadIdx.x);
+    if (w >= P.n_work) return;
+    const int g = P.order[w];
+    const int64_t g0 = P.g_start[g];
+    const int n = (int)(P.g_start[g + 1] - g0);
+    const bool qfirst = P.g_qfirst[g] != 0;
+    const double c = 0.5 * (double)P.pen_gap;
+    int32_t X[kSmall], Y[kSmall], SP[kSmall], F[kSmall], PJ[kSmall], T[kSmall];
+    int8_t ord[kSmall];  // local indices by (y, idx) ascending
+    for (int j = 0; j < n; ++j) {
+        const uint64_t x = P.ax[g0 + j], y = P.ay[g0 + j];
+        X[j] = (int32_t)x, Y[j] = (int32_t)y, SP[j] = (int32_t)(y >> 32 & 0xff);
+        F[j] = 0, PJ[j] = -1, T[j] = -1;
+        int k = j;  // insertion by (y, idx): later j is the larger idx, so ties stay behind
+        while (k > 0 && Y[ord[k - 1]] > Y[j]) {
+            ord[k] = ord[k - 1];
+            --k;
+        }
+        ord[k] = (int8_t)j;
+    }
+    uint32_t in_out = 0, in_in = 0;
+    int size_out = 0, size_in = 0, i0 = 0, st = 0, st_in = 0;
+    for (int i = 0; i < n; ++i) {
+        const int32_t xi = X[i], yi = Y[i];
+        int32_t max_f = SP[i], max_j = -1;
+        if (i0 < i && X[i0] != xi) {
+            for (int j = i0; j < i; ++j) {
+                in_out |= 1u << j, size_out++;
+                if (P.max_dist_inner > 0) in_in |= 1u << j, size_in++;
+            }
+            i0 = i;
+        }
+        while (st < i && ((int64_t)(uint32_t)xi > (int64_t)(uint32_t)X[st] + P.max_dist || size_out > P.cap_rmq_size)) {
+            if (st < i0) in_out &= ~(1u << st), size_out--;
+            ++st;
+        }
+        if (P.max_dist_inner > 0)
+            while (st_in < i &&
+                   ((int64_t)(uint32_t)xi > (int64_t)(uint32_t)X[st_in] + P.max_dist_inner || size_in > P.cap_rmq_size)) {
+                if (st_in < i0) in_in &= ~(1u << st_in), size_in--;
+                ++st_in;
+            }
+        // RMQ over (yi - max_dist, yi) in (y, idx) order; the query's anchor 0 also at y == yi
+        double bp = 0.0;
+        int32_t bj = -1;
+        const int32_t ylo = yi - P.max_dist;
+        for (uint32_t m = in_out; m; m &= m - 1) {
+            const int j = __ffs(m) - 1;
+            const int32_t yj = Y[j];
+            if (yj > ylo && (yj < yi || (yj == yi && qfirst && j == 0))) {
+                const double pr = prio(F[j], X[j], yj, c);
+                if (better(pr, j, bp, bj)) bp = pr, bj = j;
+            }
+        }
+        if (bj >= 0) {
+            int32_t exact, width;
+            const int32_t sc = F[bj] + comput_sc(xi, yi, X[bj], Y[bj], SP[bj], P.pen_gap, P.pen_skip, &exact, &width);
+            if (width <= P.bw && sc > max_f) max_f = sc, max_j = bj;
+            if (!exact && size_in > 0 && yi > 0) {
+                const int32_t ylo_in = yi - P.max_dist_inner;
+                int r = n - 1;  // last (y, idx) with y < yi
+                while (r >= 0 && Y[ord[r]] >= yi) --r;
+                int n_skip = 0;
+                for (; r >= 0; --r) {
+                    const int jj = ord[r];
+                    if (Y[jj] < ylo_in) break;
+                    if (!(in_in >> jj & 1)) continue;
+                    int32_t ex2, w2;
+                    const int32_t sc2 = F[jj] + comput_sc(xi, yi, X[jj], Y[jj], SP[jj], P.pen_gap, P.pen_skip, &ex2, &w2);
+                    if (w2 <= P.bw) {
+                        if (sc2 > max_f) {
+                            max_f = sc2, max_j = jj;
+                            if (n_skip > 0) --n_skip;
+                        } else if (T[jj] == i) {
+                            if (++n_skip > P.max_chn_skip) break;
+                        }
+                        if (PJ[jj] >= 0) T[PJ[jj]] = i;
+                    }
+                }
+            }
+        }
+        F[i] = max_f, PJ[i] = max_j;
+        P.f[g0 + i] = max_f;
+        P.p[g0 + i] = max_j < 0 ? -1 : g0 + max_j;
+    }
+}
+
+// The chaining launches for a work list: the small-group split, the wave kernel on the
+// groups above kSmall anchors, the lane kernel on the rest.  `split` is device scratch.
+int launch_chain_raw(hipStream_t st, const ChainParams &P0, int64_t blocks, int32_t *split) {
+    ChainParams P = P0;
+    hipLaunchKernelGGL(chain_small_split_kernel, dim3(1), dim3(64), 0, st, P.g_start, P.order, P.n_work, split);
+    HY_CHECK_LAUNCH("chain_small_split_kernel");
+    P.work_end = split;
+    const bool long_pass = P.max_dist > 10000;
+    if (long_pass) hipLaunchKernelGGL(chain_groups_kernel<1>, dim3((unsigned)blocks), dim3(64), kChainLds, st, P);
+    else hipLaunchKernelGGL(chain_groups_kernel<0>, dim3((unsigned)blocks), dim3(64), kChainLds, st, P);
+    HY_CHECK_LAUNCH("chain_groups_kernel");
+    hipLaunchKernelGGL(chain_small_kernel, dim3((unsigned)cdiv(P.n_work, 64)), dim3(64), 0, st, P, (const int32_t *)split);
+    HY_CHECK_LAUNCH("chain_small_kernel");
+    return HYMET_OK;
+}
+
 int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *g_start, const uint8_t *g_qfirst,
                  const int32_t *order, int32_t n_work, int32_t *f, int64_t *p, int32_t *t_global, int max_dist,
                  int max_dist_inner, int bw, int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip,
                  int64_t n_anchors, int64_t n_groups) {
     if (n_work <= 0) return HYMET_OK;
-    DevBuf cnt, sum;
+    DevBuf cnt, sum, split;
     const size_t n_sum = (size_t)(n_anchors >> 6) + (size_t)n_groups + 2;
     HY_HIP(sum.alloc(16 * kSumInts * n_sum, ctx->stream));
     HY_HIP(cnt.alloc(4, ctx->stream));
+    HY_HIP(split.alloc(4, ctx->stream));
     HY_HIP(hipMemsetAsync(cnt.p, 0, 4, ctx->stream));
     if (max_dist < bw) max_dist = bw;
     if (max_dist_inner <= 0 || max_dist_inner >= max_dist) max_dist_inner = 0;
-    ChainParams P{ax, ay, g_start, g_qfirst, order, n_work, cnt.as<int32_t>(), f, p, t_global, sum.as<int4>(), max_dist, max_dist_inner, bw, max_chn_skip, cap_rmq_size, pen_gap, pen_skip};
+    ChainParams P{ax, ay, g_start, g_qfirst, order, n_work, cnt.as<int32_t>(), f, p, t_global, sum.as<int4>(), max_dist, max_dist_inner, bw, max_chn_skip, cap_rmq_size, pen_gap, pen_skip, nullptr};
     // one wave per block, as many resident per CU as registers and LDS allow
     int64_t blocks = n_work;
     int per_cu = 0;
@@ -1426,9 +1600,7 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
     const int64_t cap = (int64_t)ctx->n_cu * per_cu;
     if (blocks > cap) blocks = cap;
     ProfScope _ps(ctx, max_dist > 10000 ? "mm_chain_long" : "mm_chain", 28.0 * (double)n_anchors);  // x,y read + f,p write per anchor
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64), kChainLds, ctx->stream, P);
-    HY_CHECK_LAUNCH("chain_groups_kernel");
-    return HYMET_OK;
+    return launch_chain_raw(ctx->stream, P, blocks, split.as<int32_t>());
 }
 
 int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, const int64_t *p, int32_t *t,

@@ -76,6 +76,11 @@ int main(int argc, char **argv) {
     std::vector<int32_t> h_order(G);
     for (int g = 0; g < G; g++) h_order[g] = g;
     std::sort(h_order.begin(), h_order.end(), [&](int a, int b) { return h_gs[a + 1] - h_gs[a] > h_gs[b + 1] - h_gs[b]; });
+    // the library's work list holds groups of >= min_cnt (3) anchors only
+    int nwork = 0;
+    while (nwork < G && h_gs[h_order[nwork] + 1] - h_gs[h_order[nwork]] >= 3) nwork++;
+    int32_t *split;
+    CK(hipMalloc(&split, 4));
     std::vector<uint8_t> h_qf(G, 0);
     h_qf[0] = 1;
     CK(hipFree(gs));
@@ -89,27 +94,67 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(qf, h_qf.data(), G, hipMemcpyHostToDevice));
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
-    const int nblk = std::min(G, prop.multiProcessorCount * 8);
+    // waves per CU as the library launches them (launch_chain: 16), HYMET_CHAIN_PROF_WPC overrides
+    const char *wpc = getenv("HYMET_CHAIN_PROF_WPC");
+    const int nblk = std::min(nwork, prop.multiProcessorCount * (wpc ? atoi(wpc) : 16));
     int max_dist = 10000 < bw ? bw : 10000;
     for (int rep = 0; rep < 2; rep++) {
         unsigned long long z[32] = {0};
+#ifdef HYMET_CHAIN_PROF
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_prof), z, sizeof(z)));
+#endif
         CK(hipMemset(cnt, 0, 4));
         CK(hipMemset(df, 0, 4 * n));
         CK(hipMemset(dp, 0xFF, 8 * n));
         CK(hipMemset(dt, 0xFF, 4 * n));
-        ChainParams P{dx, dy, gs, qf, order, G, cnt, df, dp, dt, sum, max_dist, 1000, bw, 25, 100000, 0.12f, 0.0f};
+        ChainParams P{dx, dy, gs, qf, order, nwork, cnt, df, dp, dt, sum, max_dist, 1000, bw, 25, 100000, 0.12f, 0.0f, nullptr};
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
+#ifdef HYMET_CHAIN_GTIME
+        uint64_t *gt;
+        CK(hipMalloc(&gt, 8 * (size_t)G));
+        CK(hipMemset(gt, 0, 8 * (size_t)G));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_gtime), &gt, sizeof(gt)));
+#endif
         CK(hipEventRecord(e0, 0));
-        hipLaunchKernelGGL(chain_groups_kernel<0>, dim3(nblk), dim3(64), kChainLds, 0, P);
-        CK(hipGetLastError());
+        if (getenv("HYMET_CHAIN_PROF_WAVE_ONLY")) {
+            hipLaunchKernelGGL(chain_groups_kernel<0>, dim3(nblk), dim3(64), kChainLds, 0, P);
+            CK(hipGetLastError());
+        } else if (launch_chain_raw(0, P, nblk, split) != 0) {
+            return 1;
+        }
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
         float ms = 0;
         CK(hipEventElapsedTime(&ms, e0, e1));
+#ifdef HYMET_CHAIN_PROF
         CK(hipMemcpyFromSymbol(z, HIP_SYMBOL(g_chain_prof), sizeof(z)));
+#endif
+#ifdef HYMET_CHAIN_GTIME
+        {  // per-group wall time (wall_clock64 ticks) by size class
+            std::vector<uint64_t> h(G);
+            CK(hipMemcpy(h.data(), gt, 8 * (size_t)G, hipMemcpyDeviceToHost));
+            CK(hipFree(gt));
+            int wclk = 100000;  // kHz
+            (void)hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, 0);
+            const int64_t lim[] = {3, 8, 16, 32, 64, 128, 256, 1024, 4096, 16384, INT64_MAX};
+            double tc[11] = {0}, na[11] = {0}, mx[11] = {0};
+            double tot = 0;
+            for (int g = 0; g < G; g++) {
+                const int64_t sz = h_gs[g + 1] - h_gs[g];
+                int c = 0;
+                while (sz > lim[c]) c++;
+                const double us = h[g] / (wclk / 1000.0);
+                tc[c] += us, na[c] += sz, tot += us, mx[c] = std::max(mx[c], us);
+            }
+            printf("wave-time %.1f ms total over %d groups (kernel wall x waves = %.1f ms)\n", tot / 1e3, G, ms * nblk);
+            for (int c = 0; c < 11; c++)
+                if (na[c] > 0)
+                    printf("  groups <= %6lld: %7.1f%% of wave-time, %8.3f us/anchor, max group %8.1f us\n",
+                           (long long)(c < 10 ? lim[c] : -1), 100.0 * tc[c] / tot, tc[c] / na[c], mx[c]);
+        }
+#endif
         const char *names[8] = {"i0-advance", "st+head", "st_in", "rmq", "walk", "winner+cert", "st_in-probe", "loop/batch"};
         double tot = 0;
         for (int k = 0; k < 8; k++) tot += (double)z[k];
