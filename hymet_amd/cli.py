@@ -280,6 +280,17 @@ def cmd_taxonomy_hierarchy(argv: Sequence[str]) -> int:
     return 0
 
 
+def cmd_download_db(argv: Sequence[str]) -> int:
+    """scripts/downloadDB.py <genomes_file> <output_dir> <taxonomy_file> <cache_dir>, offline
+    (SURVEY.md §8f-2): genomes already in output_dir, summaries cached in cache_dir."""
+    from .cache import build_cache
+    if len(argv) != 4:
+        print("Usage: python3 download_genomes.py <genomes_file> <output_dir> <taxonomy_file> <cache_dir>")
+        return 1
+    build_cache(argv[0], argv[1], argv[2], argv[3], log=lambda m: print(m, file=sys.stderr))
+    return 0
+
+
 def main(argv: Optional[Sequence[str]] = None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     if not argv:
@@ -306,6 +317,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         return cmd_hymet2cami(rest)
     if cmd == "taxonomy-hierarchy":
         return cmd_taxonomy_hierarchy(rest)
+    if cmd == "download-db":
+        return cmd_download_db(rest)
     print(f"unknown subcommand {cmd!r}", file=sys.stderr)
     return 2
 

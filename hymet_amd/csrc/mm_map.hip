@@ -1470,28 +1470,31 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     }
     tr.mark("anchors+sort");
     // HYMET_DUMP_ANCHORS=path (profiling, tools/chain_prof): the first call's sorted first-pass
-    // anchors as (x, y) pairs with x>>32 replaced by the (query, strand, target) group ordinal
-    if (const char *dump = getenv("HYMET_DUMP_ANCHORS")) {
-        static bool dumped = false;
-        if (!dumped && S1.n > 0) {
-            dumped = true;
-            const int64_t nd = std::min<int64_t>(S1.n, 1 << 24);
-            std::vector<uint64_t> hx(nd), hy(nd), hk(nd);
-            HY_HIP(hipMemcpyAsync(hx.data(), S1.ax.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
-            HY_HIP(hipMemcpyAsync(hy.data(), S1.ay.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
-            HY_HIP(hipMemcpyAsync(hk.data(), S1.k1.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
-            HY_HIP(hipStreamSynchronize(st));
-            if (FILE *fp = fopen(dump, "wb")) {
-                uint64_t gid = 0;
-                for (int64_t a = 0; a < nd; a++) {
-                    if (a && (hk[a] >> S1.gshift) != (hk[a - 1] >> S1.gshift)) gid++;
-                    const uint64_t v[2] = {gid << 32 | (uint32_t)hx[a], hy[a]};
-                    fwrite(v, 8, 2, fp);
-                }
-                fclose(fp);
+    // anchors as (x, y) pairs with x>>32 replaced by the (query, strand, target) group ordinal;
+    // HYMET_DUMP_ANCHORS2=path: the same for the long-join re-chain's anchors
+    auto dump_anchors = [&](const char *path, AnchorSet &S, bool &dumped) -> int {
+        if (!path || dumped || S.n == 0) return HYMET_OK;
+        dumped = true;
+        const int64_t nd = std::min<int64_t>(S.n, 1 << 24);
+        std::vector<uint64_t> hx(nd), hy(nd), hk(nd);
+        HY_HIP(hipMemcpyAsync(hx.data(), S.ax.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
+        HY_HIP(hipMemcpyAsync(hy.data(), S.ay.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
+        HY_HIP(hipMemcpyAsync(hk.data(), S.k1.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
+        HY_HIP(hipStreamSynchronize(st));
+        if (FILE *fp = fopen(path, "wb")) {
+            uint64_t gid = 0;
+            for (int64_t a = 0; a < nd; a++) {
+                if (a && (hk[a] >> S.gshift) != (hk[a - 1] >> S.gshift)) gid++;
+                const uint64_t v[2] = {gid << 32 | (uint32_t)hx[a], hy[a]};
+                fwrite(v, 8, 2, fp);
             }
+            fclose(fp);
         }
-    }
+        return HYMET_OK;
+    };
+    static bool dumped1 = false, dumped2 = false;
+    rc = dump_anchors(getenv("HYMET_DUMP_ANCHORS"), S1, dumped1);
+    if (rc) return rc;
     // ------------------------------------------------ 6 chain (+ 7 long join)
     ChainSet C1;
     rc = chain_set(ctx, opt, pen_gap, pen_skip, opt->bw, S1, n_q, C1);
@@ -1526,6 +1529,8 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                 LAUNCH1(rechain_keys_kernel, A2, C1.bx.as<uint64_t>(), C1.by.as<uint64_t>(), C1.d_qb.as<int64_t>(),
                         S2.d_off.as<int64_t>(), n_q, A2, rb, pb, key.as<uint64_t>(), val.as<uint32_t>());
                 rc = sort_anchor_keys(ctx, key, val, A2, key1_bits + pb, rb, pb, k, S2.d_off.as<int64_t>(), n_q, max_qlen, S2);
+                if (rc) return rc;
+                rc = dump_anchors(getenv("HYMET_DUMP_ANCHORS2"), S2, dumped2);
                 if (rc) return rc;
             } else {
                 DevBuf x, y, k1, k2, val;
