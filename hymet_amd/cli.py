@@ -18,6 +18,10 @@
         == tools/hymet2cami.py (CAMI profile export, run_hymet_cami.sh:214-218)
     python -m hymet_amd.cli taxonomy-hierarchy [NAMES_DMP NODES_DMP OUT]
         == scripts/taxonomy_hierarchy.py (taxdump -> taxonomy_hierarchy.tsv)
+    python -m hymet_amd.cli download-db GENOMES_FILE OUTPUT_DIR TAXONOMY_FILE CACHE_DIR
+        == scripts/downloadDB.py:178-249 offline (detailed_taxonomy.tsv, combined_genomes.fasta)
+    python -m hymet_amd.cli eval-cami [--pred-profile ... --outdir D]
+        == tools/eval_cami.py (CAMI profile and contig metrics)
 
 The thin wrappers under scripts/ call these, so run_hymet_cami.sh / main.pl can use them
 in place of the reference stage scripts unchanged.  All device work goes through
@@ -319,6 +323,9 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         return cmd_taxonomy_hierarchy(rest)
     if cmd == "download-db":
         return cmd_download_db(rest)
+    if cmd == "eval-cami":
+        from .evaluate import main as eval_main
+        return eval_main(rest)
     print(f"unknown subcommand {cmd!r}", file=sys.stderr)
     return 2
 
