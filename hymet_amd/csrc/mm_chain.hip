@@ -71,6 +71,10 @@ namespace {
 #ifndef HYMET_CHAIN_PF3
 #define HYMET_CHAIN_PF3 1
 #endif
+// A colinear batch's pre-batch best B from the O(1) window sources when they decide it.
+#ifndef HYMET_CHAIN_B0FAST
+#define HYMET_CHAIN_B0FAST 1
+#endif
 #ifndef HYMET_CHAIN_WPE  // waves per SIMD the register allocation targets (0: compiler's choice)
 #define HYMET_CHAIN_WPE 4
 #endif
@@ -112,14 +116,20 @@ __device__ unsigned long long g_chain_prof[32];
 // cheap enough not to change the schedule (the section counters above do: ~10x slower).
 #ifdef HYMET_CHAIN_GTIME
 __device__ uint64_t *g_chain_gtime;
-#define GTIME_START const uint64_t _gt0 = wall_clock64();
-#define GTIME_STOP                                                         \
-    do {                                                                   \
+__device__ int4 *g_chain_gcnt;  // per group: loop iterations, batch attempts, batches, batch anchors
+#define GTIME_START                         \
+    const uint64_t _gt0 = wall_clock64();   \
+    int4 _gc = make_int4(0, 0, 0, 0);
+#define GCNT(f, v) (_gc.f += (v))
+#define GTIME_STOP                                                                \
+    do {                                                                          \
         if (lane == 0 && g_chain_gtime) g_chain_gtime[g] = wall_clock64() - _gt0; \
+        if (lane == 0 && g_chain_gcnt) g_chain_gcnt[g] = _gc;                      \
     } while (0)
 #else
 #define GTIME_START
 #define GTIME_STOP
+#define GCNT(f, v)
 #endif
 
 struct ChainParams {
@@ -595,6 +605,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         int32_t cb = -128;  // base of the chunk in cx/cy; nx/ny hold the next one
         int32_t spec_next = 0, spec_gap = 2;  // next batch attempt (back-off after short batches)
         for (; i < n;) {
+            GCNT(x, 1);
             CPROF(7);
             if ((i >> 6) != (cb >> 6)) {
 #if HYMET_CHAIN_PF3
@@ -806,9 +817,31 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 if (walk_ok && Lb >= 2) {
                     const int offl = (i - cb) + Lb - 1;
                     const int32_t ymax = (int32_t)(offl < 64 ? rl((int32_t)cy, offl) : rl((int32_t)ny, offl - 64));
+#if HYMET_CHAIN_B0FAST
+                    // the window's best ignoring y (head suffix, block deque front, tail argmin:
+                    // the O(1) sources step 4 uses) is B when its y <= Y -- the colinear case;
+                    // only otherwise scan the block summaries
+                    bool cert = st <= (fe << 6);
+                    double gp = 0.0;
+                    int32_t gj = -1, gy = 0;
+                    if (cert) {
+                        if (st < (fb << 6)) {
+                            const int4 v = hsuf[st & 63];
+                            gp = st_pr(v), gj = v.z, gy = v.w;
+                        }
+                        if (fb < fe) {
+                            if (!bok) cert = false;
+                            else if (better(bf_pr, bf_j, gp, gj)) gp = bf_pr, gj = bf_j, gy = bf_y;
+                        }
+                        if ((fe << 6) < i0 && better(t_pr, t_j, gp, gj)) gp = t_pr, gj = t_j, gy = t_y;
+                    }
+                    if (cert && gj >= 0 && gy <= ymax) b0p = gp, b0j = gj;
+                    else
+#endif
                     window_best(ymax == INT32_MAX ? ymax : ymax + 1, INT32_MIN, false, b0p, b0j);
                 }
                 CCOUNT(8);
+                GCNT(y, 1);
                 if (b0j != i - 1) CCOUNT(10);
                 if (!walk_ok) CCOUNT(11);
                 if (b0j == i - 1 && walk_ok && Lb >= 2) {
@@ -905,6 +938,8 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         }
                         __builtin_amdgcn_wave_barrier();
                         CCOUNT(7);
+                        GCNT(z, 1);
+                        GCNT(w, acc);
                         const int nins = acc - 1;
                         if (nins > 0) {
                             if (P.max_dist_inner > 0) {

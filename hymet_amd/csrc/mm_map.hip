@@ -899,6 +899,9 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
             HY_HIP(hipMemcpyAsync(&k0, kp, 4, hipMemcpyDeviceToHost, ctx->stream));
             HY_HIP(hipStreamSynchronize(ctx->stream));
             HY_ARG(~k0 < (1u << 24) - 1, "hymet_mm_map: an anchor group exceeds 2^24 anchors");
+            static const bool stats = getenv("HYMET_CHAIN_STATS") != nullptr;  // profiling: tail size per launch
+            if (stats) fprintf(stderr, "[chain] bw %d anchors %lld groups %lld work %lld largest %u\n", bw, (long long)n,
+                               (long long)G, (long long)n_work, ~k0);
         }
         DevBuf f, p, t;
         HY_HIP(f.alloc(4 * (size_t)n, ctx->stream));

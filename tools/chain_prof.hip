@@ -116,6 +116,10 @@ int main(int argc, char **argv) {
         CK(hipMalloc(&gt, 8 * (size_t)G));
         CK(hipMemset(gt, 0, 8 * (size_t)G));
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_gtime), &gt, sizeof(gt)));
+        int4 *gc;
+        CK(hipMalloc(&gc, 16 * (size_t)G));
+        CK(hipMemset(gc, 0, 16 * (size_t)G));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_gcnt), &gc, sizeof(gc)));
 #endif
         CK(hipEventRecord(e0, 0));
         if (getenv("HYMET_CHAIN_PROF_WAVE_ONLY")) {
@@ -136,10 +140,13 @@ int main(int argc, char **argv) {
             std::vector<uint64_t> h(G);
             CK(hipMemcpy(h.data(), gt, 8 * (size_t)G, hipMemcpyDeviceToHost));
             CK(hipFree(gt));
+            std::vector<int4> hc(G);
+            CK(hipMemcpy(hc.data(), gc, 16 * (size_t)G, hipMemcpyDeviceToHost));
+            CK(hipFree(gc));
             int wclk = 100000;  // kHz
             (void)hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, 0);
             const int64_t lim[] = {3, 8, 16, 32, 64, 128, 256, 1024, 4096, 16384, INT64_MAX};
-            double tc[11] = {0}, na[11] = {0}, mx[11] = {0};
+            double tc[11] = {0}, na[11] = {0}, mx[11] = {0}, it[11] = {0}, ba[11] = {0}, bn[11] = {0}, bx[11] = {0};
             double tot = 0;
             for (int g = 0; g < G; g++) {
                 const int64_t sz = h_gs[g + 1] - h_gs[g];
@@ -147,12 +154,15 @@ int main(int argc, char **argv) {
                 while (sz > lim[c]) c++;
                 const double us = h[g] / (wclk / 1000.0);
                 tc[c] += us, na[c] += sz, tot += us, mx[c] = std::max(mx[c], us);
+                it[c] += hc[g].x, ba[c] += hc[g].y, bn[c] += hc[g].z, bx[c] += hc[g].w;
             }
             printf("wave-time %.1f ms total over %d groups (kernel wall x waves = %.1f ms)\n", tot / 1e3, G, ms * nblk);
             for (int c = 0; c < 11; c++)
                 if (na[c] > 0)
-                    printf("  groups <= %6lld: %7.1f%% of wave-time, %8.3f us/anchor, max group %8.1f us\n",
-                           (long long)(c < 10 ? lim[c] : -1), 100.0 * tc[c] / tot, tc[c] / na[c], mx[c]);
+                    printf("  groups <= %6lld: %7.1f%% of wave-time, %8.3f us/anchor, max group %8.1f us; per anchor: "
+                           "%.3f iterations, %.4f batch attempts, %.4f batches, %.3f in batches; %.2f us/iteration\n",
+                           (long long)(c < 10 ? lim[c] : -1), 100.0 * tc[c] / tot, tc[c] / na[c], mx[c], it[c] / na[c],
+                           ba[c] / na[c], bn[c] / na[c], bx[c] / na[c], tc[c] / std::max(1.0, it[c]));
         }
 #endif
         const char *names[8] = {"i0-advance", "st+head", "st_in", "rmq", "walk", "winner+cert", "st_in-probe", "loop/batch"};
