@@ -489,10 +489,25 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             const Ent e = fetch(jl);
             const double pl = prio(e.f, e.x, e.y, c);
             bool rec = true;
-            for (int k = 0; k < 64; ++k) {
-                const int32_t yk = rl(e.y, k);
-                const double pk = rld(pl, k);
-                if (k != lane && yk <= e.y && better(pk, (b << 6) + k, pl, jl)) rec = false;
+            // y strictly increasing along the block (a colinear stretch): the entries with
+            // y <= y_l are lanes [0, l], so l is a record iff it is the prefix best there
+            const int32_t ynx = __shfl_down(e.y, 1, 64);
+            if (__ballot(lane == 63 || e.y < ynx) == ~0ull) {
+                double bp = pl;
+                int32_t bj = jl;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const double op = __shfl_up(bp, d, 64);
+                    const int32_t oj = __shfl_up(bj, d, 64);
+                    if (lane >= d && better(op, oj, bp, bj)) bp = op, bj = oj;
+                }
+                rec = bj == jl;
+            } else {
+                for (int k = 0; k < 64; ++k) {
+                    const int32_t yk = rl(e.y, k);
+                    const double pk = rld(pl, k);
+                    if (k != lane && yk <= e.y && better(pk, (b << 6) + k, pl, jl)) rec = false;
+                }
             }
             const uint64_t recm = __ballot(rec);
             int rank = 0;  // records with larger y (records have distinct y)
