@@ -52,10 +52,19 @@ __global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint32_t 
     __shared__ uint64_t ws[kScanBlock / 64];
     const int64_t base = (int64_t)blockIdx.x * kScanTile;
     uint64_t s = 0;
+    if (base + kScanTile <= n && ((uintptr_t)in & 15) == 0) {  // full tile: 16-byte loads
+        const uint4 *v = reinterpret_cast<const uint4 *>(in + base);
 #pragma unroll
-    for (int j = 0; j < kScanItems; j++) {
-        const int64_t i = base + j * kScanBlock + threadIdx.x;
-        if (i < n) s += in[i];
+        for (int j = 0; j < kScanItems / 4; j++) {
+            const uint4 q = v[j * kScanBlock + threadIdx.x];
+            s += (uint64_t)q.x + q.y + q.z + q.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kScanItems; j++) {
+            const int64_t i = base + j * kScanBlock + threadIdx.x;
+            if (i < n) s += in[i];
+        }
     }
     uint64_t total;
     (void)block_excl<kScanBlock / 64>(s, ws, &total);
@@ -86,10 +95,22 @@ __global__ __launch_bounds__(kScanBlock) void scan_down_kernel(const uint32_t *_
     __shared__ uint64_t ws[kScanBlock / 64];
     const int64_t base = (int64_t)blockIdx.x * kScanTile;
     const int t = threadIdx.x;
+    const bool full = base + kScanTile <= n && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0;
+    if (full) {  // 16-byte loads, striped
+        const uint4 *v = reinterpret_cast<const uint4 *>(in + base);
 #pragma unroll
-    for (int j = 0; j < kScanItems; j++) {  // coalesced, striped
-        const int e = j * kScanBlock + t;
-        sv[pad16(e)] = base + e < n ? in[base + e] : 0u;
+        for (int j = 0; j < kScanItems / 4; j++) {
+            const int q = j * kScanBlock + t;
+            const uint4 w = v[q];
+            const int e = 4 * q;  // 4 consecutive counts: one pad word per 16 keeps them together
+            sv[pad16(e)] = w.x, sv[pad16(e) + 1] = w.y, sv[pad16(e) + 2] = w.z, sv[pad16(e) + 3] = w.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kScanItems; j++) {  // coalesced, striped
+            const int e = j * kScanBlock + t;
+            sv[pad16(e)] = base + e < n ? in[base + e] : 0u;
+        }
     }
     __syncthreads();
     uint32_t v[kScanItems];
@@ -107,10 +128,19 @@ __global__ __launch_bounds__(kScanBlock) void scan_down_kernel(const uint32_t *_
         run += v[j];
     }
     __syncthreads();
+    if (full) {  // 16-byte stores, striped
+        longlong2 *o = reinterpret_cast<longlong2 *>(out + base);
 #pragma unroll
-    for (int j = 0; j < kScanItems; j++) {
-        const int e = j * kScanBlock + t;
-        if (base + e < n) out[base + e] = so[pad16(e)];
+        for (int j = 0; j < kScanItems / 2; j++) {
+            const int q = j * kScanBlock + t, e = 2 * q;
+            o[q] = make_longlong2(so[pad16(e)], so[pad16(e) + 1]);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kScanItems; j++) {
+            const int e = j * kScanBlock + t;
+            if (base + e < n) out[base + e] = so[pad16(e)];
+        }
     }
 }
 
