@@ -60,9 +60,11 @@ def pmc_traffic(scope):
 
 
 def roofline_from_prof(prof, prefer=None):
-    """Dominant kernel = the largest summed device time (every hot kernel has a byte model).
-    The sub-scope `mm_backtrack.long` is part of `mm_backtrack` and never a candidate."""
-    cand = {k: v for k, v in prof.items() if "." not in k}
+    """Dominant kernel = the largest summed device time among the scopes that time one main
+    kernel (SCOPE_KERNEL; mm_chain also holds the small-group lane kernel, ~2 % of it).
+    Multi-kernel sections with host syncs inside (mm_anchor_gsort, mm_z_order) are not
+    candidates, nor is the sub-scope `mm_backtrack.long` (part of `mm_backtrack`)."""
+    cand = {k: v for k, v in prof.items() if k in SCOPE_KERNEL} or {k: v for k, v in prof.items() if "." not in k}
     if not cand:
         return None
     name = prefer if prefer in cand else max(cand, key=lambda k: cand[k][0])
