@@ -83,7 +83,10 @@ constexpr int kRingMask = kRing - 1;
 constexpr int kStair = 4;       // staircase entries kept per block summary
 constexpr int kSumInts = kStair + 1;  // int4 words per block summary: staircase + (ymin, ymax, n|trunc, -)
 constexpr int kSumRing = HYMET_CHAIN_SUMRING;  // LDS ring of the last complete block summaries (1.25 KB)
-constexpr int kInnerCap = 256;  // LDS inner-window list (ring-deque) + stamps: 3 KB
+#ifndef HYMET_CHAIN_INNER
+#define HYMET_CHAIN_INNER 256
+#endif
+constexpr int kInnerCap = HYMET_CHAIN_INNER;  // LDS inner-window list (ring-deque) + stamps: 3 KB at 256
 constexpr int kBdq = HYMET_CHAIN_BDQ;  // block-argmin deque, 2 int4 per element (1 KB)
 constexpr int kIdq = HYMET_CHAIN_IDQ;  // inner max-deque (idx, f + span) (0.5 KB)
 constexpr size_t kChainLds = kRing * sizeof(int4) + kSumRing * kSumInts * sizeof(int4) + 64 * 2 * sizeof(int4) +
