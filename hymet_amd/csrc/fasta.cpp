@@ -30,9 +30,23 @@ void find_starts(const char *buf, int64_t b, int64_t e, std::vector<int64_t> &ou
     }
 }
 
+// exact count of zero bytes in a 64-bit word (no borrow false positives)
+inline int zero_bytes(uint64_t v) {
+    const uint64_t m = 0x7F7F7F7F7F7F7F7Full;
+    return __builtin_popcountll(~(((v & m) + m) | v | m));
+}
+
+// '\n' and '\r' bytes in s[0, n): 8 bytes per step (SWAR), ~8x the byte loop
 int64_t count_breaks(const char *s, int64_t n) {
-    int64_t c = 0;
-    for (int64_t i = 0; i < n; i++) c += (s[i] == '\n') | (s[i] == '\r');
+    int64_t c = 0, i = 0;
+    for (; i < n && ((uintptr_t)(s + i) & 7); i++) c += (s[i] == '\n') | (s[i] == '\r');
+    const uint64_t nl = 0x0A0A0A0A0A0A0A0Aull, cr = 0x0D0D0D0D0D0D0D0Dull;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, s + i, 8);
+        c += zero_bytes(w ^ nl) + zero_bytes(w ^ cr);
+    }
+    for (; i < n; i++) c += (s[i] == '\n') | (s[i] == '\r');
     return c;
 }
 
