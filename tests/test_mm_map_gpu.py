@@ -98,3 +98,40 @@ def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy, z_runs):
         assert g_lines == o_lines
         n_mapped += len(gregs) > 0
     assert n_mapped >= 55
+
+
+def test_map_many_targets_matches_oracle(gpu):
+    """An index part of 2,300 short targets: large queries then meet more (strand, target)
+    bins than the grouped anchor sort holds in LDS (2^(1+12) > 4096), so batches with such
+    queries take the device-wide sort; small queries and the rest are unaffected."""
+    from hymet_amd import mapper
+    from hymet_amd.seqio import DevicePool, from_records
+    from oracle import oracle_lib as ol
+    rng = np.random.default_rng(33)
+    refs = [rand_seq(rng, int(rng.integers(1_500, 3_000))) for _ in range(2_300)]
+    names = [f"NZ_T{i:05d}.1" for i in range(len(refs))]
+    ss = from_records([(n, "", s) for n, s in zip(names, refs)])
+    part = mapper.IndexPart(gpu, ss)
+    opt = mapper.MapOpt.asm10()
+    opt.resolve_mid_occ(part)
+    oi = ol.MmIndex(refs, names=names)
+    oopt = ol.asm10_opt()
+    ol._mm_lib().mmo_opt_update_mid_occ(ctypes.byref(oopt), oi.h)
+    qs = []
+    for i in range(24):  # queries spanning 20-40 consecutive targets: > 4096 anchors each
+        t = int(rng.integers(0, len(refs) - 40))
+        s = b"".join(refs[t:t + int(rng.integers(20, 40))])
+        qs.append((f"span{i}", mutate(rng, s, 0.01) if i % 2 else revcomp(s)))
+    for i in range(24):
+        t = int(rng.integers(0, len(refs)))
+        qs.append((f"one{i}", mutate(rng, refs[t], 0.02)))
+    qss = from_records([(n, "", s) for n, s in qs])
+    qpool = DevicePool(gpu, qss, DevicePool.ALPHA_MINIMAP2)
+    res = mapper.map_part(gpu, part, qpool, opt)
+    for qi, (name, s) in enumerate(qs):
+        oregs, orl = ol.mm_map(oi, oopt, s, name)
+        gregs = res.query(qi)
+        assert res.rep_len[qi] == orl, name
+        g_lines = mapper.paf_lines(name, len(s), gregs, int(res.rep_len[qi]), names, ss.lengths)
+        o_lines = ol.format_paf(name, len(s), oregs, orl, names, ss.lengths)
+        assert g_lines == o_lines, name
