@@ -1,6 +1,10 @@
 // Context lifetime and thread-local error strings for the C ABI (include/hymet_gpu.h).
 #include "common.hpp"
 
+#include <algorithm>
+#include <thread>
+#include <vector>
+
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -215,6 +219,26 @@ int hymet_scratch_trim(hymet_ctx *ctx, int64_t *freed_bytes) {
 int hymet_scratch_cached(hymet_ctx *ctx, int64_t *bytes) {
     HY_ARG(ctx && bytes, "hymet_scratch_cached: null argument");
     *bytes = hymet::scratch_cached();
+    return HYMET_OK;
+}
+
+int hymet_copy_to_host(hymet_ctx *ctx, void *dst, const void *src, int64_t n, int threads) {
+    HY_ARG(ctx && (n == 0 || (dst && src)) && n >= 0, "hymet_copy_to_host: bad argument");
+    if (n == 0) return HYMET_OK;
+    // first touch of a fresh host allocation on several threads (a GB of page faults on the
+    // copy's one thread costs more than the copy), then one D2H copy on the context stream
+    threads = std::max(1, std::min(threads, 64));
+    const int64_t page = 4096;
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++)
+        th.emplace_back([=] {
+            volatile char *d = (volatile char *)dst;
+            for (int64_t o = (n * t / threads) & ~(page - 1); o < n * (t + 1) / threads; o += page) d[o] = 0;
+        });
+    for (auto &x : th) x.join();
+    HY_HIP(hipSetDevice(ctx->device));
+    HY_HIP(hipMemcpyAsync(dst, src, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    HY_HIP(hipStreamSynchronize(ctx->stream));
     return HYMET_OK;
 }
 

@@ -203,16 +203,21 @@ def _dev_buf(gpu, bufs, key, nbytes):
     return b
 
 
+_bytes_new = _c.pythonapi.PyBytes_FromStringAndSize
+_bytes_new.restype = _c.py_object
+_bytes_new.argtypes = [_c.c_void_p, _c.c_ssize_t]
+
+
 def _to_host(gpu, bufs, key, dev, n) -> bytes:
-    """D2H of n bytes through a reusable pinned host buffer."""
+    """D2H of n bytes straight into a new bytes object (its pages first touched on 16 host
+    threads, then one copy): no pinned bounce buffer and no second host copy, which cost
+    ~0.35 s per GB of PAF text."""
     if n == 0:
         return b""
-    h = bufs.get(key)
-    if h is None or h.numel() < n:
-        h = gpu.torch.empty(int(n * 1.25) + 4096, dtype=gpu.torch.uint8, pin_memory=True)
-        bufs[key] = h
-    h[:n].copy_(dev[:n])
-    return h[:n].numpy().tobytes()
+    b = _bytes_new(None, int(n))  # uninitialised, filled below before anyone sees it
+    addr = _c.cast(_c.c_char_p(b), _c.c_void_p).value
+    check(gpu.lib.hymet_copy_to_host(gpu.ctx, addr, ptr(dev), int(n), 16), "hymet_copy_to_host")
+    return b
 
 
 def emit_paf_bytes(gpu, ix: IndexSet, sh: QueryShard, acc: PafAcc, bufs) -> bytes:
