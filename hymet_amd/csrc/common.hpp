@@ -17,6 +17,9 @@ struct hymet_ctx {
     bool prof = false;
     std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> ev;
     std::map<std::string, double> bytes;  // algorithmic bytes of the timed launches
+    // pinned staging for hymet_copy_to_host (two chunks, allocated on first use)
+    void *stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
 };
 
 namespace hymet {

@@ -209,9 +209,9 @@ _bytes_new.argtypes = [_c.c_void_p, _c.c_ssize_t]
 
 
 def _to_host(gpu, bufs, key, dev, n) -> bytes:
-    """D2H of n bytes straight into a new bytes object (its pages first touched on 16 host
-    threads, then one copy): no pinned bounce buffer and no second host copy, which cost
-    ~0.35 s per GB of PAF text."""
+    """D2H of n bytes into a new bytes object through the library's double-buffered pinned
+    staging (16 host copy threads): no torch pinned buffer and no extra bytes copy, which
+    cost ~0.35 s per GB of PAF text."""
     if n == 0:
         return b""
     b = _bytes_new(None, int(n))  # uninitialised, filled below before anyone sees it

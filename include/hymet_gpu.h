@@ -60,8 +60,9 @@ int hymet_prof_names(hymet_ctx *ctx, char *buf, int64_t cap);
  * allocates large tensors); cached reports the bytes held. */
 int hymet_scratch_trim(hymet_ctx *ctx, int64_t *freed_bytes);
 int hymet_scratch_cached(hymet_ctx *ctx, int64_t *bytes);
-/* n bytes of device memory (written by this context's stream) into pageable host memory;
- * the destination's pages are first touched on `threads` host threads.  Synchronous.
+/* n bytes of device memory (written by this context's stream) into pageable host memory,
+ * through two pinned 64 MiB staging chunks (PCIe and `threads` host copy threads overlap).
+ * Synchronous.
  * (The PAF / TSV text copy-out: resultados.paf is written by minimap2.sh:23, the TSV by
  * classification_cami.py:333-339.) */
 int hymet_copy_to_host(hymet_ctx *ctx, void *dst, const void *src, int64_t n, int threads);
