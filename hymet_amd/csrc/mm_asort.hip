@@ -13,7 +13,7 @@
 //     position and lists the non-empty bins -- the (query, strand, target) groups; the tiles
 //     scatter their anchors to their runs; every group of <= 4096 anchors is then sorted by
 //     (rpos, y) in one block, and the larger groups (a query against its own genome) by one
-//     device radix sort over all of them together (key = group rank | rpos).
+//     device radix sort over all of them together (key = group rank | key bits below the bin).
 // A block sort packs (the key's bits below q or below rid, y) into one 64-bit word, sorts it
 // in registers (bitonic, ITEMS per thread) and merges the runs in LDS: merge path splits,
 // then each thread's outputs by a bitonic half-cleaner over two windows of ITEMS words
@@ -21,9 +21,10 @@
 // bitonic sort on (key, y), those of <= 8 a register network in one thread; class lists
 // are filled with one global atomic per class and block.  Equal keys after the device radix
 // sort (one target position hit by several query minimizers) are put in y order on write.
-// The caller falls back to the device sort of the whole batch (return 1) when a large query
-// meets more than 4096 bins (index parts of > 2047 targets) or the packed words would not
-// fit 64 bits.
+// Index parts of more than 2047 targets use coarse bins of 2^cs consecutive targets (the
+// bin histogram always fits LDS), sorted inside by (low target bits, rpos, y).  The caller
+// falls back to the device sort of the whole batch (return 1) when the packed words would
+// not fit 64 bits.
 #include "mm_common.hpp"
 
 namespace hymet {
@@ -483,7 +484,11 @@ int sort_segments(hymet_ctx *ctx, const Seg *lists, int64_t cap, const int32_t *
 int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val, int64_t n, const int64_t *d_qoff, int n_q,
                         int rb, int pb, uint64_t yhi, int64_t max_qlen, uint64_t *okey, uint32_t *oval, uint64_t *ax,
                         uint64_t *ay) {
-    const int nbins = 1 << (1 + rb);
+    // bins = (strand, target) -- or, for parts of more than 2047 targets, (strand, target >> cs):
+    // coarse bins of 2^cs consecutive targets, sorted inside by (low target bits, rpos, y)
+    const int cs = std::max(0, 1 + rb - 12);
+    const int nbins = 1 << (1 + rb - cs);
+    const int gb = pb + cs;  // key bits below the bin
     const int ybits = bits_of(max_qlen);
     if (n <= 0 || n_q <= 0 || 1 + rb + pb + ybits > 63) return 1;
     hipStream_t st = ctx->stream;
@@ -500,7 +505,6 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     int32_t hq[kClasses] = {};
     HY_HIP(hipMemcpyAsync(hq, qcnt.p, 4 * kClasses, hipMemcpyDeviceToHost, st));
     HY_HIP(hipStreamSynchronize(st));
-    if (hq[kLarge] > 0 && nbins > kMaxBins) return 1;
     ProfScope _ps(ctx, "mm_anchor_gsort", 60.0 * (double)n);  // key+y read, scatter write, sort read, key+x+y write
     // 2 small queries: sorted whole
     int rc = sort_segments(ctx, qlists.as<Seg>(), n_q, hq, key, val, 1 + rb + pb, ybits, out);
@@ -521,7 +525,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     hipLaunchKernelGGL(tile_map_kernel, dim3((unsigned)cdiv(nl, 256)), dim3(256), 0, st, large, nl, tpos.as<int64_t>(),
                        ta0.as<int64_t>(), tq.as<int32_t>(), tn.as<int32_t>());
     HY_CHECK_LAUNCH("tile_map_kernel");
-    hipLaunchKernelGGL(tile_hist_kernel, dim3((unsigned)NT), dim3(256), 0, st, key, ta0.as<int64_t>(), tn.as<int32_t>(), pb,
+    hipLaunchKernelGGL(tile_hist_kernel, dim3((unsigned)NT), dim3(256), 0, st, key, ta0.as<int64_t>(), tn.as<int32_t>(), gb,
                        nbins, H.as<uint32_t>());
     HY_CHECK_LAUNCH("tile_hist_kernel");
     const int64_t gcap = std::min<int64_t>(n, NT * (int64_t)nbins);  // a group holds >= 1 anchor
@@ -534,7 +538,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
                        H.as<uint32_t>(), groups.as<Seg>(), ng.as<int32_t>());
     HY_CHECK_LAUNCH("query_scan_kernel");
     hipLaunchKernelGGL(tile_scatter_kernel, dim3((unsigned)NT), dim3(256), 0, st, key, val, ta0.as<int64_t>(), tq.as<int32_t>(),
-                       tn.as<int32_t>(), d_qoff, pb, nbins, H.as<uint32_t>(), okey, oval);
+                       tn.as<int32_t>(), d_qoff, gb, nbins, H.as<uint32_t>(), okey, oval);
     HY_CHECK_LAUNCH("tile_scatter_kernel");
     // 4 groups of the large queries, sorted in place by (rpos, y)
     int32_t G = 0;
@@ -551,7 +555,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     int32_t hg[kClasses] = {};
     HY_HIP(hipMemcpyAsync(hg, gcnt.p, 4 * kClasses, hipMemcpyDeviceToHost, st));
     HY_HIP(hipStreamSynchronize(st));
-    rc = sort_segments(ctx, glists.as<Seg>(), (int64_t)G, hg, okey, oval, pb, ybits, out);
+    rc = sort_segments(ctx, glists.as<Seg>(), (int64_t)G, hg, okey, oval, gb, ybits, out);
     if (rc) return rc;
     if (hg[kLarge] > 0) {
         const int nbig = hg[kLarge];
@@ -568,17 +572,18 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
         HY_HIP(tk2.alloc(8 * (size_t)NB, st));
         HY_HIP(tv.alloc(4 * (size_t)NB, st));
         HY_HIP(tv2.alloc(4 * (size_t)NB, st));
-        hipLaunchKernelGGL(big_gather_kernel, dim3((unsigned)nbig), dim3(256), 0, st, big, bdst.as<int64_t>(), pb, okey, oval,
+        hipLaunchKernelGGL(big_gather_kernel, dim3((unsigned)nbig), dim3(256), 0, st, big, bdst.as<int64_t>(), gb, okey, oval,
                            tk.as<uint64_t>(), tv.as<uint32_t>());
         HY_CHECK_LAUNCH("big_gather_kernel");
-        const int end_bit = pb + bits_of(nbig);
+        const int end_bit = gb + bits_of(nbig);
+        HY_ARG(end_bit <= 64, "grouped_anchor_sort: group rank and key bits exceed 64");
         size_t tb = 0;
         HY_HIP(rocprim::radix_sort_pairs(nullptr, tb, tk.as<uint64_t>(), tk2.as<uint64_t>(), tv.as<uint32_t>(), tv2.as<uint32_t>(),
                                          (size_t)NB, 0, end_bit, st));
         HY_HIP(tmp.alloc(tb, st));
         HY_HIP(rocprim::radix_sort_pairs(tmp.p, tb, tk.as<uint64_t>(), tk2.as<uint64_t>(), tv.as<uint32_t>(), tv2.as<uint32_t>(),
                                          (size_t)NB, 0, end_bit, st));
-        hipLaunchKernelGGL(big_put_kernel, dim3((unsigned)nbig), dim3(256), 0, st, big, bdst.as<int64_t>(), pb, okey,
+        hipLaunchKernelGGL(big_put_kernel, dim3((unsigned)nbig), dim3(256), 0, st, big, bdst.as<int64_t>(), gb, okey,
                            tk2.as<uint64_t>(), tv2.as<uint32_t>(), out);
         HY_CHECK_LAUNCH("big_put_kernel");
     }

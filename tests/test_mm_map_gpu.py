@@ -101,9 +101,9 @@ def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy, z_runs):
 
 
 def test_map_many_targets_matches_oracle(gpu):
-    """An index part of 2,300 short targets: large queries then meet more (strand, target)
-    bins than the grouped anchor sort holds in LDS (2^(1+12) > 4096), so batches with such
-    queries take the device-wide sort; small queries and the rest are unaffected."""
+    """An index part of 2,300 short targets: more (strand, target) bins (2^(1+12)) than the
+    grouped anchor sort's LDS histogram holds, so large queries sort by coarse bins of two
+    consecutive targets and then by (low target bit, rpos, y) inside them."""
     from hymet_amd import mapper
     from hymet_amd.seqio import DevicePool, from_records
     from oracle import oracle_lib as ol
