@@ -431,6 +431,14 @@ __global__ void group_qfirst_kernel(const int64_t *qoff, int n_q, const int32_t 
     if (q < n_q && qoff[q] < qoff[q + 1]) out[gid[qoff[q]]] = 1;
 }
 
+__global__ void nonwork_fp_kernel(const int64_t *g_start, int32_t G, int min_cnt, int32_t *f, int64_t *p) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    const int64_t a0 = g_start[g], a1 = g_start[g + 1];
+    if (a1 - a0 >= min_cnt) return;
+    for (int64_t a = a0; a < a1; a++) f[a] = 0, p[a] = -1;
+}
+
 __global__ void group_size_kernel(const int64_t *g_start, int32_t G, int min_cnt, uint32_t *key, uint32_t *gidx,
                                   uint32_t *is_work) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -907,8 +915,9 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(f.alloc(4 * (size_t)n, ctx->stream));
         HY_HIP(p.alloc(8 * (size_t)n, ctx->stream));
         HY_HIP(t.alloc(4 * (size_t)n, ctx->stream));
-        HY_HIP(hipMemsetAsync(f.p, 0, 4 * (size_t)n, ctx->stream));
-        HY_HIP(hipMemsetAsync(p.p, 0xFF, 8 * (size_t)n, ctx->stream));
+        // the chaining kernels write f/p of every anchor of a work group; the rest (groups of
+        // fewer than min_cnt anchors) get f = 0, p = -1 here instead of memsets of all n
+        LAUNCH1(nonwork_fp_kernel, G, g_start.as<int64_t>(), (int32_t)G, opt->min_cnt, f.as<int32_t>(), p.as<int64_t>());
         HY_HIP(hipMemsetAsync(t.p, 0xFF, 4 * (size_t)n, ctx->stream));
         DevBuf qfirst;
         HY_HIP(qfirst.alloc((size_t)G, ctx->stream));
