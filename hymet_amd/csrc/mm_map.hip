@@ -431,6 +431,20 @@ __global__ void group_qfirst_kernel(const int64_t *qoff, int n_q, const int32_t 
     if (q < n_q && qoff[q] < qoff[q + 1]) out[gid[qoff[q]]] = 1;
 }
 
+// largest group: the first of the size-descending list, or, when sizes tie at the 16-bit
+// key's cap, the largest of that tied prefix
+__global__ void max_group_kernel(const int64_t *g_start, const int32_t *order, int32_t G, int64_t *out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    int64_t best = 0;
+    for (int32_t w = 0; w < G; w++) {
+        const int g = order[w];
+        const int64_t sz = g_start[g + 1] - g_start[g];
+        best = max(best, sz);
+        if (sz < 0xffff) break;
+    }
+    *out = best;
+}
+
 __global__ void nonwork_fp_kernel(const int64_t *g_start, int32_t G, int min_cnt, int32_t *f, int64_t *p) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
@@ -444,7 +458,9 @@ __global__ void group_size_kernel(const int64_t *g_start, int32_t G, int min_cnt
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
     const int64_t sz = g_start[g + 1] - g_start[g];
-    key[g] = ~(uint32_t)min(sz, (int64_t)0xffffffff);  // descending size
+    // descending size in 16 bits (two radix passes): groups above 65535 anchors tie at the
+    // front, non-work groups (< min_cnt <= 3 anchors) come after every work group
+    key[g] = 0xffffu - (uint32_t)min(sz, (int64_t)0xffff);
     gidx[g] = (uint32_t)g;
     is_work[g] = sz >= min_cnt ? 1u : 0u;
 }
@@ -885,7 +901,8 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
     LAUNCH1(group_start_kernel, n, flag.as<uint32_t>(), gpos.as<int64_t>(), n, g_start.as<int64_t>(), gid.as<int32_t>());
     HY_HIP(hipMemcpyAsync(g_start.as<int64_t>() + G, &n, 8, hipMemcpyHostToDevice, ctx->stream));
     // work list: groups with >= min_cnt anchors, biggest first
-    DevBuf skey, sidx, swork, skey2, sidx2;
+    DevBuf skey, sidx, swork, skey2, sidx2, gmax;
+    HY_HIP(gmax.alloc(8, ctx->stream));
     HY_HIP(skey.alloc(4 * (size_t)G, ctx->stream));
     HY_HIP(sidx.alloc(4 * (size_t)G, ctx->stream));
     HY_HIP(swork.alloc(4 * (size_t)G, ctx->stream));
@@ -900,16 +917,17 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         rc = scan_flags(ctx, swork.as<uint32_t>(), G, wpos, &n_work);
         if (rc) return rc;
         uint32_t *kp = skey.as<uint32_t>(), *ka = skey2.as<uint32_t>(), *vp = sidx.as<uint32_t>(), *va = sidx2.as<uint32_t>();
-        rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 32, "radix_sort_groups");
+        rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 16, "radix_sort_groups");
         if (rc) return rc;
         {  // the chaining kernel packs local predecessor indices in 24 bits
-            uint32_t k0 = 0;
-            HY_HIP(hipMemcpyAsync(&k0, kp, 4, hipMemcpyDeviceToHost, ctx->stream));
+            int64_t big = 0;
+            LAUNCH1(max_group_kernel, 1, g_start.as<int64_t>(), (const int32_t *)vp, (int32_t)G, gmax.as<int64_t>());
+            HY_HIP(hipMemcpyAsync(&big, gmax.p, 8, hipMemcpyDeviceToHost, ctx->stream));
             HY_HIP(hipStreamSynchronize(ctx->stream));
-            HY_ARG(~k0 < (1u << 24) - 1, "hymet_mm_map: an anchor group exceeds 2^24 anchors");
+            HY_ARG(big < (1ll << 24) - 1, "hymet_mm_map: an anchor group exceeds 2^24 anchors");
             static const bool stats = getenv("HYMET_CHAIN_STATS") != nullptr;  // profiling: tail size per launch
-            if (stats) fprintf(stderr, "[chain] bw %d anchors %lld groups %lld work %lld largest %u\n", bw, (long long)n,
-                               (long long)G, (long long)n_work, ~k0);
+            if (stats) fprintf(stderr, "[chain] bw %d anchors %lld groups %lld work %lld largest %lld\n", bw, (long long)n,
+                               (long long)G, (long long)n_work, (long long)big);
         }
         DevBuf f, p, t;
         HY_HIP(f.alloc(4 * (size_t)n, ctx->stream));
@@ -1755,13 +1773,16 @@ int hymet_mm_chain_dp(hymet_ctx *ctx, const uint64_t *h_x, const uint64_t *h_y, 
     LAUNCH1(group_size_kernel, G, g_start.as<int64_t>(), (int32_t)G, 1, skey.as<uint32_t>(), sidx.as<uint32_t>(),
             swork.as<uint32_t>());
     uint32_t *kp = skey.as<uint32_t>(), *ka = skey2.as<uint32_t>(), *vp = sidx.as<uint32_t>(), *va = sidx2.as<uint32_t>();
-    rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 32, "radix_sort_groups");
+    rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 16, "radix_sort_groups");
     if (rc) return rc;
     {  // the chaining kernel packs local predecessor indices in 24 bits
-        uint32_t k0 = 0;
-        HY_HIP(hipMemcpyAsync(&k0, kp, 4, hipMemcpyDeviceToHost, st));
+        DevBuf gmax;
+        HY_HIP(gmax.alloc(8, st));
+        LAUNCH1(max_group_kernel, 1, g_start.as<int64_t>(), (const int32_t *)vp, (int32_t)G, gmax.as<int64_t>());
+        int64_t big = 0;
+        HY_HIP(hipMemcpyAsync(&big, gmax.p, 8, hipMemcpyDeviceToHost, st));
         HY_HIP(hipStreamSynchronize(st));
-        HY_ARG(~k0 < (1u << 24) - 1, "hymet_mm_chain_dp: an anchor group exceeds 2^24 anchors");
+        HY_ARG(big < (1ll << 24) - 1, "hymet_mm_chain_dp: an anchor group exceeds 2^24 anchors");
     }
     HY_HIP(f.alloc(4 * (size_t)n, st));
     HY_HIP(p.alloc(8 * (size_t)n, st));
