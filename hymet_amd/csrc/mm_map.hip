@@ -676,7 +676,7 @@ __global__ void chain_cnt_kernel(const uint64_t *cu, int64_t n, uint32_t *cnt) {
 __global__ __launch_bounds__(256) void chain_copy_kernel(const uint64_t *cu, const int64_t *cfirst, const int64_t *bpos,
                                                          const int64_t *chain_ids, const uint64_t *ax, const uint64_t *ay,
                                                          int64_t n_chain, int64_t nb, uint64_t *bx, uint64_t *by,
-                                                         int32_t *bchain) {
+                                                         int32_t *bchain, int32_t *bsrc) {
     // flat over the output anchors: the block's first chain by binary search over bpos, each
     // lane's by a short forward walk (chains are tens to thousands of anchors long)
     __shared__ int64_t s_c0;
@@ -700,6 +700,75 @@ __global__ __launch_bounds__(256) void chain_copy_kernel(const uint64_t *cu, con
     bx[b] = ax[a];
     by[b] = ay[a];
     bchain[b] = (int32_t)c;
+    bsrc[b] = (int32_t)a;  // index in the chained anchor set (the long join compacts by it)
+}
+
+// long join: anchors of flagged queries' chains marked in the first-pass anchor set
+__global__ void rechain_mark_kernel(const int32_t *bchain, const uint32_t *cq, const int32_t *bsrc, const uint32_t *flag,
+                                    int64_t nb, uint8_t *mark) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb && flag[cq[bchain[b]]]) mark[bsrc[b]] = 1;
+}
+
+// marked anchors per 4096-anchor tile (16 per thread, one 16-byte load)
+__global__ __launch_bounds__(256) void mark_count_kernel(const uint8_t *mark, int64_t n, uint32_t *cnt) {
+    __shared__ uint32_t ws[4];
+    const int64_t e0 = (int64_t)blockIdx.x * 4096 + threadIdx.x * 16;
+    uint32_t c = 0;
+    if (e0 + 16 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(mark + e0);
+        c = __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);  // marks are 0 / 1 bytes
+    } else {
+        for (int64_t e = e0; e < n && e < e0 + 16; e++) c += mark[e];
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor((int)c, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// stable compaction of the marked anchors (x, y, group key): the first-pass set is sorted by
+// (key, y), so its marked subsequence is the long join's sorted anchor set -- no re-sort.
+// Rows of 256 anchors, lanes striped (coalesced), positions by ballot counts.
+__global__ __launch_bounds__(256) void mark_compact_kernel(const uint8_t *mark, int64_t n, const int64_t *tile_off,
+                                                           const uint64_t *ax, const uint64_t *ay, const uint64_t *k1,
+                                                           uint64_t *ox, uint64_t *oy, uint64_t *ok1) {
+    __shared__ uint32_t rc[64];  // marks per (row, wave), row-major
+    const int64_t t0 = (int64_t)blockIdx.x * 4096;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    bool m[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int64_t e = t0 + j * 256 + threadIdx.x;
+        m[j] = e < n && mark[e];
+        const uint64_t b = __ballot(m[j]);
+        if (lane == 0) rc[j * 4 + w] = (uint32_t)__popcll(b);
+    }
+    __syncthreads();
+    uint32_t v = 0, inc = 0;
+    if (w == 0) {  // wave 0: exclusive scan of the 64 counts in element order
+        v = rc[lane];
+        inc = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= d) inc += o;
+        }
+    }
+    __syncthreads();
+    if (w == 0) rc[lane] = inc - v;
+    __syncthreads();
+    const int64_t base = tile_off[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint64_t b = __ballot(m[j]);
+        if (m[j]) {
+            const int64_t e = t0 + j * 256 + threadIdx.x;
+            const int64_t o = base + rc[j * 4 + w] + __popcll(b & ((1ull << lane) - 1));
+            ox[o] = ax[e];
+            oy[o] = ay[e];
+            ok1[o] = k1[e];
+        }
+    }
 }
 
 // query of each chain (from the sorted first-anchor key, via the anchor query offsets)
@@ -805,6 +874,7 @@ struct AnchorSet {
 struct ChainSet {
     DevBuf bx, by, cu, cboff;  // cboff: offset of each chain's anchors in bx/by
     DevBuf bchain, cq;         // chain of each compacted anchor; query of each chain
+    DevBuf bsrc;               // index of each compacted anchor in the chained anchor set
     int64_t n_anchor = 0, n_chain = 0;
     std::vector<int64_t> h_qc;   // n_q + 1 chain offsets per query
     std::vector<int64_t> h_qb;   // n_q + 1 anchor offsets per query
@@ -1091,10 +1161,11 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(C.bx.alloc(8 * (size_t)(NB + 1), ctx->stream));
         HY_HIP(C.by.alloc(8 * (size_t)(NB + 1), ctx->stream));
         HY_HIP(C.bchain.alloc(4 * (size_t)(NB + 1), ctx->stream));
+        HY_HIP(C.bsrc.alloc(4 * (size_t)(NB + 1), ctx->stream));
         if (NC > 0 && NB > 0)
             LAUNCH1(chain_copy_kernel, NB, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), C.cboff.as<int64_t>(),
                     chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, NB, C.bx.as<uint64_t>(),
-                    C.by.as<uint64_t>(), C.bchain.as<int32_t>());
+                    C.by.as<uint64_t>(), C.bchain.as<int32_t>(), C.bsrc.as<int32_t>());
         // per-query chain offsets
         DevBuf &cq = C.cq;
         HY_HIP(cq.alloc(4 * (size_t)(NC + 1), ctx->stream));
@@ -1552,7 +1623,37 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
             const int64_t A2 = S2.h_off[n_q];
             HY_HIP(S2.d_off.alloc(8 * (size_t)(n_q + 1), st));
             HY_HIP(hipMemcpyAsync(S2.d_off.p, S2.h_off.data(), 8 * (size_t)(n_q + 1), hipMemcpyHostToDevice, st));
-            if (key_path) {
+            const bool resort = getenv("HYMET_RECHAIN_SORT") != nullptr;  // tests: the re-sort path
+            if (key_path && !resort) {
+                // the flagged queries' chain anchors, compacted out of the first-pass set in its
+                // (key, y) order -- already the long join's sorted anchor set
+                const int64_t n1 = S1.n, nt = cdiv(n1, 4096);
+                DevBuf mark, tcnt, toff;
+                HY_HIP(mark.alloc((size_t)n1 + 16, st));
+                HY_HIP(hipMemsetAsync(mark.p, 0, (size_t)n1 + 16, st));
+                LAUNCH1(rechain_mark_kernel, C1.n_anchor, C1.bchain.as<int32_t>(), C1.cq.as<uint32_t>(), C1.bsrc.as<int32_t>(),
+                        flag.as<uint32_t>(), C1.n_anchor, mark.as<uint8_t>());
+                HY_HIP(tcnt.alloc(4 * (size_t)(nt + 1), st));
+                HY_HIP(toff.alloc(8 * (size_t)(nt + 1), st));
+                hipLaunchKernelGGL(mark_count_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<uint8_t>(), n1,
+                                   tcnt.as<uint32_t>());
+                HY_CHECK_LAUNCH("mark_count_kernel");
+                int64_t got = 0;
+                rc = exclusive_scan_u32_i64(ctx, tcnt.as<uint32_t>(), toff.as<int64_t>(), nt, &got);
+                if (rc) return rc;
+                if (got != A2) return hymet::fail(HYMET_E_INTERNAL, "hymet_mm_map: long-join anchor count mismatch");
+                HY_HIP(S2.ax.alloc(8 * (size_t)(A2 + 1), st));
+                HY_HIP(S2.ay.alloc(8 * (size_t)(A2 + 1), st));
+                HY_HIP(S2.k1.alloc(8 * (size_t)(A2 + 1), st));
+                hipLaunchKernelGGL(mark_compact_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<uint8_t>(), n1,
+                                   toff.as<int64_t>(), S1.ax.as<uint64_t>(), S1.ay.as<uint64_t>(), S1.k1.as<uint64_t>(),
+                                   S2.ax.as<uint64_t>(), S2.ay.as<uint64_t>(), S2.k1.as<uint64_t>());
+                HY_CHECK_LAUNCH("mark_compact_kernel");
+                S2.gshift = S1.gshift;
+                S2.n = A2;
+                rc = dump_anchors(getenv("HYMET_DUMP_ANCHORS2"), S2, dumped2);
+                if (rc) return rc;
+            } else if (key_path) {
                 DevBuf key, val;
                 HY_HIP(key.alloc(8 * (size_t)(A2 + 1), st));
                 HY_HIP(val.alloc(4 * (size_t)(A2 + 1), st));

@@ -53,13 +53,17 @@ def _queries(rng, refs):
     return qs
 
 
-@pytest.mark.parametrize("bt_long,legacy,z_runs", [(None, None, None), ("4", None, None), (None, "1", "1"),
-                                                  (None, None, "2")])
-def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy, z_runs):
+@pytest.mark.parametrize("bt_long,legacy,z_runs,resort", [(None, None, None, None), ("4", None, None, None),
+                                                         (None, "1", "1", None), (None, None, "2", None),
+                                                         (None, None, None, "1")])
+def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy, z_runs, resort):
     """bt_long = "4": nearly every chain group takes the wave-per-group backtrack path.
     legacy = "1": anchors take the two-key sort path (used when the one-key anchor sort key
     would exceed 64 bits).  z_runs: backtrack-order groups of more ascending runs than this
-    take the sort fallbacks (block bitonic / global radix) instead of the run merge."""
+    take the sort fallbacks (block bitonic / global radix) instead of the run merge.
+    resort = "1": the long join re-sorts its anchors instead of compacting the first pass's."""
+    if resort is not None:
+        monkeypatch.setenv("HYMET_RECHAIN_SORT", resort)
     if bt_long is not None:
         monkeypatch.setenv("HYMET_BT_LONG", bt_long)
     if legacy is not None:
