@@ -1197,7 +1197,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
                    int64_t NB, int64_t NC, int64_t NM, const int32_t *bchain, const uint32_t *cq,
-                   const int32_t *pos_tab, const int64_t *qbase);
+                   const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q);
 
 namespace {
 // dense query position -> index among the query's seeded minimizers (mini_pos order), for
@@ -1604,8 +1604,8 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     ChainSet *CF = &C1;
     ChainSet C2;
     std::vector<uint32_t> h_flag(n_q, 0);
+    DevBuf flag;  // queries re-chained by the long join (their first-pass regions are not built)
     if (opt->bw_long > opt->bw && C1.n_chain > 0) {
-        DevBuf flag;
         HY_HIP(flag.alloc(4 * (size_t)n_q, st));
         hipLaunchKernelGGL(rechain_flag_kernel, dim3((unsigned)cdiv(n_q, 256)), dim3(256), 0, st, C1.by.as<uint64_t>(),
                            C1.cu.as<uint64_t>(), C1.d_qc.as<int64_t>(), C1.d_qb.as<int64_t>(), d_qlen.as<int64_t>(), n_q,
@@ -1686,7 +1686,7 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     tr.mark("long join");
     // -------------------------------------------------------------- 8 regions
     // region records stay in HBM: per chain set, records at the set's chain offsets + counts
-    auto run_regions = [&](ChainSet &C, DevBuf &rg, DevBuf &nr) -> int {
+    auto run_regions = [&](ChainSet &C, DevBuf &rg, DevBuf &nr, const uint32_t *skip_q) -> int {
         const int64_t NC = C.n_chain;
         DevBuf z, wv, cov, tmp;
         HY_HIP(z.alloc(16 * (size_t)(NC + 1), st));
@@ -1700,13 +1700,13 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                               d_qlen.as<int64_t>(), d_hash.as<uint32_t>(), rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
                               z.p, rg.as<hymet_mm_reg>(), wv.as<int32_t>(), cov.as<uint64_t>(), tmp.as<int32_t>(),
                               nr.as<int32_t>(), C.n_anchor, NC, NM, C.bchain.as<int32_t>(), C.cq.as<uint32_t>(),
-                              pos_tab.as<int32_t>(), d_qbase.as<int64_t>());
+                              pos_tab.as<int32_t>(), d_qbase.as<int64_t>(), skip_q);
     };
     DevBuf rg1, nr1, rg2, nr2, d_flag;
-    rc = run_regions(C1, rg1, nr1);
+    rc = run_regions(C1, rg1, nr1, CF ? nullptr : flag.as<uint32_t>());
     if (rc) return rc;
     if (!CF) {
-        rc = run_regions(C2, rg2, nr2);
+        rc = run_regions(C2, rg2, nr2, nullptr);
         if (rc) return rc;
         HY_HIP(d_flag.alloc(4 * (size_t)n_q, st));
         HY_HIP(hipMemcpyAsync(d_flag.p, h_flag.data(), 4 * (size_t)n_q, hipMemcpyHostToDevice, st));

@@ -91,6 +91,7 @@ struct RegParams {
     // per-chain anchor statistics (chain_stats_kernel)
     const int32_t *c_mlen, *c_blen, *c_st, *c_last, *c_fv;
     const uint64_t *q_sumk;
+    const uint32_t *skip_q;        // queries whose regions come from the long join (nullable)
 };
 
 __device__ void set_coor(hymet_mm_reg *r, int32_t qlen, const uint64_t *ax, const uint64_t *ay, int32_t mlen,
@@ -133,6 +134,7 @@ struct AnchorStatParams {
     int32_t *a_idx, *c_mlen, *c_blen, *c_st, *c_last;
     const int32_t *pos_tab;  // query base -> minimizer index (or -1), at qbase[q] + position
     const int64_t *qbase;
+    const uint32_t *skip_q;  // queries whose chains are superseded by the long join (nullable)
 };
 
 // per chained anchor: its index among the query minimizers (mm_est_err's get_mini_idx).  The
@@ -143,6 +145,7 @@ __global__ void anchor_mini_idx_kernel(AnchorStatParams P) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= P.NB) return;
     const int64_t q = P.cq[P.bchain[b]];
+    if (P.skip_q && P.skip_q[q]) return;
     const int qlen = (int)P.qlen[q];
     const uint64_t ax = P.bx[b], ay = P.by[b];
     int32_t x = (int32_t)ay;
@@ -167,6 +170,7 @@ __device__ __forceinline__ int wmin(int v) {
 __global__ __launch_bounds__(64) void chain_stats_kernel(AnchorStatParams P, const int32_t *a_idx, int32_t *c_fv) {
     const int lane = threadIdx.x;
     for (int64_t c = blockIdx.x; c < P.NC; c += gridDim.x) {
+        if (P.skip_q && P.skip_q[P.cq[c]]) continue;  // wave-uniform
         const int32_t cnt = (int32_t)P.cu[c];
         const int64_t o = P.cboff[c];
         const bool rev = P.bx[o] >> 63;
@@ -221,7 +225,7 @@ __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
     const int64_t c0 = P.qc[q], c1 = P.qc[q + 1];
     int n = (int)(c1 - c0);
     const int32_t qlen = (int32_t)P.qlen[q];
-    if (n == 0 || qlen == 0) {
+    if (n == 0 || qlen == 0 || (P.skip_q && P.skip_q[q])) {
         P.n_regs[q] = 0;
         return;
     }
@@ -415,7 +419,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
                    int64_t NB, int64_t NC, int64_t NM, const int32_t *bchain, const uint32_t *cq,
-                   const int32_t *pos_tab, const int64_t *qbase) {
+                   const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q) {
     if (n_q <= 0) return HYMET_OK;
     hipStream_t st = ctx->stream;
     DevBuf a_idx, cst, sumk;
@@ -427,7 +431,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
     {
         ProfScope _ps(ctx, "mm_chain_stats", (double)NB * (16.0 + 16.0 + 8.0) + (double)NM * 8.0);
         AnchorStatParams A{bx, by, cu, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, bchain, cq, a_idx.as<int32_t>(),
-                           c_mlen, c_blen, c_st, c_last, pos_tab, qbase};
+                           c_mlen, c_blen, c_st, c_last, pos_tab, qbase, skip_q};
         if (NB > 0) {
             hipLaunchKernelGGL(anchor_mini_idx_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A);
             HY_CHECK_LAUNCH("anchor_mini_idx_kernel");
@@ -442,7 +446,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
     }
     RegParams P{bx, by, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
-                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk.as<uint64_t>()};
+                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk.as<uint64_t>(), skip_q};
     ProfScope _ps(ctx, "mm_regions", (double)NC * (8.0 + 8.0 + 4.0 * 5) + (double)n_q * 64.0);  // chain + stats reads, reg writes
     hipLaunchKernelGGL(regions_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P);
     HY_CHECK_LAUNCH("regions_kernel");
