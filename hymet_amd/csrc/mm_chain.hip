@@ -75,6 +75,16 @@ namespace {
 #ifndef HYMET_CHAIN_B0FAST
 #define HYMET_CHAIN_B0FAST 1
 #endif
+// Block summaries of colinear blocks (y increasing) by one DPP prefix min and popcounts
+// instead of a shuffle scan and a readlane loop over the records (~64 per colinear block).
+#ifndef HYMET_CHAIN_CBFAST
+#define HYMET_CHAIN_CBFAST 1
+#endif
+// Colinear batch commits: the inner max-deque's records and the tail block's argmin from the
+// batch's monotone values in O(1) when f + span rises and the priority falls along the batch.
+#ifndef HYMET_CHAIN_MONO
+#define HYMET_CHAIN_MONO 1
+#endif
 #ifndef HYMET_CHAIN_WPE  // waves per SIMD the register allocation targets (0: compiler's choice)
 #define HYMET_CHAIN_WPE 4
 #endif
@@ -492,10 +502,21 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             const Ent e = fetch(jl);
             const double pl = prio(e.f, e.x, e.y, c);
             bool rec = true;
+            uint64_t recm;
+            int rank = 0;  // records with larger y (records have distinct y)
+            int32_t ymn = e.y, ymx = e.y;
             // y strictly increasing along the block (a colinear stretch): the entries with
             // y <= y_l are lanes [0, l], so l is a record iff it is the prefix best there
+            // (ties -> the larger index, i.e. l itself: pl equals the inclusive prefix min),
+            // its rank is the number of records in higher lanes, and the y range is lanes 0, 63
             const int32_t ynx = __shfl_down(e.y, 1, 64);
             if (__ballot(lane == 63 || e.y < ynx) == ~0ull) {
+#if HYMET_CHAIN_CBFAST
+                rec = scan_min_d(pl) == pl;
+                recm = __ballot(rec);
+                rank = __popcll(lane == 63 ? 0ull : recm >> (lane + 1));
+                ymn = rl(e.y, 0), ymx = rl(e.y, 63);
+#else
                 double bp = pl;
                 int32_t bj = jl;
 #pragma unroll
@@ -505,22 +526,28 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     if (lane >= d && better(op, oj, bp, bj)) bp = op, bj = oj;
                 }
                 rec = bj == jl;
+                recm = __ballot(rec);
+                for (uint64_t m = recm; m;) {
+                    const int k = __ffsll((unsigned long long)m) - 1;
+                    m &= m - 1;
+                    rank += rl(e.y, k) > e.y;
+                }
+                wave_minmax(ymn, ymx);
+#endif
             } else {
                 for (int k = 0; k < 64; ++k) {
                     const int32_t yk = rl(e.y, k);
                     const double pk = rld(pl, k);
                     if (k != lane && yk <= e.y && better(pk, (b << 6) + k, pl, jl)) rec = false;
                 }
+                recm = __ballot(rec);
+                for (uint64_t m = recm; m;) {
+                    const int k = __ffsll((unsigned long long)m) - 1;
+                    m &= m - 1;
+                    rank += rl(e.y, k) > e.y;
+                }
+                wave_minmax(ymn, ymx);
             }
-            const uint64_t recm = __ballot(rec);
-            int rank = 0;  // records with larger y (records have distinct y)
-            for (uint64_t m = recm; m;) {
-                const int k = __ffsll((unsigned long long)m) - 1;
-                m &= m - 1;
-                rank += rl(e.y, k) > e.y;
-            }
-            int32_t ymn = e.y, ymx = e.y;
-            wave_minmax(ymn, ymx);
             const int nrec = __popcll(recm);
             const int4 meta = make_int4(ymn, ymx, min(nrec, kStair) | (nrec > kStair ? 256 : 0), 0);
             int4 *ls = ssum + (b & (kSumRing - 1)) * kSumInts;
@@ -707,6 +734,13 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 const Ent e = fetch(j);
                 double pr = prio(e.f, e.x, e.y, c);
                 int32_t pj = j, py = e.y;
+#if HYMET_CHAIN_MONO
+                // priorities non-increasing along the block: every suffix's argmin is lane 63
+                const double pnx = __shfl_down(pr, 1, 64);
+                if (__ballot(lane == 63 || !(pr < pnx)) == ~0ull) {
+                    pr = rld(pr, 63), pj = (b << 6) + 63, py = rl(e.y, 63);
+                } else
+#endif
                 for (int d = 1; d < 64; d <<= 1) {
                     const double op = __shfl_down(pr, d, 64);
                     const int32_t oj = __shfl_down(pj, d, 64), oy = __shfl_down(py, d, 64);
@@ -978,12 +1012,24 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                                 // the batch's suffix records (values greater than all later ones)
                                 const int v = fk + ksp;
                                 int run = lane < nins ? v : INT32_MIN;
-                                for (int d = 1; d < 64; d <<= 1) {
-                                    const int o = __shfl_down(run, d, 64);
-                                    if (lane + d < 64) run = max(run, o);
+                                int sfx;
+#if HYMET_CHAIN_MONO
+                                // f + span increasing along the batch (colinear): the last entry
+                                // is the only record and the maximum
+                                const int vnx = __shfl_down(v, 1, 64);
+                                if (__ballot(lane >= nins - 1 || v < vnx) == ~0ull) {
+                                    run = rl(v, nins - 1);
+                                    sfx = lane < nins - 1 ? run : INT32_MIN;
+                                } else
+#endif
+                                {
+                                    for (int d = 1; d < 64; d <<= 1) {
+                                        const int o = __shfl_down(run, d, 64);
+                                        if (lane + d < 64) run = max(run, o);
+                                    }
+                                    sfx = __shfl_down(run, 1, 64);
+                                    if (lane == 63) sfx = INT32_MIN;
                                 }
-                                int sfx = __shfl_down(run, 1, 64);
-                                if (lane == 63) sfx = INT32_MIN;
                                 const int vmax = rl(run, 0);
                                 while (it > ih && ib_v <= vmax) {
                                     --it;
@@ -1006,6 +1052,19 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                             // tail-block argmin, and blocks completed by the insertions
                             const int32_t nb0 = i >> 6, nb1 = (i + nins) >> 6;
                             for (int32_t b = nb0; b < nb1; ++b) complete_block(b);
+#if HYMET_CHAIN_MONO
+                            // the last inserted entry is the batch's prefix minimum (priorities fall
+                            // along a colinear chain): it is the argmin of any suffix of the batch,
+                            // so the tail block's argmin is it (or the old tail's, no block completed)
+                            const double pl_last = rld(pk, nins - 1);
+                            if (((i + nins) & 63) == 0) {
+                                t_pr = 0.0, t_j = -1, t_y = 0;  // the tail block is empty
+                            } else if (rld(ipm, nins - 1) == pl_last) {
+                                // the old tail [i & ~63, i) competes only if no block completed
+                                if (nb1 > nb0 || (i & 63) == 0 || t_j < 0 || !(t_pr < pl_last))
+                                    t_pr = pl_last, t_j = i + nins - 1, t_y = rl(ky, nins - 1);
+                            } else
+#endif
                             {
                                 const int32_t tb = (i + nins) & ~63, j = tb + lane;
                                 double tp = 0.0;
