@@ -1243,8 +1243,8 @@ struct BacktrackParams {
     const int32_t *f;
     const int64_t *p;
     int32_t *t;                // zeroed by the caller
-    const int64_t *z_off;      // per group: start of its (f, idx)-ascending z list
-    const int32_t *z_idx;      // anchor indices ordered by (group, f, idx) ascending
+    const int32_t *z_cnt;      // per group: length of its (f, idx)-ascending z list
+    const int32_t *z_idx;      // per group, from g_start[g]: anchor indices by (f, idx) ascending
     int32_t n_groups;
     int min_cnt, min_sc, max_drop;
     int64_t long_min;          // groups above this size go to backtrack_long_kernel
@@ -1285,6 +1285,10 @@ constexpr int64_t kBtLong = 128;
 #define HYMET_BT_CHUNKS 1
 #endif
 constexpr int kBtChunks = HYMET_BT_CHUNKS;
+#ifndef HYMET_BT_PROBE
+#define HYMET_BT_PROBE 4
+#endif
+constexpr int kBtProbe = HYMET_BT_PROBE;  // z probe block: kBtProbe * 64 entries
 
 __device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int64_t uni64(int64_t v) {
@@ -1328,31 +1332,43 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
         if (w >= n_long) break;
         const int32_t g = uni(list[w]);
         const int64_t g0 = uni64(P.g_start[g]);
-        const int64_t z0 = uni64(P.z_off[g]), z1 = uni64(P.z_off[g + 1]);
+        const int64_t z0 = g0, z1 = g0 + uni(P.z_cnt[g]);
         int64_t wpos = g0;
         int nc = 0;
         int64_t k = z1 - 1;
         uint64_t c_probe = 0, c_walk = 0, c_step = 0, c_reload = 0, t_walk = 0, t_post = 0;
         const uint64_t t_g0 = P.prof ? clock64() : 0;
+        // Probe block: kBtProbe * 64 z entries (z index + t mark) loaded in one round trip,
+        // kept across walks.  A walk only marks anchors that were unmarked before it (the few
+        // it unmarks again were marked by itself), so a "marked" reading never goes stale:
+        // after a walk only the next unmarked-looking candidate is re-read (one load) instead
+        // of re-probing the block (most walks are short, so re-probing after each one made
+        // deeper blocks slower).
+        int64_t ptop = -1;  // the block covers z positions (ptop - 64 * kBtProbe, ptop]
+        int32_t zc[kBtProbe], tv[kBtProbe];
+        bool stale = false;
         while (k >= z0) {
-            // probe kBtChunks * 64 z entries per round trip: all index loads, then all t loads
-            c_probe++;
-            int32_t zc[kBtChunks], tv[kBtChunks];
+            if (ptop < 0 || k <= ptop - 64 * kBtProbe) {
+                c_probe++;
+                ptop = k;
+                stale = false;
 #pragma unroll
-            for (int c = 0; c < kBtChunks; c++) {
-                const int64_t kk = k - 64 * c - lane;
-                zc[c] = kk >= z0 ? P.z_idx[kk] : 0;
-            }
+                for (int c = 0; c < kBtProbe; c++) {
+                    const int64_t kk = k - 64 * c - lane;
+                    zc[c] = kk >= z0 ? P.z_idx[kk] : 0;
+                }
 #pragma unroll
-            for (int c = 0; c < kBtChunks; c++) {
-                const int64_t kk = k - 64 * c - lane;
-                tv[c] = kk >= z0 ? ld_l2(P.t + zc[c]) : 1;
+                for (int c = 0; c < kBtProbe; c++) {
+                    const int64_t kk = k - 64 * c - lane;
+                    tv[c] = kk >= z0 ? ld_l2(P.t + zc[c]) : 1;
+                }
             }
+            const int d = (int)(ptop - k);  // entries above k in the block are done
             int hit = -1;
             int32_t zsel = 0;
 #pragma unroll
-            for (int c = kBtChunks - 1; c >= 0; c--) {  // the nearest chunk with an unmarked entry wins
-                const uint64_t m = __ballot(tv[c] == 0);
+            for (int c = kBtProbe - 1; c >= 0; c--) {  // the nearest unmarked entry at or below k wins
+                const uint64_t m = __ballot(tv[c] == 0 && 64 * c + lane >= d);
                 if (m) {
                     const int h = __ffsll((unsigned long long)m) - 1;
                     hit = 64 * c + h;
@@ -1361,11 +1377,13 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             }
             hit = uni(hit);
             if (hit < 0) {
-                k -= 64 * kBtChunks;
+                k = ptop - 64 * kBtProbe;
                 continue;
             }
             const int64_t zi = (int64_t)uni(zsel);
-            k -= hit + 1;
+            k = ptop - hit - 1;
+            if (stale && uni(ld_l2(P.t + zi)) != 0) continue;  // marked by a walk since the probe
+            stale = true;
             const int32_t zf = uni(P.f[zi]);
             int64_t *buf = P.chain_ids + wpos;
             buf[0] = zi;  // every lane: same value, same address
@@ -1481,7 +1499,7 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
     if (P.g_start[g + 1] - g0 > P.long_min) return;  // backtrack_long_kernel
     int64_t wpos = g0;  // next free slot in chain_ids
     int nc = 0;
-    const int64_t z0 = P.z_off[g], z1 = P.z_off[g + 1];
+    const int64_t z0 = g0, z1 = g0 + P.z_cnt[g];
     int64_t k = z1 - 1;
     while (k >= z0) {
         // next z entry (descending) whose anchor is unmarked
@@ -1716,7 +1734,7 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
 }
 
 int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, const int64_t *p, int32_t *t,
-                     const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, const int32_t *order, int32_t n_work,
+                     const int32_t *z_cnt, const int32_t *z_idx, int32_t n_groups, const int32_t *order, int32_t n_work,
                      int min_cnt, int min_sc, int max_drop, int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first,
                      int32_t *n_chains, int64_t n_anchors) {
     if (n_groups <= 0) return HYMET_OK;
@@ -1729,7 +1747,7 @@ int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, c
         HY_HIP(pbuf.alloc(64, ctx->stream));
         HY_HIP(hipMemsetAsync(pbuf.p, 0, 64, ctx->stream));
     }
-    BacktrackParams P{g_start,  f,         p,       t,           z_off,    z_idx, n_groups, min_cnt, min_sc, max_drop,
+    BacktrackParams P{g_start,  f,         p,       t,           z_cnt,    z_idx, n_groups, min_cnt, min_sc, max_drop,
                       long_min, (unsigned long long *)pbuf.p, chain_ids, chain_u, chain_first, n_chains};
     DevBuf cnt;
     HY_HIP(cnt.alloc(8, ctx->stream));

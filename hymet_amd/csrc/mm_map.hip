@@ -29,6 +29,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 struct hymet_mm_result {
     int n_q = 0;
@@ -45,7 +46,7 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
                  int max_dist_inner, int bw, int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip,
                  int64_t n_anchors, int64_t n_groups);
 int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, const int64_t *p, int32_t *t,
-                     const int64_t *z_off, const int32_t *z_idx, int32_t n_groups, const int32_t *order, int32_t n_work,
+                     const int32_t *z_cnt, const int32_t *z_idx, int32_t n_groups, const int32_t *order, int32_t n_work,
                      int min_cnt, int min_sc, int max_drop, int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first,
                      int32_t *n_chains, int64_t n_anchors);
 
@@ -465,148 +466,186 @@ __global__ void group_size_kernel(const int64_t *g_start, int32_t G, int min_cnt
     is_work[g] = sz >= min_cnt ? 1u : 0u;
 }
 
-__global__ void zflag_kernel(const int32_t *f, int64_t n, int min_sc, uint32_t *flag) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) flag[i] = f[i] >= min_sc ? 1u : 0u;
-}
-
-__global__ void zfill_kernel(const int32_t *f, const uint32_t *flag, const int64_t *pos, const int32_t *gid, int64_t n,
-                             uint32_t *zf, uint32_t *zi, uint32_t *zg) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !flag[i]) return;
-    const int64_t o = pos[i];
-    zf[o] = (uint32_t)f[i];
-    zi[o] = (uint32_t)i;
-    zg[o] = (uint32_t)gid[i];
-}
-
-__global__ void zoff_kernel(const uint32_t *zg_sorted, int64_t nz, int32_t G, int64_t *z_off) {
-    // z_off[g] = first position with group >= g
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p > nz) return;
-    const int64_t gp = p == 0 ? -1 : (int64_t)zg_sorted[p - 1];
-    const int64_t gc = p == nz ? (int64_t)G : (int64_t)zg_sorted[p];
-    for (int64_t g = gp + 1; g <= gc; g++) z_off[g] = p;
-}
-
 // ---- backtrack order: z = anchors with f >= min_sc, per group ascending (f, idx) (the
-// backtrack walks it from the end: canonical T3).  A group's z entries are a contiguous,
-// idx-ordered run of the flag scan, so the order is a segmented sort of 64-bit (f << 32 |
-// idx) keys.  Those segments are nearly sorted already: f grows along a colinear chain, so
-// a group is a few ascending runs (one per chain or chain piece).  Runs are found by a flat
-// descent scan; a group of <= kZRuns runs is merged in place of a sort -- every entry's
-// position is its offset in its own run plus, per other run, a binary search (keys are
-// unique).  Groups with more runs fall back to a block bitonic sort in LDS (<= kZs entries)
-// or one global radix sort over all such larger groups.
+// backtrack walks it from the end: canonical T3).  A group's z entries are kept inside the
+// group's own anchor range [g_start[g], g_start[g] + z_cnt[g]), so no global flag scan or
+// offset table is needed.  The entries are nearly sorted already: f grows along a colinear
+// chain, so a group is a few ascending runs (one per chain or chain piece).
+//  * groups of <= kZLane anchors: one lane each, ranks by all-pairs comparison in registers;
+//  * larger groups: one wave each reads the group's f once, compacts its z keys (ballot), finds
+//    the descents between consecutive keys (the previous key by shuffle) and records the
+//    starts of the first kZRuns runs.  A single run is already the order (the wave wrote it).
+//    Groups of <= max_runs runs are merged by a flat kernel -- every entry's position is its
+//    offset in its own run plus, per other run, a binary search (keys are unique).  Groups
+//    with more runs go to a block bitonic sort in LDS (<= kZs entries) or one global radix
+//    sort over all such larger groups (lists appended with atomics: the sorted result does
+//    not depend on the list order).
 constexpr int kZs = 2048;
 constexpr int kZRuns = 16;
+constexpr int kZLane = 16;
 
-__global__ void zoff_direct_kernel(const int64_t *g_start, const int64_t *zpos, int32_t G, int64_t nz, int64_t *z_off) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < G) z_off[g] = zpos[g_start[g]];
-    else if (g == G) z_off[G] = nz;
+struct ZParams {
+    const int32_t *f;
+    const int64_t *g_start;
+    const int32_t *order;  // all groups by descending size (the chaining work list, whole)
+    int32_t G;
+    int min_sc, max_runs;
+    uint64_t *zkey;        // n: (f << 32 | idx) at the group's compacted z positions
+    int32_t *z_idx;        // n: the order, at the same positions
+    int32_t *z_cnt;        // per group: number of z entries
+    int32_t *z_runs;       // per group: ascending runs (0 when empty)
+    int32_t *run_start;    // per group, kZRuns entries: run starts relative to g_start
+    int32_t *lists;        // [0] split, [1] mid count, [2] big count, [4..5] big total (i64, 8-byte aligned)
+    int32_t *mid_list;     // groups for the block sort
+    int32_t *big_list;     // groups for the radix path
+    int64_t *big_off;      // their offsets in the radix arrays
+};
+
+// first list position whose group has <= kZLane anchors
+__global__ void zsplit_kernel(ZParams P) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int32_t lo = 0, hi = P.G;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        const int g = P.order[mid];
+        if (P.g_start[g + 1] - P.g_start[g] <= kZLane) hi = mid;
+        else lo = mid + 1;
+    }
+    P.lists[0] = lo;
 }
 
-__global__ void zfill_key_kernel(const int32_t *f, const uint32_t *flag, const int64_t *pos, const int32_t *gid, int64_t n,
-                                 uint64_t *zkey, uint32_t *zg) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && flag[i]) {
-        const int64_t o = pos[i];
-        zkey[o] = (uint64_t)(uint32_t)f[i] << 32 | (uint32_t)i;
-        zg[o] = (uint32_t)gid[i];
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return (uint64_t)hi << 32 | lo;
+}
+
+// one wave per group of > kZLane anchors (grid-stride over the list prefix)
+__global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
+    const int lane = threadIdx.x & 63;
+    const int32_t split = P.lists[0];
+    const int nw = (int)(gridDim.x * (blockDim.x >> 6));
+    for (int w = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); w < split; w += nw) {
+        const int g = P.order[w];
+        const int64_t g0 = P.g_start[g], n = P.g_start[g + 1] - g0;
+        int32_t *rs = P.run_start + (int64_t)g * kZRuns;
+        int m = 0, K = 0;  // z entries so far, descents so far (wave-uniform)
+        uint64_t last = 0;
+        const uint64_t below = (1ull << lane) - 1;
+        for (int64_t base = 0; base < n; base += 64) {
+            const int64_t i = base + lane;
+            const bool ok = i < n;
+            const int32_t fv = ok ? P.f[g0 + i] : 0;
+            const bool z = ok && fv >= P.min_sc;
+            const uint64_t bal = __ballot(z);
+            if (bal == 0) continue;
+            const uint64_t key = (uint64_t)(uint32_t)fv << 32 | (uint32_t)(g0 + i);
+            const uint64_t lower = bal & below;
+            const int pos = m + __popcll(lower);
+            const int prev = lower ? 63 - __clzll((long long)lower) : lane;
+            uint64_t pk = shfl64(key, prev);
+            if (!lower) pk = last;
+            const bool desc = z && pos > 0 && key < pk;
+            const uint64_t dbal = __ballot(desc);
+            if (z) {
+                P.zkey[g0 + pos] = key;
+                P.z_idx[g0 + pos] = (int32_t)(g0 + i);
+            }
+            if (desc) {
+                const int r = K + 1 + __popcll(dbal & below);
+                if (r < kZRuns) rs[r] = pos;
+            }
+            K += __popcll(dbal);
+            m += __popcll(bal);
+            last = shfl64(key, 63 - __clzll((long long)bal));
+        }
+        const int runs = m > 0 ? K + 1 : 0;
+        if (lane == 0) {
+            rs[0] = 0;
+            P.z_cnt[g] = m;
+            P.z_runs[g] = runs;
+            if (runs > P.max_runs) {
+                if (m <= kZs) {
+                    P.mid_list[atomicAdd(P.lists + 1, 1)] = g;
+                } else {
+                    const int r = atomicAdd(P.lists + 2, 1);
+                    P.big_list[r] = g;
+                    P.big_off[r] = (int64_t)atomicAdd((unsigned long long *)(P.lists + 4), (unsigned long long)m);
+                }
+            }
+        }
     }
 }
 
-// a descent starts a new ascending run inside a group
-__global__ void zdesc_kernel(const uint64_t *zkey, const uint32_t *zg, int64_t nz, uint32_t *desc) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < nz) desc[p] = (p > 0 && zg[p - 1] == zg[p] && zkey[p] < zkey[p - 1]) ? 1u : 0u;
-}
-
-__global__ void zruns_kernel(const uint32_t *desc, const int64_t *dpos, const uint32_t *zg, const int64_t *z_off, int64_t nz,
-                             int64_t *run_start) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= nz || !desc[p]) return;
-    const uint32_t g = zg[p];
-    const int64_t r = dpos[p] - dpos[z_off[g]] + 1;
-    if (r < kZRuns) run_start[(int64_t)g * kZRuns + r] = p;
-}
-
-__device__ __forceinline__ int64_t z_runs(const int64_t *dpos, int64_t z0, int64_t z1) { return dpos[z1] - dpos[z0] + 1; }
-
-// groups with more than kZRuns runs: a block sort (<= kZs entries) or the big radix path
-__global__ void zclass_kernel(const int64_t *z_off, const int64_t *dpos, int32_t G, int max_runs, int32_t *mid_list,
-                              int32_t *mid_cnt, uint32_t *big_flag, uint32_t *big_size) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= G) return;
-    const int64_t z0 = z_off[g], n = z_off[g + 1] - z0;
-    const bool many = n > 1 && z_runs(dpos, z0, z0 + n) > max_runs;
-    big_flag[g] = many && n > kZs ? 1u : 0u;
-    big_size[g] = many && n > kZs ? (uint32_t)n : 0u;
-    // one atomic per wave
-    const bool mid = many && n <= kZs;
-    const uint64_t m = __ballot(mid);
-    if (m) {
-        const int lane = threadIdx.x & 63, first = __ffsll((unsigned long long)m) - 1;
-        int base = 0;
-        if (lane == first) base = atomicAdd(mid_cnt, __popcll(m));
-        base = __shfl(base, first, 64);
-        if (mid) mid_list[base + __popcll(m & ((1ull << lane) - 1))] = g;
+// one lane per group of <= kZLane anchors: rank = number of smaller keys
+__global__ __launch_bounds__(256) void zorder_lane_kernel(ZParams P) {
+    const int32_t w = P.lists[0] + (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (w >= P.G) return;
+    const int g = P.order[w];
+    const int64_t g0 = P.g_start[g];
+    const int n = (int)(P.g_start[g + 1] - g0);
+    uint64_t key[kZLane];
+#pragma unroll
+    for (int j = 0; j < kZLane; j++) {
+        const int32_t fv = j < n ? P.f[g0 + j] : 0;
+        key[j] = j < n && fv >= P.min_sc ? (uint64_t)(uint32_t)fv << 32 | (uint32_t)(g0 + j) : ~0ull;
     }
+    int m = 0;
+#pragma unroll
+    for (int j = 0; j < kZLane; j++) {
+        if (key[j] == ~0ull) continue;
+        int r = 0;
+#pragma unroll
+        for (int k = 0; k < kZLane; k++) r += key[k] < key[j];
+        P.z_idx[g0 + r] = (int32_t)(uint32_t)key[j];
+        m++;
+    }
+    P.z_cnt[g] = m;
+    P.z_runs[g] = m > 0 ? 1 : 0;  // complete
 }
 
-// groups of <= kZRuns ascending runs: merge by ranks
-__global__ void zmerge_kernel(const uint64_t *zkey, const uint32_t *zg, const int64_t *z_off, const int64_t *dpos,
-                              const uint32_t *desc, const int64_t *run_start, int64_t nz, int max_runs, int32_t *z_idx) {
+// groups of 2..max_runs ascending runs: merge by ranks (flat over the anchor positions)
+__global__ void zmerge_kernel(ZParams P, const int32_t *gid, int64_t n) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= nz) return;
-    const uint32_t g = zg[p];
-    const int64_t z0 = z_off[g], z1 = z_off[g + 1];
-    const int64_t K = z_runs(dpos, z0, z1);
-    const uint64_t key = zkey[p];
-    if (K == 1) {
-        z_idx[p] = (int32_t)(uint32_t)key;
-        return;
-    }
-    if (K > max_runs) return;
-    const int r = (int)(dpos[p] + desc[p] - dpos[z0]);
-    const int64_t *rs = run_start + (int64_t)g * kZRuns;
-    int64_t pos = 0;
+    if (p >= n) return;
+    const int g = gid[p];
+    const int K = P.z_runs[g];
+    if (K <= 1 || K > P.max_runs) return;
+    const int64_t z0 = P.g_start[g];
+    const int q = (int)(p - z0), m = P.z_cnt[g];
+    if (q >= m) return;
+    const int32_t *rs = P.run_start + (int64_t)g * kZRuns;
+    const uint64_t *zk = P.zkey + z0;
+    const uint64_t key = zk[q];
+    int pos = 0;
     for (int k = 0; k < K; k++) {
-        const int64_t s0 = k == 0 ? z0 : rs[k], s1 = k + 1 < K ? rs[k + 1] : z1;
-        if (k == r) {
-            pos += p - s0;
+        const int s0 = rs[k], s1 = k + 1 < K ? rs[k + 1] : m;
+        if (q >= s0 && q < s1) {  // own run
+            pos += q - s0;
             continue;
         }
-        int64_t lo = s0, hi = s1;  // first entry >= key
+        int lo = s0, hi = s1;  // first entry >= key
         while (lo < hi) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (zkey[mid] < key) lo = mid + 1;
+            const int mid = (lo + hi) >> 1;
+            if (zk[mid] < key) lo = mid + 1;
             else hi = mid;
         }
         pos += lo - s0;
     }
-    z_idx[z0 + pos] = (int32_t)(uint32_t)key;
-}
-
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
-    return (uint64_t)hi << 32 | lo;
+    P.z_idx[z0 + pos] = (int32_t)(uint32_t)key;
 }
 
 // one block per listed group of <= kZs z entries (grid-stride over the list)
-__global__ __launch_bounds__(256) void zsort_block_kernel(const uint64_t *zkey, const int64_t *z_off, const int32_t *list,
-                                                          const int32_t *cnt, int32_t *z_idx) {
+__global__ __launch_bounds__(256) void zsort_block_kernel(ZParams P) {
     __shared__ uint64_t s[kZs];
-    const int n_list = *cnt;
+    const int n_list = P.lists[1];
     for (int w = blockIdx.x; w < n_list; w += gridDim.x) {
-        const int g = list[w];
-        const int64_t z0 = z_off[g];
-        const int n = (int)(z_off[g + 1] - z0);
+        const int g = P.mid_list[w];
+        const int64_t z0 = P.g_start[g];
+        const int n = P.z_cnt[g];
         int np = 128;
         while (np < n) np <<= 1;
-        for (int i = threadIdx.x; i < np; i += 256) s[i] = i < n ? zkey[z0 + i] : ~0ull;
+        for (int i = threadIdx.x; i < np; i += 256) s[i] = i < n ? P.zkey[z0 + i] : ~0ull;
         __syncthreads();
         for (int k = 2; k <= np; k <<= 1)
             for (int j = k >> 1; j > 0; j >>= 1) {
@@ -622,33 +661,26 @@ __global__ __launch_bounds__(256) void zsort_block_kernel(const uint64_t *zkey, 
                 }
                 __syncthreads();
             }
-        for (int i = threadIdx.x; i < n; i += 256) z_idx[z0 + i] = (int32_t)(uint32_t)s[i];
+        for (int i = threadIdx.x; i < n; i += 256) P.z_idx[z0 + i] = (int32_t)(uint32_t)s[i];
         __syncthreads();
     }
 }
 
-__global__ void zbig_list_kernel(const uint32_t *big_flag, const int64_t *big_rank, int32_t G, int32_t *big_list) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < G && big_flag[g]) big_list[big_rank[g]] = g;
-}
-
-// entries of the large groups, group-major: key = rank << 32 | f, value = idx
-__global__ void zbig_gather_kernel(const uint64_t *zkey, const int64_t *z_off, const int32_t *big_list,
-                                   const int64_t *sub_off, uint64_t *skey, uint32_t *sval) {
-    const int r = blockIdx.x, g = big_list[r];
-    const int64_t z0 = z_off[g], n = z_off[g + 1] - z0, o = sub_off[g];
+// entries of the large groups, list-major: key = rank << 32 | f, value = idx
+__global__ void zbig_gather_kernel(ZParams P, uint64_t *skey, uint32_t *sval) {
+    const int r = blockIdx.x, g = P.big_list[r];
+    const int64_t z0 = P.g_start[g], n = P.z_cnt[g], o = P.big_off[r];
     for (int64_t t = threadIdx.x; t < n; t += blockDim.x) {
-        const uint64_t k = zkey[z0 + t];
+        const uint64_t k = P.zkey[z0 + t];
         skey[o + t] = (uint64_t)r << 32 | (k >> 32);
         sval[o + t] = (uint32_t)k;
     }
 }
 
-__global__ void zbig_scatter_kernel(const uint32_t *sval, const int64_t *z_off, const int32_t *big_list,
-                                    const int64_t *sub_off, int32_t *z_idx) {
-    const int g = big_list[blockIdx.x];
-    const int64_t z0 = z_off[g], n = z_off[g + 1] - z0, o = sub_off[g];
-    for (int64_t t = threadIdx.x; t < n; t += blockDim.x) z_idx[z0 + t] = (int32_t)sval[o + t];
+__global__ void zbig_scatter_kernel(ZParams P, const uint32_t *sval) {
+    const int r = blockIdx.x, g = P.big_list[r];
+    const int64_t z0 = P.g_start[g], n = P.z_cnt[g], o = P.big_off[r];
+    for (int64_t t = threadIdx.x; t < n; t += blockDim.x) P.z_idx[z0 + t] = (int32_t)sval[o + t];
 }
 
 // chain list entries: (key = first anchor index) -> sorted
@@ -677,9 +709,12 @@ __global__ __launch_bounds__(256) void chain_copy_kernel(const uint64_t *cu, con
                                                          const int64_t *chain_ids, const uint64_t *ax, const uint64_t *ay,
                                                          int64_t n_chain, int64_t nb, uint64_t *bx, uint64_t *by,
                                                          int32_t *bchain, int32_t *bsrc) {
-    // flat over the output anchors: the block's first chain by binary search over bpos, each
-    // lane's by a short forward walk (chains are tens to thousands of anchors long)
+    // flat over the output anchors: the block's first chain c0 by binary search over bpos; at
+    // most 256 more chains start inside the block (every chain has >= 1 anchor), so their
+    // starts are staged in LDS and each lane finds its chain by an 8-step search there (a
+    // forward walk per lane cost up to 255 dependent loads where chains are short)
     __shared__ int64_t s_c0;
+    __shared__ int32_t s_st[257];  // block-relative starts of chains c0 .. c0 + 256 (clamped)
     const int64_t b0 = (int64_t)blockIdx.x * blockDim.x;
     if (threadIdx.x == 0) {
         int64_t lo = 0, hi = n_chain - 1;  // last c with bpos[c] <= b0
@@ -691,10 +726,21 @@ __global__ __launch_bounds__(256) void chain_copy_kernel(const uint64_t *cu, con
         s_c0 = lo;
     }
     __syncthreads();
+    const int64_t c0 = s_c0;
+    for (int i = threadIdx.x; i < 257; i += blockDim.x) {
+        const int64_t c = c0 + i;
+        s_st[i] = c < n_chain ? (int32_t)min(bpos[c] - b0, (int64_t)256) : 256;
+    }
+    __syncthreads();
     const int64_t b = b0 + threadIdx.x;
     if (b >= nb) return;
-    int64_t c = s_c0;
-    while (c + 1 < n_chain && bpos[c + 1] <= b) c++;
+    int lo = 0, hi = 256;  // last i with s_st[i] <= threadIdx.x (s_st[0] <= 0, nondecreasing)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_st[mid] <= (int)threadIdx.x) lo = mid;
+        else hi = mid - 1;
+    }
+    const int64_t c = c0 + lo;
     const int32_t m = (int32_t)cu[c];
     const int64_t a = chain_ids[cfirst[c] + m - 1 - (b - bpos[c])];  // backtrack stores end -> start
     bx[b] = ax[a];
@@ -1016,77 +1062,59 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
                           (int32_t)n_work, f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(), opt->max_gap,
                           opt->rmq_inner_dist, bw, opt->max_chain_skip, opt->rmq_size_cap, pen_gap, pen_skip, n, G);
         if (rc) return rc;
-        // z = anchors with f >= min_sc ordered by (group, f, idx)
-        DevBuf zflag, zpos;
-        HY_HIP(zflag.alloc(4 * (size_t)n, ctx->stream));
-        LAUNCH1(zflag_kernel, n, f.as<int32_t>(), n, opt->min_chain_score, zflag.as<uint32_t>());
-        int64_t nz = 0;
-        rc = scan_flags(ctx, zflag.as<uint32_t>(), n, zpos, &nz);
-        if (rc) return rc;
-        DevBuf z_off, zkey, zidx;
-        HY_HIP(z_off.alloc(8 * (size_t)(G + 1), ctx->stream));
-        HY_HIP(zkey.alloc(8 * (size_t)(nz + 1), ctx->stream));
-        HY_HIP(zidx.alloc(4 * (size_t)(nz + 1), ctx->stream));
+        // z = anchors with f >= min_sc ordered by (group, f, idx), inside each group's range
+        DevBuf zkey, zidx, z_cnt, z_runs, run_start, zlists, mid_list, big_list, big_off;
+        HY_HIP(zkey.alloc(8 * (size_t)n, ctx->stream));
+        HY_HIP(zidx.alloc(4 * (size_t)n, ctx->stream));
+        HY_HIP(z_cnt.alloc(4 * (size_t)G, ctx->stream));
+        HY_HIP(z_runs.alloc(4 * (size_t)G, ctx->stream));
+        HY_HIP(run_start.alloc(4 * (size_t)G * kZRuns, ctx->stream));
+        HY_HIP(zlists.alloc(32, ctx->stream));
+        HY_HIP(mid_list.alloc(4 * (size_t)G, ctx->stream));
+        HY_HIP(big_list.alloc(4 * (size_t)G, ctx->stream));
+        HY_HIP(big_off.alloc(8 * (size_t)G, ctx->stream));
         const int32_t *vi = zidx.as<int32_t>();
         {
-            ProfScope _ps(ctx, "mm_z_order", 8.0 * (double)n + 48.0 * (double)nz);  // f, gid read; key/group write, read twice; idx write
-            LAUNCH1(zoff_direct_kernel, G + 1, g_start.as<int64_t>(), zpos.as<int64_t>(), (int32_t)G, nz,
-                    z_off.as<int64_t>());
-            DevBuf zg, desc, dpos, run_start;
-            HY_HIP(zg.alloc(4 * (size_t)(nz + 1), ctx->stream));
-            LAUNCH1(zfill_key_kernel, n, f.as<int32_t>(), zflag.as<uint32_t>(), zpos.as<int64_t>(), gid.as<int32_t>(), n,
-                    zkey.as<uint64_t>(), zg.as<uint32_t>());
-            HY_HIP(desc.alloc(4 * (size_t)(nz + 1), ctx->stream));
-            LAUNCH1(zdesc_kernel, nz, zkey.as<uint64_t>(), zg.as<uint32_t>(), nz, desc.as<uint32_t>());
-            int64_t n_desc = 0;
-            rc = scan_flags(ctx, desc.as<uint32_t>(), nz, dpos, &n_desc);
-            if (rc) return rc;
-            HY_HIP(hipMemcpyAsync(dpos.as<int64_t>() + nz, &n_desc, 8, hipMemcpyHostToDevice, ctx->stream));
-            HY_HIP(run_start.alloc(8 * (size_t)G * kZRuns, ctx->stream));
-            LAUNCH1(zruns_kernel, nz, desc.as<uint32_t>(), dpos.as<int64_t>(), zg.as<uint32_t>(), z_off.as<int64_t>(), nz,
-                    run_start.as<int64_t>());
-            DevBuf mid_list, zcnt, big_flag, big_size;
-            HY_HIP(mid_list.alloc(4 * (size_t)G, ctx->stream));
-            HY_HIP(zcnt.alloc(4, ctx->stream));
-            HY_HIP(big_flag.alloc(4 * (size_t)(G + 1), ctx->stream));
-            HY_HIP(big_size.alloc(4 * (size_t)(G + 1), ctx->stream));
-            HY_HIP(hipMemsetAsync(zcnt.p, 0, 4, ctx->stream));
+            ProfScope _ps(ctx, "mm_z_order", 16.0 * (double)n);  // f read, key + idx written (z entries <= anchors)
+            HY_HIP(hipMemsetAsync(zlists.p, 0, 32, ctx->stream));
             // HYMET_Z_RUNS (tests): merge groups of at most that many runs, sort the others
             const char *ev = getenv("HYMET_Z_RUNS");
             const int max_runs = ev ? std::max(1, std::min(kZRuns, atoi(ev))) : kZRuns;
-            LAUNCH1(zclass_kernel, G, z_off.as<int64_t>(), dpos.as<int64_t>(), (int32_t)G, max_runs, mid_list.as<int32_t>(),
-                    zcnt.as<int32_t>(), big_flag.as<uint32_t>(), big_size.as<uint32_t>());
-            LAUNCH1(zmerge_kernel, nz, zkey.as<uint64_t>(), zg.as<uint32_t>(), z_off.as<int64_t>(), dpos.as<int64_t>(),
-                    desc.as<uint32_t>(), run_start.as<int64_t>(), nz, max_runs, zidx.as<int32_t>());
+            ZParams Z{f.as<int32_t>(), g_start.as<int64_t>(), (const int32_t *)vp, (int32_t)G, opt->min_chain_score,
+                      max_runs, zkey.as<uint64_t>(), zidx.as<int32_t>(), z_cnt.as<int32_t>(), z_runs.as<int32_t>(),
+                      run_start.as<int32_t>(), zlists.as<int32_t>(), mid_list.as<int32_t>(), big_list.as<int32_t>(),
+                      big_off.as<int64_t>()};
+            hipLaunchKernelGGL(zsplit_kernel, dim3(1), dim3(64), 0, ctx->stream, Z);
+            HY_CHECK_LAUNCH("zsplit_kernel");
+            const int64_t nwb = std::min<int64_t>(cdiv(G, 4), (int64_t)ctx->n_cu * 8);
+            hipLaunchKernelGGL(zorder_wave_kernel, dim3((unsigned)std::max<int64_t>(nwb, 1)), dim3(256), 0, ctx->stream, Z);
+            HY_CHECK_LAUNCH("zorder_wave_kernel");
+            LAUNCH1(zorder_lane_kernel, G, Z);
+            LAUNCH1(zmerge_kernel, n, Z, (const int32_t *)gid.as<int32_t>(), n);
             const int64_t nb = std::min<int64_t>(G, (int64_t)ctx->n_cu * 8);
-            hipLaunchKernelGGL(zsort_block_kernel, dim3((unsigned)nb), dim3(256), 0, ctx->stream, zkey.as<uint64_t>(),
-                               z_off.as<int64_t>(), mid_list.as<int32_t>(), zcnt.as<int32_t>(), zidx.as<int32_t>());
+            hipLaunchKernelGGL(zsort_block_kernel, dim3((unsigned)nb), dim3(256), 0, ctx->stream, Z);
             HY_CHECK_LAUNCH("zsort_block_kernel");
-            DevBuf big_rank, sub_off;
-            int64_t n_big = 0, nz_big = 0;
-            rc = scan_flags(ctx, big_flag.as<uint32_t>(), G, big_rank, &n_big);
-            if (rc) return rc;
-            rc = scan_flags(ctx, big_size.as<uint32_t>(), G, sub_off, &nz_big);
-            if (rc) return rc;
+            int32_t hl[8];
+            HY_HIP(hipMemcpyAsync(hl, zlists.p, 32, hipMemcpyDeviceToHost, ctx->stream));
+            HY_HIP(hipStreamSynchronize(ctx->stream));
+            const int64_t n_big = hl[2];
+            int64_t nz_big = 0;
+            std::memcpy(&nz_big, hl + 4, 8);
             if (n_big > 0) {
-                DevBuf big_list, sk, sk2, sv, sv2;
-                HY_HIP(big_list.alloc(4 * (size_t)n_big, ctx->stream));
+                DevBuf sk, sk2, sv, sv2;
                 HY_HIP(sk.alloc(8 * (size_t)nz_big, ctx->stream));
                 HY_HIP(sk2.alloc(8 * (size_t)nz_big, ctx->stream));
                 HY_HIP(sv.alloc(4 * (size_t)nz_big, ctx->stream));
                 HY_HIP(sv2.alloc(4 * (size_t)nz_big, ctx->stream));
-                LAUNCH1(zbig_list_kernel, G, big_flag.as<uint32_t>(), big_rank.as<int64_t>(), (int32_t)G,
-                        big_list.as<int32_t>());
-                hipLaunchKernelGGL(zbig_gather_kernel, dim3((unsigned)n_big), dim3(256), 0, ctx->stream, zkey.as<uint64_t>(),
-                                   z_off.as<int64_t>(), big_list.as<int32_t>(), sub_off.as<int64_t>(), sk.as<uint64_t>(),
+                hipLaunchKernelGGL(zbig_gather_kernel, dim3((unsigned)n_big), dim3(256), 0, ctx->stream, Z, sk.as<uint64_t>(),
                                    sv.as<uint32_t>());
                 HY_CHECK_LAUNCH("zbig_gather_kernel");
                 uint64_t *kp = sk.as<uint64_t>(), *ka = sk2.as<uint64_t>();
                 uint32_t *vp2 = sv.as<uint32_t>(), *va2 = sv2.as<uint32_t>();
                 rc = sort_pairs(ctx, kp, ka, vp2, va2, nz_big, 0, 32 + bits_for(n_big), "radix_sort_z_big");
                 if (rc) return rc;
-                hipLaunchKernelGGL(zbig_scatter_kernel, dim3((unsigned)n_big), dim3(256), 0, ctx->stream, vp2,
-                                   z_off.as<int64_t>(), big_list.as<int32_t>(), sub_off.as<int64_t>(), zidx.as<int32_t>());
+                hipLaunchKernelGGL(zbig_scatter_kernel, dim3((unsigned)n_big), dim3(256), 0, ctx->stream, Z,
+                                   (const uint32_t *)vp2);
                 HY_CHECK_LAUNCH("zbig_scatter_kernel");
             }
         }
@@ -1096,14 +1124,16 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(chain_first.alloc(8 * (size_t)n, ctx->stream));
         HY_HIP(n_chains.alloc(4 * (size_t)G, ctx->stream));
         if (getenv("HYMET_TRACE_BT")) {  // diagnostic: backtrack time vs the largest groups
-            std::vector<int64_t> gs(G + 1), zo(G + 1);
+            std::vector<int64_t> gs(G + 1);
+            std::vector<int32_t> zc(G);
             HY_HIP(hipMemcpyAsync(gs.data(), g_start.p, 8 * (size_t)(G + 1), hipMemcpyDeviceToHost, ctx->stream));
-            HY_HIP(hipMemcpyAsync(zo.data(), z_off.p, 8 * (size_t)(G + 1), hipMemcpyDeviceToHost, ctx->stream));
+            HY_HIP(hipMemcpyAsync(zc.data(), z_cnt.p, 4 * (size_t)G, hipMemcpyDeviceToHost, ctx->stream));
             HY_HIP(hipStreamSynchronize(ctx->stream));
-            int64_t mg = 0, mz = 0, big = 0;
+            int64_t mg = 0, mz = 0, big = 0, nz = 0;
             for (int64_t g = 0; g < G; g++) {
                 mg = std::max(mg, gs[g + 1] - gs[g]);
-                mz = std::max(mz, zo[g + 1] - zo[g]);
+                mz = std::max(mz, (int64_t)zc[g]);
+                nz += zc[g];
                 big += gs[g + 1] - gs[g] > 10000;
             }
             fprintf(stderr, "[bt] G=%lld n=%lld nz=%lld max_group=%lld max_z=%lld groups>10k=%lld", (long long)G,
@@ -1111,7 +1141,7 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         }
         const auto bt0 = std::chrono::steady_clock::now();
         rc = launch_backtrack(ctx, g_start.as<int64_t>(), f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(),
-                              z_off.as<int64_t>(), (const int32_t *)vi, (int32_t)G, (const int32_t *)vp, (int32_t)n_work,
+                              z_cnt.as<int32_t>(), (const int32_t *)vi, (int32_t)G, (const int32_t *)vp, (int32_t)n_work,
                               opt->min_cnt, opt->min_chain_score, bw,
                               chain_ids.as<int64_t>(), chain_u.as<uint64_t>(), chain_first.as<int64_t>(),
                               n_chains.as<int32_t>(), n);
