@@ -1338,12 +1338,13 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
         int64_t k = z1 - 1;
         uint64_t c_probe = 0, c_walk = 0, c_step = 0, c_reload = 0, t_walk = 0, t_post = 0;
         const uint64_t t_g0 = P.prof ? clock64() : 0;
-        // Probe block: kBtProbe * 64 z entries (z index + t mark) loaded in one round trip,
+        // Probe block: kBtProbe * 64 z entries (z index, then t mark: two dependent loads),
         // kept across walks.  A walk only marks anchors that were unmarked before it (the few
         // it unmarks again were marked by itself), so a "marked" reading never goes stale:
-        // after a walk only the next unmarked-looking candidate is re-read (one load) instead
-        // of re-probing the block (most walks are short, so re-probing after each one made
-        // deeper blocks slower).
+        // after a walk only the marks that read unmarked are re-read, from the cached z
+        // indices (one round trip instead of two).  (Re-reading just the next candidate after
+        // each walk was 2.6x slower: walks mark the upcoming candidates, so most re-reads
+        // failed one round trip at a time.)
         int64_t ptop = -1;  // the block covers z positions (ptop - 64 * kBtProbe, ptop]
         int32_t zc[kBtProbe], tv[kBtProbe];
         bool stale = false;
@@ -1361,6 +1362,13 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                 for (int c = 0; c < kBtProbe; c++) {
                     const int64_t kk = k - 64 * c - lane;
                     tv[c] = kk >= z0 ? ld_l2(P.t + zc[c]) : 1;
+                }
+            } else if (stale) {  // a walk since the probe: re-read the marks (z indices stay valid)
+                stale = false;
+#pragma unroll
+                for (int c = 0; c < kBtProbe; c++) {
+                    const int64_t kk = ptop - 64 * c - lane;
+                    if (kk >= z0 && kk <= k && tv[c] == 0) tv[c] = ld_l2(P.t + zc[c]);
                 }
             }
             const int d = (int)(ptop - k);  // entries above k in the block are done
@@ -1382,7 +1390,6 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             }
             const int64_t zi = (int64_t)uni(zsel);
             k = ptop - hit - 1;
-            if (stale && uni(ld_l2(P.t + zi)) != 0) continue;  // marked by a walk since the probe
             stale = true;
             const int32_t zf = uni(P.f[zi]);
             int64_t *buf = P.chain_ids + wpos;

@@ -699,20 +699,57 @@ __global__ void chain_list_kernel(const int64_t *g_start, const int32_t *n_chain
     }
 }
 
-__global__ void chain_cnt_kernel(const uint64_t *cu, int64_t n, uint32_t *cnt) {
+// anchors per chain in the compacted copy; with a long join (qflag), chains of flagged
+// queries are left out of the copy and counted in cnt2 instead (they are only marked)
+__global__ void chain_cnt_kernel(const uint64_t *cu, const uint32_t *cq, const uint32_t *qflag, int64_t n, uint32_t *cnt,
+                                 uint32_t *cnt2) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) cnt[i] = (uint32_t)cu[i];
+    if (i >= n) return;
+    const uint32_t m = (uint32_t)cu[i];
+    const bool fl = qflag && qflag[cq[i]];
+    cnt[i] = fl ? 0u : m;
+    if (cnt2) cnt2[i] = fl ? m : 0u;
 }
 
-// anchors of chain c in start -> end order, and c per anchor
+// long join, first pass (map.c's rmq rescue): a query is re-chained when it has more than one
+// chain and its first chain (compact order) leaves too much of it uncovered -- read from the
+// chain list before the copy
+__global__ void rechain_flag_kernel(const uint64_t *ay, const int64_t *chain_ids, const uint64_t *cu, const int64_t *cfirst,
+                                    const int64_t *qc, const int64_t *qlen, int n_q, int rescue_size, float rescue_ratio,
+                                    uint32_t *flag) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n_q) return;
+    const int64_t c0 = qc[q], nc = qc[q + 1] - c0;
+    uint32_t f = 0;
+    if (nc > 1) {
+        const int32_t m = (int32_t)cu[c0];
+        const int64_t fo = cfirst[c0];  // backtrack stores end -> start
+        const int32_t st = (int32_t)ay[chain_ids[fo + m - 1]], en = (int32_t)ay[chain_ids[fo]];
+        const int32_t ql = (int32_t)qlen[q];
+        if (ql - (en - st) > rescue_size || (float)(en - st) > __fmul_rn((float)ql, rescue_ratio)) f = 1;
+    }
+    flag[q] = f;
+}
+
+// per-query anchor offsets of a compacted copy: the offset of the query's first chain
+__global__ void chain_qb_kernel(const int64_t *qc, const int64_t *bpos, int64_t n_chain, int64_t nb, int n_q, int64_t *qb) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q > n_q) return;
+    const int64_t c = qc[q];
+    qb[q] = c < n_chain ? bpos[c] : nb;
+}
+
+// anchors of chain c in start -> end order, and c per anchor; or (mark != nullptr) only a mark
+// on every counted chain's anchors in the chained anchor set (the long join compacts by it)
 __global__ __launch_bounds__(256) void chain_copy_kernel(const uint64_t *cu, const int64_t *cfirst, const int64_t *bpos,
                                                          const int64_t *chain_ids, const uint64_t *ax, const uint64_t *ay,
                                                          int64_t n_chain, int64_t nb, uint64_t *bx, uint64_t *by,
-                                                         int32_t *bchain, int32_t *bsrc) {
-    // flat over the output anchors: the block's first chain c0 by binary search over bpos; at
-    // most 256 more chains start inside the block (every chain has >= 1 anchor), so their
-    // starts are staged in LDS and each lane finds its chain by an 8-step search there (a
-    // forward walk per lane cost up to 255 dependent loads where chains are short)
+                                                         int32_t *bchain, uint8_t *mark) {
+    // flat over the output anchors: the block's first chain c0 by binary search over bpos; the
+    // starts of the next 256 chains are staged in LDS and each lane finds its chain by an
+    // 8-step search there (a forward walk per lane cost up to 255 dependent loads where chains
+    // are short).  Chains left out of the copy have no anchors, so more than 256 may start in
+    // the block: lanes past the staged ones search bpos itself.
     __shared__ int64_t s_c0;
     __shared__ int32_t s_st[257];  // block-relative starts of chains c0 .. c0 + 256 (clamped)
     const int64_t b0 = (int64_t)blockIdx.x * blockDim.x;
@@ -740,20 +777,25 @@ __global__ __launch_bounds__(256) void chain_copy_kernel(const uint64_t *cu, con
         if (s_st[mid] <= (int)threadIdx.x) lo = mid;
         else hi = mid - 1;
     }
-    const int64_t c = c0 + lo;
+    int64_t c = c0 + lo;
+    if (lo == 256) {  // last c with bpos[c] <= b beyond the staged chains
+        int64_t l2 = c, h2 = n_chain - 1;
+        while (l2 < h2) {
+            const int64_t mid = (l2 + h2 + 1) >> 1;
+            if (bpos[mid] <= b) l2 = mid;
+            else h2 = mid - 1;
+        }
+        c = l2;
+    }
     const int32_t m = (int32_t)cu[c];
     const int64_t a = chain_ids[cfirst[c] + m - 1 - (b - bpos[c])];  // backtrack stores end -> start
+    if (mark) {
+        mark[a] = 1;
+        return;
+    }
     bx[b] = ax[a];
     by[b] = ay[a];
     bchain[b] = (int32_t)c;
-    bsrc[b] = (int32_t)a;  // index in the chained anchor set (the long join compacts by it)
-}
-
-// long join: anchors of flagged queries' chains marked in the first-pass anchor set
-__global__ void rechain_mark_kernel(const int32_t *bchain, const uint32_t *cq, const int32_t *bsrc, const uint32_t *flag,
-                                    int64_t nb, uint8_t *mark) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nb && flag[cq[bchain[b]]]) mark[bsrc[b]] = 1;
 }
 
 // marked anchors per 4096-anchor tile (16 per thread, one 16-byte load)
@@ -920,11 +962,24 @@ struct AnchorSet {
 struct ChainSet {
     DevBuf bx, by, cu, cboff;  // cboff: offset of each chain's anchors in bx/by
     DevBuf bchain, cq;         // chain of each compacted anchor; query of each chain
-    DevBuf bsrc;               // index of each compacted anchor in the chained anchor set
     int64_t n_anchor = 0, n_chain = 0;
     std::vector<int64_t> h_qc;   // n_q + 1 chain offsets per query
     std::vector<int64_t> h_qb;   // n_q + 1 anchor offsets per query
     DevBuf d_qc, d_qb;
+};
+
+// A first pass followed by the long join (map.c's rmq rescue): chain_set flags the re-chained
+// queries from its chain list; with mark_only their chains are not copied out (their regions
+// are never built) but marked in the chained anchor set, which the long join compacts.
+struct LeanJoin {
+    const int64_t *qlen;
+    int rescue_size;
+    float rescue_ratio;
+    bool mark_only;
+    DevBuf flag;                 // per query: re-chained
+    DevBuf mark;                 // mark_only: per anchor of the set (+16 bytes for 16-byte loads)
+    std::vector<int64_t> h_qb2;  // mark_only: n_q + 1 offsets of the re-chained queries' chain anchors
+    int64_t n2 = 0;
 };
 
 // sort raw anchors (x, y, k1 with k2 keys) into an AnchorSet
@@ -993,7 +1048,7 @@ static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n,
 
 // chaining + backtrack + compact_a over an anchor set
 static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, float pen_skip, int bw, AnchorSet &A,
-                     int n_q, ChainSet &C) {
+                     int n_q, ChainSet &C, LeanJoin *lj = nullptr) {
     const int64_t n = A.n;
     C.h_qc.assign(n_q + 1, 0);
     C.h_qb.assign(n_q + 1, 0);
@@ -1180,22 +1235,6 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         LAUNCH1(gather_kernel<uint64_t>, NC, C.cu.as<uint64_t>(), pp, cu_s.as<uint64_t>(), NC);
         LAUNCH1(gather_kernel<int64_t>, NC, cfirst.as<int64_t>(), pp, cf_s.as<int64_t>(), NC);
         C.cu.swap(cu_s);
-        // anchors of every chain, compacted in chain order
-        DevBuf ccnt;
-        HY_HIP(ccnt.alloc(4 * (size_t)(NC + 1), ctx->stream));
-        LAUNCH1(chain_cnt_kernel, NC, C.cu.as<uint64_t>(), NC, ccnt.as<uint32_t>());
-        int64_t NB = 0;
-        rc = scan_flags(ctx, ccnt.as<uint32_t>(), NC, C.cboff, &NB);
-        if (rc) return rc;
-        C.n_anchor = NB;
-        HY_HIP(C.bx.alloc(8 * (size_t)(NB + 1), ctx->stream));
-        HY_HIP(C.by.alloc(8 * (size_t)(NB + 1), ctx->stream));
-        HY_HIP(C.bchain.alloc(4 * (size_t)(NB + 1), ctx->stream));
-        HY_HIP(C.bsrc.alloc(4 * (size_t)(NB + 1), ctx->stream));
-        if (NC > 0 && NB > 0)
-            LAUNCH1(chain_copy_kernel, NB, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), C.cboff.as<int64_t>(),
-                    chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, NB, C.bx.as<uint64_t>(),
-                    C.by.as<uint64_t>(), C.bchain.as<int32_t>(), C.bsrc.as<int32_t>());
         // per-query chain offsets
         DevBuf &cq = C.cq;
         HY_HIP(cq.alloc(4 * (size_t)(NC + 1), ctx->stream));
@@ -1204,14 +1243,54 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         hipLaunchKernelGGL(count_per_query_kernel, dim3((unsigned)cdiv(NC + 1, 256)), dim3(256), 0, ctx->stream,
                            cq.as<uint32_t>(), NC, n_q, C.d_qc.as<int64_t>());
         HY_CHECK_LAUNCH("count_per_query_kernel");
-        HY_HIP(hipMemcpyAsync(C.h_qc.data(), C.d_qc.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, ctx->stream));
-        std::vector<int64_t> cbo(NC + 1);
-        if (NC) HY_HIP(hipMemcpyAsync(cbo.data(), C.cboff.p, 8 * (size_t)NC, hipMemcpyDeviceToHost, ctx->stream));
-        HY_HIP(hipStreamSynchronize(ctx->stream));
-        cbo[NC] = NB;
-        for (int q = 0; q <= n_q; q++) C.h_qb[q] = cbo[C.h_qc[q]];
+        // long join: the re-chained queries, from the chain list
+        const uint32_t *qflag = nullptr;
+        if (lj) {
+            HY_HIP(lj->flag.alloc(4 * (size_t)n_q, ctx->stream));
+            LAUNCH1(rechain_flag_kernel, n_q, A.ay.as<uint64_t>(), chain_ids.as<int64_t>(), C.cu.as<uint64_t>(),
+                    cf_s.as<int64_t>(), C.d_qc.as<int64_t>(), lj->qlen, n_q, lj->rescue_size, lj->rescue_ratio,
+                    lj->flag.as<uint32_t>());
+            if (lj->mark_only) qflag = lj->flag.as<uint32_t>();
+        }
+        // anchors of every chain (but those only marked), compacted in chain order
+        DevBuf ccnt, ccnt2;
+        HY_HIP(ccnt.alloc(4 * (size_t)(NC + 1), ctx->stream));
+        if (qflag) HY_HIP(ccnt2.alloc(4 * (size_t)(NC + 1), ctx->stream));
+        LAUNCH1(chain_cnt_kernel, NC, C.cu.as<uint64_t>(), cq.as<uint32_t>(), qflag, NC, ccnt.as<uint32_t>(),
+                qflag ? ccnt2.as<uint32_t>() : nullptr);
+        int64_t NB = 0;
+        rc = scan_flags(ctx, ccnt.as<uint32_t>(), NC, C.cboff, &NB);
+        if (rc) return rc;
+        C.n_anchor = NB;
+        HY_HIP(C.bx.alloc(8 * (size_t)(NB + 1), ctx->stream));
+        HY_HIP(C.by.alloc(8 * (size_t)(NB + 1), ctx->stream));
+        HY_HIP(C.bchain.alloc(4 * (size_t)(NB + 1), ctx->stream));
+        if (NC > 0 && NB > 0)
+            LAUNCH1(chain_copy_kernel, NB, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), C.cboff.as<int64_t>(),
+                    chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, NB, C.bx.as<uint64_t>(),
+                    C.by.as<uint64_t>(), C.bchain.as<int32_t>(), (uint8_t *)nullptr);
         HY_HIP(C.d_qb.alloc(8 * (size_t)(n_q + 1), ctx->stream));
-        HY_HIP(hipMemcpyAsync(C.d_qb.p, C.h_qb.data(), 8 * (size_t)(n_q + 1), hipMemcpyHostToDevice, ctx->stream));
+        LAUNCH1(chain_qb_kernel, n_q + 1, C.d_qc.as<int64_t>(), C.cboff.as<int64_t>(), NC, NB, n_q, C.d_qb.as<int64_t>());
+        HY_HIP(hipMemcpyAsync(C.h_qc.data(), C.d_qc.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, ctx->stream));
+        HY_HIP(hipMemcpyAsync(C.h_qb.data(), C.d_qb.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, ctx->stream));
+        if (qflag) {  // the re-chained queries' chain anchors: marked in the chained set, per-query counts
+            DevBuf boff2, qb2;
+            int64_t NB2 = 0;
+            rc = scan_flags(ctx, ccnt2.as<uint32_t>(), NC, boff2, &NB2);
+            if (rc) return rc;
+            HY_HIP(lj->mark.alloc((size_t)n + 16, ctx->stream));
+            HY_HIP(hipMemsetAsync(lj->mark.p, 0, (size_t)n + 16, ctx->stream));
+            if (NB2 > 0)
+                LAUNCH1(chain_copy_kernel, NB2, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), boff2.as<int64_t>(),
+                        chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, NB2, (uint64_t *)nullptr,
+                        (uint64_t *)nullptr, (int32_t *)nullptr, lj->mark.as<uint8_t>());
+            HY_HIP(qb2.alloc(8 * (size_t)(n_q + 1), ctx->stream));
+            LAUNCH1(chain_qb_kernel, n_q + 1, C.d_qc.as<int64_t>(), boff2.as<int64_t>(), NC, NB2, n_q, qb2.as<int64_t>());
+            lj->h_qb2.assign(n_q + 1, 0);
+            HY_HIP(hipMemcpyAsync(lj->h_qb2.data(), qb2.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, ctx->stream));
+            lj->n2 = NB2;
+            HY_HIP(hipStreamSynchronize(ctx->stream));
+        }
         HY_HIP(hipStreamSynchronize(ctx->stream));
     }
     return HYMET_OK;
@@ -1238,21 +1317,6 @@ __global__ void mini_table_kernel(const uint64_t *my, const uint32_t *seed_n, co
     if (i >= M || !seed_n[i]) return;
     const uint32_t q = qid[i];
     pos_tab[qbase[q] + ((uint32_t)my[i] >> 1)] = (int32_t)(mp_pos[i] - mp_pos[qm_off[q]]);
-}
-
-__global__ void rechain_flag_kernel(const uint64_t *by, const uint64_t *cu, const int64_t *qc, const int64_t *qb,
-                                    const int64_t *qlen, int n_q, int rescue_size, float rescue_ratio, uint32_t *flag) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n_q) return;
-    const int64_t c0 = qc[q], nc = qc[q + 1] - c0;
-    uint32_t f = 0;
-    if (nc > 1) {  // map.c: re-chain / long-join for long sequences
-        const int64_t b0 = qb[q];
-        const int32_t st = (int32_t)by[b0], en = (int32_t)by[b0 + (int32_t)cu[c0] - 1];
-        const int32_t ql = (int32_t)qlen[q];
-        if (ql - (en - st) > rescue_size || (float)(en - st) > __fmul_rn((float)ql, rescue_ratio)) f = 1;
-    }
-    flag[q] = f;
 }
 
 // re-chain input: the chained anchors of flagged queries (query-major), with sort keys
@@ -1628,19 +1692,18 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     if (rc) return rc;
     // ------------------------------------------------ 6 chain (+ 7 long join)
     ChainSet C1;
-    rc = chain_set(ctx, opt, pen_gap, pen_skip, opt->bw, S1, n_q, C1);
+    const bool long_join = opt->bw_long > opt->bw;
+    const bool resort = getenv("HYMET_RECHAIN_SORT") != nullptr;  // tests: the re-sort path
+    LeanJoin lj{d_qlen.as<int64_t>(), opt->rmq_rescue_size, opt->rmq_rescue_ratio, key_path && !resort};
+    rc = chain_set(ctx, opt, pen_gap, pen_skip, opt->bw, S1, n_q, C1, long_join ? &lj : nullptr);
     if (rc) return rc;
     tr.mark("chain_set 1");
     ChainSet *CF = &C1;
     ChainSet C2;
     std::vector<uint32_t> h_flag(n_q, 0);
     DevBuf flag;  // queries re-chained by the long join (their first-pass regions are not built)
-    if (opt->bw_long > opt->bw && C1.n_chain > 0) {
-        HY_HIP(flag.alloc(4 * (size_t)n_q, st));
-        hipLaunchKernelGGL(rechain_flag_kernel, dim3((unsigned)cdiv(n_q, 256)), dim3(256), 0, st, C1.by.as<uint64_t>(),
-                           C1.cu.as<uint64_t>(), C1.d_qc.as<int64_t>(), C1.d_qb.as<int64_t>(), d_qlen.as<int64_t>(), n_q,
-                           opt->rmq_rescue_size, opt->rmq_rescue_ratio, flag.as<uint32_t>());
-        HY_CHECK_LAUNCH("rechain_flag_kernel");
+    if (long_join && C1.n_chain > 0) {
+        flag.swap(lj.flag);
         HY_HIP(hipMemcpyAsync(h_flag.data(), flag.p, 4 * (size_t)n_q, hipMemcpyDeviceToHost, st));
         HY_HIP(hipStreamSynchronize(st));
         bool any = false;
@@ -1649,20 +1712,17 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
             // anchors of flagged queries only: new per-query offsets
             AnchorSet S2;
             S2.h_off.assign(n_q + 1, 0);
-            for (int q = 0; q < n_q; q++) S2.h_off[q + 1] = S2.h_off[q] + (h_flag[q] ? C1.h_qb[q + 1] - C1.h_qb[q] : 0);
+            const std::vector<int64_t> &qb = lj.mark_only ? lj.h_qb2 : C1.h_qb;
+            for (int q = 0; q < n_q; q++) S2.h_off[q + 1] = S2.h_off[q] + (h_flag[q] ? qb[q + 1] - qb[q] : 0);
             const int64_t A2 = S2.h_off[n_q];
             HY_HIP(S2.d_off.alloc(8 * (size_t)(n_q + 1), st));
             HY_HIP(hipMemcpyAsync(S2.d_off.p, S2.h_off.data(), 8 * (size_t)(n_q + 1), hipMemcpyHostToDevice, st));
-            const bool resort = getenv("HYMET_RECHAIN_SORT") != nullptr;  // tests: the re-sort path
-            if (key_path && !resort) {
-                // the flagged queries' chain anchors, compacted out of the first-pass set in its
-                // (key, y) order -- already the long join's sorted anchor set
+            if (lj.mark_only) {
+                // the flagged queries' chain anchors (marked by chain_set), compacted out of the
+                // first-pass set in its (key, y) order -- already the long join's sorted anchor set
                 const int64_t n1 = S1.n, nt = cdiv(n1, 4096);
-                DevBuf mark, tcnt, toff;
-                HY_HIP(mark.alloc((size_t)n1 + 16, st));
-                HY_HIP(hipMemsetAsync(mark.p, 0, (size_t)n1 + 16, st));
-                LAUNCH1(rechain_mark_kernel, C1.n_anchor, C1.bchain.as<int32_t>(), C1.cq.as<uint32_t>(), C1.bsrc.as<int32_t>(),
-                        flag.as<uint32_t>(), C1.n_anchor, mark.as<uint8_t>());
+                DevBuf &mark = lj.mark;
+                DevBuf tcnt, toff;
                 HY_HIP(tcnt.alloc(4 * (size_t)(nt + 1), st));
                 HY_HIP(toff.alloc(8 * (size_t)(nt + 1), st));
                 hipLaunchKernelGGL(mark_count_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<uint8_t>(), n1,
@@ -1671,7 +1731,7 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                 int64_t got = 0;
                 rc = exclusive_scan_u32_i64(ctx, tcnt.as<uint32_t>(), toff.as<int64_t>(), nt, &got);
                 if (rc) return rc;
-                if (got != A2) return hymet::fail(HYMET_E_INTERNAL, "hymet_mm_map: long-join anchor count mismatch");
+                if (got != A2 || got != lj.n2) return hymet::fail(HYMET_E_INTERNAL, "hymet_mm_map: long-join anchor count mismatch");
                 HY_HIP(S2.ax.alloc(8 * (size_t)(A2 + 1), st));
                 HY_HIP(S2.ay.alloc(8 * (size_t)(A2 + 1), st));
                 HY_HIP(S2.k1.alloc(8 * (size_t)(A2 + 1), st));
