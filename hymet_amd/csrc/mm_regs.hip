@@ -2,12 +2,11 @@
 // mm_gen_regs (score + hash order), mm_reg_set_coor / mm_cal_fuzzy_len, mm_set_parent,
 // mm_select_sub (+ mm_sync_regs), mm_est_err, mm_filter_strand_retained, mm_set_mapq.
 // Everything that walks a chain's anchors is anchor-parallel and runs first:
-//   anchor_mini_idx_kernel  one thread per chained anchor: its index among the query
-//                           minimizers (mm_est_err's get_mini_idx, by table lookup);
-//   chain_stats_kernel      one wave per chain: mlen/blen sums (mm_reg_set_coor) and the first
-//                           anchor, in est_err's walking order, whose minimizer index does not
-//                           increase -- est_err's sequential two-pointer walk matches exactly
-//                           the prefix before it;
+//   chain_stats_flat_kernel one thread per chained anchor: mlen/blen terms (mm_reg_set_coor),
+//                           its minimizer index (mm_est_err's get_mini_idx, by table lookup)
+//                           and the first anchor, in est_err's walking order, whose index does
+//                           not increase -- est_err's sequential two-pointer walk matches
+//                           exactly the prefix before it; segmented per chain;
 //   query_sumk_kernel       one wave per query: sum of minimizer spans (avg_k).
 // regions_kernel then runs one thread per query: a query has few chains (tens) and every step
 // left is an O(n^2)-at-most scan over them.  Scratch lives in global memory at the query's
@@ -88,7 +87,7 @@ struct RegParams {
     uint64_t *cov;
     int32_t *tmp;
     int32_t *n_regs;
-    // per-chain anchor statistics (chain_stats_kernel)
+    // per-chain anchor statistics (chain_stats_flat_kernel)
     const int32_t *c_mlen, *c_blen, *c_st, *c_last, *c_fv;
     const uint64_t *q_sumk;
     const uint32_t *skip_q;        // queries whose regions come from the long join (nullable)
@@ -108,7 +107,7 @@ __device__ void set_coor(hymet_mm_reg *r, int32_t qlen, const uint64_t *ax, cons
         r->qs = qlen - ((int32_t)ay[k + r->cnt - 1] + 1);
         r->qe = qlen - ((int32_t)ay[k] + 1 - q_span);
     }
-    r->mlen = mlen;  // span(first) + sum over consecutive anchors (chain_stats_kernel)
+    r->mlen = mlen;  // span(first) + sum over consecutive anchors (chain_stats_flat_kernel)
     r->blen = blen;
 }
 
@@ -131,80 +130,78 @@ struct AnchorStatParams {
     int n_q;
     const int32_t *bchain;   // chain of each anchor (chain_copy_kernel)
     const uint32_t *cq;      // query of each chain
-    int32_t *a_idx, *c_mlen, *c_blen, *c_st, *c_last;
+    int32_t *c_mlen, *c_blen, *c_st, *c_last;
     const int32_t *pos_tab;  // query base -> minimizer index (or -1), at qbase[q] + position
     const int64_t *qbase;
     const uint32_t *skip_q;  // queries whose chains are superseded by the long join (nullable)
 };
 
-// per chained anchor: its index among the query minimizers (mm_est_err's get_mini_idx).  The
-// binary search over the query's minimizer positions is replaced by one load from a dense
+// Per-chain anchor statistics, flat over the chained anchors (chains are contiguous runs of
+// the copy): mm_reg_set_coor's mlen/blen sums, and for mm_est_err the walk-order first/last
+// minimizer index and the first anchor whose index does not increase (est_err's loop
+// `for (k=1, j=st+1; j<nm && k<cnt; ++j) if (idx(k) == j) ++k, ++n_match;` matches anchor k
+// iff idx(1..k) strictly increase from st; the first that does not, or has no minimizer,
+// stalls it to the end).  The minimizer index (get_mini_idx) is one load from a dense
 // position -> index table (pos_tab, one int32 per query base, -1 where no seeded minimizer
-// starts; built by mini_table_kernel in hymet_mm_map): same result, one random read.
-__global__ void anchor_mini_idx_kernel(AnchorStatParams P) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= P.NB) return;
-    const int64_t q = P.cq[P.bchain[b]];
-    if (P.skip_q && P.skip_q[q]) return;
-    const int qlen = (int)P.qlen[q];
+// starts; built by mini_table_kernel in hymet_mm_map) instead of a binary search.  Every
+// anchor computes its own mm_reg_set_coor terms and est_err stall candidate -- the
+// minimizer index of itself and of its walk-order predecessor by two pos_tab loads, so no
+// a_idx pass -- then a segmented wave reduction by chain id and one atomic per chain piece
+// in the wave.  c_mlen / c_blen start at 0, c_fv at INT32_MAX (every anchor offers cnt).
+// (One wave per chain spent most of its time on the chain's dependent loads: chains are
+// short and many.)
+__device__ __forceinline__ int32_t mini_idx_at(const AnchorStatParams &P, int64_t q, int qlen, int64_t b) {
     const uint64_t ax = P.bx[b], ay = P.by[b];
     int32_t x = (int32_t)ay;
     if (ax >> 63) x = qlen - 1 - (int32_t)ay + (int32_t)(ay >> 32 & 0xff) - 1;
-    P.a_idx[b] = (x >= 0 && x < qlen) ? P.pos_tab[P.qbase[q] + x] : -1;
+    return (x >= 0 && x < qlen) ? P.pos_tab[P.qbase[q] + x] : -1;
 }
 
-__device__ __forceinline__ int wsum(int v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ int wmin(int v) {
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
-}
-
-// one wave per chain (grid-stride): mm_reg_set_coor's mlen/blen sums, and for mm_est_err the
-// walk-order first/last minimizer index and the first anchor whose index does not increase:
-// est_err's loop `for (k=1, j=st+1; j<nm && k<cnt; ++j) if (idx(k) == j) ++k, ++n_match;`
-// matches anchor k iff idx(1..k) strictly increase from st; the first that does not (or has no
-// minimizer) stalls it to the end
-__global__ __launch_bounds__(64) void chain_stats_kernel(AnchorStatParams P, const int32_t *a_idx, int32_t *c_fv) {
-    const int lane = threadIdx.x;
-    for (int64_t c = blockIdx.x; c < P.NC; c += gridDim.x) {
-        if (P.skip_q && P.skip_q[P.cq[c]]) continue;  // wave-uniform
-        const int32_t cnt = (int32_t)P.cu[c];
+__global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams P, int32_t *c_fv) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool in = b < P.NB;
+    const int32_t c = in ? P.bchain[b] : -1;
+    const int64_t q = in ? (int64_t)P.cq[c] : 0;
+    const bool act = in && !(P.skip_q && P.skip_q[q]);
+    int dm = 0, db = 0, fv = INT32_MAX;
+    if (act) {
         const int64_t o = P.cboff[c];
-        const bool rev = P.bx[o] >> 63;
-        int dm_sum = 0, db_sum = 0, fv = cnt;
-        for (int32_t j0 = 0; j0 < cnt; j0 += 64) {
-            const int32_t j = j0 + lane;
-            if (j >= cnt) continue;
-            const int64_t b = o + j;
-            const uint64_t x = P.bx[b], y = P.by[b];
-            const int32_t span = (int32_t)(y >> 32 & 0xff);
-            if (j == 0) {
-                dm_sum += span, db_sum += span;
-            } else {  // hit.c mm_reg_set_coor
-                const int32_t tl = (int32_t)x - (int32_t)P.bx[b - 1];
-                const int32_t ql = (int32_t)y - (int32_t)P.by[b - 1];
-                db_sum += tl > ql ? tl : ql;
-                dm_sum += tl > span && ql > span ? span : tl < ql ? tl : ql;
-            }
-            const int32_t kk = rev ? cnt - 1 - j : j;  // est_err walking order
-            if (kk >= 1) {
-                const int32_t cur = a_idx[b], prev = a_idx[rev ? b + 1 : b - 1];
-                if (cur < 0 || cur <= prev) fv = min(fv, kk);
-            }
+        const int32_t cnt = (int32_t)P.cu[c], j = (int32_t)(b - o);
+        const int qlen = (int)P.qlen[q];
+        const uint64_t x = P.bx[b], y = P.by[b];
+        const bool rev = x >> 63;
+        const int32_t span = (int32_t)(y >> 32 & 0xff);
+        if (j == 0) {
+            dm = db = span;
+        } else {  // hit.c mm_reg_set_coor
+            const int32_t tl = (int32_t)x - (int32_t)P.bx[b - 1];
+            const int32_t ql = (int32_t)y - (int32_t)P.by[b - 1];
+            db = tl > ql ? tl : ql;
+            dm = tl > span && ql > span ? span : tl < ql ? tl : ql;
         }
-        dm_sum = wsum(dm_sum);
-        db_sum = wsum(db_sum);
-        fv = wmin(fv);
-        if (lane == 0) {
-            P.c_mlen[c] = dm_sum;
-            P.c_blen[c] = db_sum;
-            c_fv[c] = fv;
-            P.c_st[c] = a_idx[rev ? o + cnt - 1 : o];
-            P.c_last[c] = a_idx[rev ? o : o + cnt - 1];
+        const int32_t kk = rev ? cnt - 1 - j : j;  // est_err walking order
+        const int32_t cur = mini_idx_at(P, q, qlen, b);
+        fv = cnt;
+        if (kk >= 1) {
+            const int32_t prev = mini_idx_at(P, q, qlen, rev ? b + 1 : b - 1);
+            if (cur < 0 || cur <= prev) fv = kk;
         }
+        if (kk == 0) P.c_st[c] = cur;
+        if (kk == cnt - 1) P.c_last[c] = cur;
+    }
+    // segmented inclusive reduction over lanes of the same chain (contiguous in the wave)
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int32_t co = __shfl_up(c, d, 64);
+        const int dmo = __shfl_up(dm, d, 64), dbo = __shfl_up(db, d, 64), fvo = __shfl_up(fv, d, 64);
+        if (lane >= d && co == c) dm += dmo, db += dbo, fv = min(fv, fvo);
+    }
+    const int32_t cn = __shfl_down(c, 1, 64);
+    if (act && (lane == 63 || cn != c)) {  // last lane of its chain piece in this wave
+        atomicAdd(P.c_mlen + c, dm);
+        atomicAdd(P.c_blen + c, db);
+        atomicMin(c_fv + c, fv);
     }
 }
 
@@ -349,7 +346,7 @@ __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
         }
         n = k;
     }
-    // ---- mm_est_err (the per-anchor walk was done by chain_stats_kernel)
+    // ---- mm_est_err (the per-anchor walk was done by chain_stats_flat_kernel)
     {
         const int64_t m0 = P.mp_off[q];
         const int32_t nm = (int32_t)(P.mp_off[q + 1] - m0);
@@ -422,22 +419,20 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
                    const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q) {
     if (n_q <= 0) return HYMET_OK;
     hipStream_t st = ctx->stream;
-    DevBuf a_idx, cst, sumk;
-    HY_HIP(a_idx.alloc(4 * (size_t)(NB + 1), st));
+    DevBuf cst, sumk;
     HY_HIP(cst.alloc(4 * 5 * (size_t)(NC + 1), st));
     HY_HIP(sumk.alloc(8 * (size_t)n_q, st));
     int32_t *c_mlen = cst.as<int32_t>(), *c_blen = c_mlen + (NC + 1), *c_st = c_blen + (NC + 1), *c_last = c_st + (NC + 1),
             *c_fv = c_last + (NC + 1);
     {
         ProfScope _ps(ctx, "mm_chain_stats", (double)NB * (16.0 + 16.0 + 8.0) + (double)NM * 8.0);
-        AnchorStatParams A{bx, by, cu, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, bchain, cq, a_idx.as<int32_t>(),
+        AnchorStatParams A{bx, by, cu, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, bchain, cq,
                            c_mlen, c_blen, c_st, c_last, pos_tab, qbase, skip_q};
         if (NB > 0) {
-            hipLaunchKernelGGL(anchor_mini_idx_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A);
-            HY_CHECK_LAUNCH("anchor_mini_idx_kernel");
-            const int64_t nb = NC < (int64_t)ctx->n_cu * 64 ? NC : (int64_t)ctx->n_cu * 64;
-            hipLaunchKernelGGL(chain_stats_kernel, dim3((unsigned)nb), dim3(64), 0, st, A, a_idx.as<int32_t>(), c_fv);
-            HY_CHECK_LAUNCH("chain_stats_kernel");
+            HY_HIP(hipMemsetAsync(c_mlen, 0, 8 * (size_t)(NC + 1), st));  // c_mlen, c_blen
+            HY_HIP(hipMemsetAsync(c_fv, 0x7f, 4 * (size_t)(NC + 1), st));
+            hipLaunchKernelGGL(chain_stats_flat_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A, c_fv);
+            HY_CHECK_LAUNCH("chain_stats_flat_kernel");
         }
         const int nqb = n_q < ctx->n_cu * 64 ? n_q : ctx->n_cu * 64;
         hipLaunchKernelGGL(query_sumk_kernel, dim3((unsigned)nqb), dim3(64), 0, st, mini_pos, mp_off, n_q,
