@@ -2,7 +2,7 @@
 // write_anchor_keys_kernel / rechain_keys_kernel) into (key, y) order -- minimap2's radix
 // sort of a query's anchors by x (map.c collect_seed_hits -> radix_sort_128x), with the
 // canonical full (x, y) tie order T1 -- written out directly as the anchor
-// set (x, y, key), so no unpack pass follows.
+// set (x, y), so no unpack pass follows.
 //
 // The keys arrive query-major (one query's anchors are contiguous), so the global LSD sort
 // over ~47 key bits (six 8-bit passes over 12 B per anchor) is replaced by work local to a
@@ -52,13 +52,13 @@ __device__ __forceinline__ int seg_class(int64_t n) {
          : n <= kTile ? kB4K : kLarge;
 }
 
-// the anchor set written for sorted position i: key (k1), x, y
+// the anchor set written for sorted position i: x, y (groups are read from x and the query
+// offsets, so the sorted key itself is not written)
 struct AnchorOut {
-    uint64_t *key, *ax, *ay;
+    uint64_t *ax, *ay;
     int rb, pb;
     uint64_t yhi;
     __device__ __forceinline__ void put(int64_t i, uint64_t k, uint32_t y) const {
-        key[i] = k;
         const uint64_t rev = k >> (rb + pb) & 1, rid = k >> pb & ((1ull << rb) - 1), rpos = k & ((1ull << pb) - 1);
         ax[i] = rev << 63 | rid << 32 | rpos;
         ay[i] = yhi << 32 | y;
@@ -496,7 +496,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     const int ybits = bits_of(max_qlen);
     if (n <= 0 || n_q <= 0 || 1 + rb + pb + ybits > 63) return 1;
     hipStream_t st = ctx->stream;
-    const AnchorOut out{okey, ax, ay, rb, pb, yhi};
+    const AnchorOut out{ax, ay, rb, pb, yhi};
     // 1 queries by size
     DevBuf qlists, qcnt, nt;
     HY_HIP(qlists.alloc(sizeof(Seg) * kClasses * (size_t)n_q, st));
@@ -509,7 +509,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     int32_t hq[kClasses] = {};
     HY_HIP(hipMemcpyAsync(hq, qcnt.p, 4 * kClasses, hipMemcpyDeviceToHost, st));
     HY_HIP(hipStreamSynchronize(st));
-    ProfScope _ps(ctx, "mm_anchor_gsort", 60.0 * (double)n);  // key+y read, scatter write, sort read, key+x+y write
+    ProfScope _ps(ctx, "mm_anchor_gsort", 52.0 * (double)n);  // key+y read, scatter write, sort read, x+y write
     // 2 small queries: sorted whole
     int rc = sort_segments(ctx, qlists.as<Seg>(), n_q, hq, key, val, 1 + rb + pb, ybits, out);
     if (rc || hq[kLarge] == 0) return rc;

@@ -1346,7 +1346,8 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
         // each walk was 2.6x slower: walks mark the upcoming candidates, so most re-reads
         // failed one round trip at a time.)
         int64_t ptop = -1;  // the block covers z positions (ptop - 64 * kBtProbe, ptop]
-        int32_t zc[kBtProbe], tv[kBtProbe];
+        int32_t zc[kBtProbe], tv[kBtProbe], zfv[kBtProbe];
+        int64_t zpv[kBtProbe];  // f and p of the entries that read unmarked: a walk's start
         bool stale = false;
         while (k >= z0) {
             if (ptop < 0 || k <= ptop - 64 * kBtProbe) {
@@ -1363,6 +1364,11 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                     const int64_t kk = k - 64 * c - lane;
                     tv[c] = kk >= z0 ? ld_l2(P.t + zc[c]) : 1;
                 }
+#pragma unroll
+                for (int c = 0; c < kBtProbe; c++) {  // (f and p are read-only here: never stale)
+                    zfv[c] = tv[c] == 0 ? P.f[zc[c]] : 0;
+                    zpv[c] = tv[c] == 0 ? P.p[zc[c]] : -1;
+                }
             } else if (stale) {  // a walk since the probe: re-read the marks (z indices stay valid)
                 stale = false;
 #pragma unroll
@@ -1373,7 +1379,8 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             }
             const int d = (int)(ptop - k);  // entries above k in the block are done
             int hit = -1;
-            int32_t zsel = 0;
+            int32_t zsel = 0, zfsel = 0;
+            int64_t zpsel = -1;
 #pragma unroll
             for (int c = kBtProbe - 1; c >= 0; c--) {  // the nearest unmarked entry at or below k wins
                 const uint64_t m = __ballot(tv[c] == 0 && 64 * c + lane >= d);
@@ -1381,6 +1388,8 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                     const int h = __ffsll((unsigned long long)m) - 1;
                     hit = 64 * c + h;
                     zsel = __builtin_amdgcn_readlane(zc[c], h);
+                    zfsel = __builtin_amdgcn_readlane(zfv[c], h);
+                    zpsel = rlane64(zpv[c], h);
                 }
             }
             hit = uni(hit);
@@ -1391,13 +1400,13 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             const int64_t zi = (int64_t)uni(zsel);
             k = ptop - hit - 1;
             stale = true;
-            const int32_t zf = uni(P.f[zi]);
+            const int32_t zf = uni(zfsel);
             int64_t *buf = P.chain_ids + wpos;
             buf[0] = zi;  // every lane: same value, same address
             P.t[zi] = 1;  // path nodes are marked as recorded; those past the best end are unmarked after
             int64_t len = 1, nv = 0;  // recorded path nodes; chain = path[0, nv)
             int32_t max_s = 0;
-            int64_t nxt = uni64(P.p[zi]);
+            int64_t nxt = uni64(zpsel);
             int64_t whi = -1;  // window: chunk c, lane l holds anchor whi - 64c - l
             int64_t wpc[kBtChunks];
             int32_t wfc[kBtChunks], wtc[kBtChunks];

@@ -408,14 +408,92 @@ __global__ void anchor_unpack_kernel(const uint64_t *key, const uint32_t *val, i
 }
 
 // group = (query, strand, target): the key without its low `shift` (rpos) bits
-__global__ void group_flag_kernel(const uint64_t *k1, int64_t n, int shift, uint32_t *flag) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) flag[i] = (i == 0 || (k1[i] >> shift) != (k1[i - 1] >> shift)) ? 1u : 0u;
-}
-
 __global__ void group_flag_x_kernel(const uint64_t *x, int64_t n, uint32_t *flag) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) flag[i] = (i == 0 || (x[i] >> 32) != (x[i - 1] >> 32)) ? 1u : 0u;
+}
+
+// Groups of an anchor set sorted by (query, x, y) in two passes over tiles of 4096 anchors
+// (instead of flag, scan and start passes over per-anchor flags): a group starts at every
+// query's first anchor and wherever x >> 32 (strand, target) changes.  Pass 1 counts the
+// starts per tile; after a scan of the tile counts, pass 2 recomputes them and writes g_start
+// and every anchor's group id.  A tile's query starts come from the query offsets into an LDS
+// bitmap.
+constexpr int kGTile = 4096;
+
+__device__ __forceinline__ void group_tile_heads(const uint64_t *x, int64_t n, const int64_t *qoff, int n_q, int64_t t0,
+                                                 uint32_t *qs, uint32_t *rc, bool (&h)[16]) {
+    __shared__ int s_q0;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t t1 = min(t0 + kGTile, n);
+    for (int k = threadIdx.x; k < kGTile / 32; k += 256) qs[k] = 0;
+    if (threadIdx.x == 0) {  // first query whose range ends after t0
+        int lo = 0, hi = n_q;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (qoff[mid + 1] <= t0) lo = mid + 1;
+            else hi = mid;
+        }
+        s_q0 = lo;
+    }
+    __syncthreads();
+    for (int q = s_q0 + (int)threadIdx.x; q < n_q; q += 256) {
+        const int64_t a = qoff[q];
+        if (a >= t1) break;
+        if (a >= t0 && a < qoff[q + 1]) atomicOr(&qs[(a - t0) >> 5], 1u << ((a - t0) & 31));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int64_t i = t0 + j * 256 + threadIdx.x;
+        const int64_t l = i - t0;
+        h[j] = i < n && (i == 0 || (qs[l >> 5] >> (l & 31) & 1) || (x[i] >> 32) != (x[i - 1] >> 32));
+        const uint64_t b = __ballot(h[j]);
+        if (lane == 0) rc[j * 4 + w] = (uint32_t)__popcll(b);
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void group_count_kernel(const uint64_t *x, int64_t n, const int64_t *qoff, int n_q,
+                                                          uint32_t *tile_cnt) {
+    __shared__ uint32_t qs[kGTile / 32], rc[64];
+    bool h[16];
+    group_tile_heads(x, n, qoff, n_q, (int64_t)blockIdx.x * kGTile, qs, rc, h);
+    if (threadIdx.x < 64) {
+        uint32_t v = rc[threadIdx.x];
+        for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+        if (threadIdx.x == 0) tile_cnt[blockIdx.x] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void group_write_kernel(const uint64_t *x, int64_t n, const int64_t *qoff, int n_q,
+                                                          const int64_t *tile_off, int64_t *g_start, int32_t *gid) {
+    __shared__ uint32_t qs[kGTile / 32], rc[64];
+    bool h[16];
+    const int64_t t0 = (int64_t)blockIdx.x * kGTile;
+    group_tile_heads(x, n, qoff, n_q, t0, qs, rc, h);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (w == 0) {  // exclusive scan of the 64 (row, wave) counts in anchor order
+        const uint32_t v = rc[lane];
+        uint32_t inc = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= d) inc += o;
+        }
+        rc[lane] = inc - v;
+    }
+    __syncthreads();
+    const int64_t base = tile_off[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int64_t i = t0 + j * 256 + threadIdx.x;
+        const uint64_t b = __ballot(h[j]);
+        const int64_t g = base + rc[j * 4 + w] + __popcll(b & ((2ull << lane) - 1)) - 1;  // inclusive - 1
+        if (i < n) {
+            gid[i] = (int32_t)g;
+            if (h[j]) g_start[g] = i;
+        }
+    }
 }
 
 __global__ void group_start_kernel(const uint32_t *flag, const int64_t *gpos, int64_t n, int64_t *g_start, int32_t *gid) {
@@ -532,10 +610,12 @@ __global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
         int m = 0, K = 0;  // z entries so far, descents so far (wave-uniform)
         uint64_t last = 0;
         const uint64_t below = (1ull << lane) - 1;
+        int32_t fnx = lane < n ? P.f[g0 + lane] : 0;  // next chunk's f, loaded one chunk ahead
         for (int64_t base = 0; base < n; base += 64) {
             const int64_t i = base + lane;
             const bool ok = i < n;
-            const int32_t fv = ok ? P.f[g0 + i] : 0;
+            const int32_t fv = fnx;
+            fnx = i + 64 < n ? P.f[g0 + i + 64] : 0;
             const bool z = ok && fv >= P.min_sc;
             const uint64_t bal = __ballot(z);
             if (bal == 0) continue;
@@ -815,12 +895,12 @@ __global__ __launch_bounds__(256) void mark_count_kernel(const uint8_t *mark, in
     if (threadIdx.x == 0) cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// stable compaction of the marked anchors (x, y, group key): the first-pass set is sorted by
-// (key, y), so its marked subsequence is the long join's sorted anchor set -- no re-sort.
+// stable compaction of the marked anchors (x, y): the first-pass set is sorted by (query, x,
+// y), so its marked subsequence is the long join's sorted anchor set -- no re-sort.
 // Rows of 256 anchors, lanes striped (coalesced), positions by ballot counts.
 __global__ __launch_bounds__(256) void mark_compact_kernel(const uint8_t *mark, int64_t n, const int64_t *tile_off,
-                                                           const uint64_t *ax, const uint64_t *ay, const uint64_t *k1,
-                                                           uint64_t *ox, uint64_t *oy, uint64_t *ok1) {
+                                                           const uint64_t *ax, const uint64_t *ay, uint64_t *ox,
+                                                           uint64_t *oy) {
     __shared__ uint32_t rc[64];  // marks per (row, wave), row-major
     const int64_t t0 = (int64_t)blockIdx.x * 4096;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -854,7 +934,6 @@ __global__ __launch_bounds__(256) void mark_compact_kernel(const uint8_t *mark, 
             const int64_t o = base + rc[j * 4 + w] + __popcll(b & ((1ull << lane) - 1));
             ox[o] = ax[e];
             oy[o] = ay[e];
-            ok1[o] = k1[e];
         }
     }
 }
@@ -950,8 +1029,7 @@ static int bits_for(int64_t v) {
 
 // An anchor set sorted by (query, x, y): arrays + per-query offsets (device + host).
 struct AnchorSet {
-    DevBuf ax, ay, k1;  // k1 >> gshift = group (query, strand, target)
-    int gshift = 0;
+    DevBuf ax, ay;
     int64_t n = 0;
     std::vector<int64_t> h_off;  // n_q + 1
     DevBuf d_off;
@@ -1000,10 +1078,8 @@ static int sort_anchor_set(hymet_ctx *ctx, DevBuf &x, DevBuf &y, DevBuf &k1, Dev
     if (rc) return rc;
     HY_HIP(out.ax.alloc(8 * (size_t)n, ctx->stream));
     HY_HIP(out.ay.alloc(8 * (size_t)n, ctx->stream));
-    HY_HIP(out.k1.alloc(8 * (size_t)n, ctx->stream));
     LAUNCH1(gather_kernel<uint64_t>, n, x.as<uint64_t>(), vv, out.ax.as<uint64_t>(), n);
     LAUNCH1(gather_kernel<uint64_t>, n, y.as<uint64_t>(), vv, out.ay.as<uint64_t>(), n);
-    HY_HIP(hipMemcpyAsync(out.k1.p, k1p, 8 * (size_t)n, hipMemcpyDeviceToDevice, ctx->stream));
     out.n = n;
     return HYMET_OK;
 }
@@ -1018,7 +1094,6 @@ static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n,
     HY_HIP(vb.alloc(4 * (size_t)n, ctx->stream));
     HY_HIP(out.ax.alloc(8 * (size_t)n, ctx->stream));
     HY_HIP(out.ay.alloc(8 * (size_t)n, ctx->stream));
-    out.gshift = pb;
     out.n = n;
     uint64_t *kk = key.as<uint64_t>(), *kka = kb.as<uint64_t>();
     uint32_t *vv = val.as<uint32_t>(), *vva = vb.as<uint32_t>();
@@ -1029,10 +1104,7 @@ static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n,
     if (gsort) {
         const int rc = grouped_anchor_sort(ctx, kk, vv, n, d_qoff, n_q, rb, pb, (uint64_t)yhi, max_qlen, kka, vva,
                                            out.ax.as<uint64_t>(), out.ay.as<uint64_t>());
-        if (rc == HYMET_OK) {
-            out.k1.swap(kb);
-            return HYMET_OK;
-        }
+        if (rc == HYMET_OK) return HYMET_OK;
         if (rc != 1) return rc;
     }
     int rc = sort_pairs<uint64_t, uint32_t, HYMET_ANCHOR_RB>(ctx, kk, kka, vv, vva, n, 0, end_bit, "radix_sort_anchors");
@@ -1041,8 +1113,6 @@ static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n,
         ProfScope _ps(ctx, "mm_anchor_unpack", 28.0 * (double)n);  // key + value read, x + y write
         LAUNCH1(anchor_unpack_kernel, n, kk, vv, n, rb, pb, (uint64_t)yhi, out.ax.as<uint64_t>(), out.ay.as<uint64_t>());
     }
-    if (kk == kb.as<uint64_t>()) out.k1.swap(kb);
-    else out.k1.swap(key);
     return HYMET_OK;
 }
 
@@ -1059,17 +1129,23 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(hipMemsetAsync(C.d_qb.p, 0, 8 * (size_t)(n_q + 1), ctx->stream));
         return HYMET_OK;
     }
-    // groups
-    DevBuf flag, gpos, gid;
-    HY_HIP(flag.alloc(4 * (size_t)n, ctx->stream));
-    LAUNCH1(group_flag_kernel, n, A.k1.as<uint64_t>(), n, A.gshift, flag.as<uint32_t>());
+    // groups: (query, strand, target) runs, by tiles (count, scan of the tile counts, write)
+    DevBuf tcnt, toff, gid;
+    const int64_t ntile = cdiv(n, kGTile);
+    HY_HIP(tcnt.alloc(4 * (size_t)(ntile + 1), ctx->stream));
+    HY_HIP(toff.alloc(8 * (size_t)(ntile + 1), ctx->stream));
+    hipLaunchKernelGGL(group_count_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.ax.as<uint64_t>(), n,
+                       A.d_off.as<int64_t>(), n_q, tcnt.as<uint32_t>());
+    HY_CHECK_LAUNCH("group_count_kernel");
     int64_t G = 0;
-    int rc = scan_flags(ctx, flag.as<uint32_t>(), n, gpos, &G);
+    int rc = exclusive_scan_u32_i64(ctx, tcnt.as<uint32_t>(), toff.as<int64_t>(), ntile, &G);
     if (rc) return rc;
     DevBuf g_start;
     HY_HIP(g_start.alloc(8 * (size_t)(G + 1), ctx->stream));
     HY_HIP(gid.alloc(4 * (size_t)n, ctx->stream));
-    LAUNCH1(group_start_kernel, n, flag.as<uint32_t>(), gpos.as<int64_t>(), n, g_start.as<int64_t>(), gid.as<int32_t>());
+    hipLaunchKernelGGL(group_write_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.ax.as<uint64_t>(), n,
+                       A.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), g_start.as<int64_t>(), gid.as<int32_t>());
+    HY_CHECK_LAUNCH("group_write_kernel");
     HY_HIP(hipMemcpyAsync(g_start.as<int64_t>() + G, &n, 8, hipMemcpyHostToDevice, ctx->stream));
     // work list: groups with >= min_cnt anchors, biggest first
     DevBuf skey, sidx, swork, skey2, sidx2, gmax;
@@ -1671,15 +1747,19 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
         if (!path || dumped || S.n == 0) return HYMET_OK;
         dumped = true;
         const int64_t nd = std::min<int64_t>(S.n, 1 << 24);
-        std::vector<uint64_t> hx(nd), hy(nd), hk(nd);
+        std::vector<uint64_t> hx(nd), hy(nd);
+        std::vector<int64_t> qo(n_q + 1);
         HY_HIP(hipMemcpyAsync(hx.data(), S.ax.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
         HY_HIP(hipMemcpyAsync(hy.data(), S.ay.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
-        HY_HIP(hipMemcpyAsync(hk.data(), S.k1.p, 8 * (size_t)nd, hipMemcpyDeviceToHost, st));
+        HY_HIP(hipMemcpyAsync(qo.data(), S.d_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, st));
         HY_HIP(hipStreamSynchronize(st));
         if (FILE *fp = fopen(path, "wb")) {
             uint64_t gid = 0;
+            int q = 0;
             for (int64_t a = 0; a < nd; a++) {
-                if (a && (hk[a] >> S.gshift) != (hk[a - 1] >> S.gshift)) gid++;
+                bool qs = false;  // a query's first anchor
+                while (q < n_q && qo[q + 1] <= a) q++, qs = true;
+                if (a && (qs || (hx[a] >> 32) != (hx[a - 1] >> 32))) gid++;
                 const uint64_t v[2] = {gid << 32 | (uint32_t)hx[a], hy[a]};
                 fwrite(v, 8, 2, fp);
             }
@@ -1734,12 +1814,10 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                 if (got != A2 || got != lj.n2) return hymet::fail(HYMET_E_INTERNAL, "hymet_mm_map: long-join anchor count mismatch");
                 HY_HIP(S2.ax.alloc(8 * (size_t)(A2 + 1), st));
                 HY_HIP(S2.ay.alloc(8 * (size_t)(A2 + 1), st));
-                HY_HIP(S2.k1.alloc(8 * (size_t)(A2 + 1), st));
                 hipLaunchKernelGGL(mark_compact_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<uint8_t>(), n1,
-                                   toff.as<int64_t>(), S1.ax.as<uint64_t>(), S1.ay.as<uint64_t>(), S1.k1.as<uint64_t>(),
-                                   S2.ax.as<uint64_t>(), S2.ay.as<uint64_t>(), S2.k1.as<uint64_t>());
+                                   toff.as<int64_t>(), S1.ax.as<uint64_t>(), S1.ay.as<uint64_t>(), S2.ax.as<uint64_t>(),
+                                   S2.ay.as<uint64_t>());
                 HY_CHECK_LAUNCH("mark_compact_kernel");
-                S2.gshift = S1.gshift;
                 S2.n = A2;
                 rc = dump_anchors(getenv("HYMET_DUMP_ANCHORS2"), S2, dumped2);
                 if (rc) return rc;
