@@ -86,6 +86,8 @@ struct SketchParams {
     const int64_t *out_off;    // per chunk (write pass)
     uint64_t *out_x;
     uint64_t *out_y;
+    int slot_cap;              // > 0: one-pass mode -- chunk g writes at g * slot_cap and its count
+    uint32_t *overflow;        // one-pass mode: set when a chunk exceeds slot_cap
 };
 
 // Count (WRITE=false) or emit (WRITE=true) the minimizers of every chunk; defined in

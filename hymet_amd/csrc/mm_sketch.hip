@@ -10,7 +10,9 @@
 // outputs are bit-identical to mm_sketch, push order included.  The
 // window lives in registers as a shift register (W compile-time), so the oldest slot is
 // index 0 and "the minimum left the window" is min_step == step - W.
-// Two launches: count (WRITE=false) -> exclusive scan -> write (WRITE=true).
+// Two launches: count (WRITE=false) -> exclusive scan -> write (WRITE=true); or, for query
+// batches, one write launch into fixed per-chunk slots (slot_cap entries, counted on the
+// way) -> scan of the counts -> a compaction copy (the winnowing replay runs once).
 //
 // Index: minimizer (hash = x>>8, y) pairs are sorted by (hash, y) with two stable rocPRIM
 // radix passes and laid out as a CSR over ALL 4^k hash values (k <= 15: 2^30+1 uint32
@@ -19,6 +21,7 @@
 #include "mm_common.hpp"
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace hymet {
@@ -53,10 +56,11 @@ __global__ __launch_bounds__(256) void mm_sketch_kernel(SketchParams P) {
     uint64_t minx = kMax64, miny = kMax64;
     int64_t step = 0, min_step = -W;
     uint32_t cnt = 0;
-    const int64_t out0 = WRITE ? P.out_off[g] : 0;
+    const int64_t out0 = WRITE ? (P.slot_cap ? g * P.slot_cap : P.out_off[g]) : 0;
+    const uint32_t lim = P.slot_cap ? (uint32_t)P.slot_cap : 0xffffffffu;
     uint32_t cw = 0, mw = 0;
     auto push = [&](uint64_t x, uint64_t y) {
-        if (WRITE) {
+        if (WRITE && cnt < lim) {
             P.out_x[out0 + cnt] = x;
             P.out_y[out0 + cnt] = y;
         }
@@ -122,7 +126,19 @@ __global__ __launch_bounds__(256) void mm_sketch_kernel(SketchParams P) {
         ++step;
     }
     if (cen == L && minx != kMax64) push(minx, miny);
-    if (!WRITE) P.counts[g] = cnt;
+    if (!WRITE || P.slot_cap) P.counts[g] = cnt;
+    if (WRITE && P.slot_cap && cnt > lim) atomicOr(P.overflow, 1u);
+}
+
+// one-pass mode: chunk g's slot entries to its place in the packed output
+__global__ __launch_bounds__(64) void sketch_compact_kernel(const uint64_t *sx, const uint64_t *sy, const uint32_t *cnt,
+                                                            const int64_t *off, int slot_cap, uint64_t *ox, uint64_t *oy) {
+    const int64_t g = blockIdx.x;
+    const int64_t s0 = g * slot_cap, o = off[g];
+    for (uint32_t j = threadIdx.x; j < cnt[g]; j += 64) {
+        ox[o + j] = sx[s0 + j];
+        oy[o + j] = sy[s0 + j];
+    }
 }
 
 __global__ void bucket_hist_kernel(const uint64_t *__restrict__ x, int64_t n, uint32_t *__restrict__ cnt,
@@ -193,18 +209,53 @@ int sketch_sequences(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mas
     P.warm = w + k + 16;
     P.rid_mode = rid_mode;
     P.counts = d_cnt.as<uint32_t>();
-    int rc = launch_sketch(ctx, w, false, P);
-    if (rc) return rc;
     int64_t total = 0;
-    rc = exclusive_scan_u32_i64(ctx, d_cnt.as<uint32_t>(), d_off.as<int64_t>(), n_chunks, &total);
-    if (rc) return rc;
-    HY_HIP(d_x.alloc(8 * (size_t)total, ctx->stream));
-    HY_HIP(d_y.alloc(8 * (size_t)total, ctx->stream));
-    P.out_off = d_off.as<int64_t>();
-    P.out_x = d_x.as<uint64_t>();
-    P.out_y = d_y.as<uint64_t>();
-    rc = launch_sketch(ctx, w, true, P);
-    if (rc) return rc;
+    int rc = HYMET_OK;
+    // one pass into per-chunk slots when they fit a modest scratch (query batches; the index
+    // build's gigabases take the two-pass path).  A chunk pushes each window minimum once, so
+    // it holds at most its 512 positions plus the warm-up window's: slot_cap never overflows
+    // in practice, and an overflow falls back to the two passes.
+    constexpr int kSlotCap = kChunk + 64;
+    bool done = false;
+    if (n_chunks > 0 && (double)n_chunks * kSlotCap * 16.0 <= 2.0e9 && !getenv("HYMET_SKETCH_TWO_PASS")) {
+        DevBuf sx, sy;
+        HY_HIP(sx.alloc(8 * (size_t)n_chunks * kSlotCap, ctx->stream));
+        HY_HIP(sy.alloc(8 * (size_t)n_chunks * kSlotCap, ctx->stream));
+        HY_HIP(hipMemsetAsync(d_cnt.as<uint32_t>() + n_chunks, 0, 4, ctx->stream));
+        SketchParams Q = P;
+        Q.slot_cap = kSlotCap;
+        Q.overflow = d_cnt.as<uint32_t>() + n_chunks;
+        Q.out_x = sx.as<uint64_t>();
+        Q.out_y = sy.as<uint64_t>();
+        rc = launch_sketch(ctx, w, true, Q);
+        if (rc) return rc;
+        uint32_t ovf = 0;
+        HY_HIP(hipMemcpyAsync(&ovf, Q.overflow, 4, hipMemcpyDeviceToHost, ctx->stream));
+        rc = exclusive_scan_u32_i64(ctx, d_cnt.as<uint32_t>(), d_off.as<int64_t>(), n_chunks, &total);
+        if (rc) return rc;
+        if (!ovf) {
+            HY_HIP(d_x.alloc(8 * (size_t)total, ctx->stream));
+            HY_HIP(d_y.alloc(8 * (size_t)total, ctx->stream));
+            hipLaunchKernelGGL(sketch_compact_kernel, dim3((unsigned)n_chunks), dim3(64), 0, ctx->stream, sx.as<uint64_t>(),
+                               sy.as<uint64_t>(), d_cnt.as<uint32_t>(), d_off.as<int64_t>(), kSlotCap, d_x.as<uint64_t>(),
+                               d_y.as<uint64_t>());
+            HY_CHECK_LAUNCH("sketch_compact_kernel");
+            done = true;
+        }
+    }
+    if (!done) {
+        rc = launch_sketch(ctx, w, false, P);
+        if (rc) return rc;
+        rc = exclusive_scan_u32_i64(ctx, d_cnt.as<uint32_t>(), d_off.as<int64_t>(), n_chunks, &total);
+        if (rc) return rc;
+        HY_HIP(d_x.alloc(8 * (size_t)total, ctx->stream));
+        HY_HIP(d_y.alloc(8 * (size_t)total, ctx->stream));
+        P.out_off = d_off.as<int64_t>();
+        P.out_x = d_x.as<uint64_t>();
+        P.out_y = d_y.as<uint64_t>();
+        rc = launch_sketch(ctx, w, true, P);
+        if (rc) return rc;
+    }
     if (d_seq_off) {
         // per-sequence offsets = chunk offsets sampled at each sequence's first chunk
         std::vector<int64_t> so(n_seq + 1);
