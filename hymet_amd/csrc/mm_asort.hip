@@ -209,27 +209,85 @@ __global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const
     }
 }
 
+// The scatter of a large query's tile to its (tile, bin) runs.  Consecutive anchors of a tile
+// fall into many bins (one minimizer hits every strain of the taxon), so writing each anchor
+// straight to its run position scattered 12-byte writes over as many cache lines; instead each
+// round of kSub anchors is ranked by bin in LDS (wave-aggregated atomics), its bin counts are
+// scanned, the round is laid out bin by bin in LDS, and written run by run (consecutive lanes,
+// consecutive addresses).  56 KB of LDS per block.
+constexpr int kSub = 2048;
+
 __global__ __launch_bounds__(256) void tile_scatter_kernel(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
                                                            const int64_t *__restrict__ tile_a0, const int32_t *__restrict__ tile_q,
                                                            const int32_t *__restrict__ tile_n, const int64_t *__restrict__ qoff,
                                                            int pb, int nbins, const uint32_t *__restrict__ H,
                                                            uint64_t *__restrict__ okey, uint32_t *__restrict__ oval) {
-    __shared__ uint32_t c[kMaxBins];
+    __shared__ uint32_t c[kMaxBins];       // run position of every bin for the next round
+    __shared__ uint32_t lo[kMaxBins];      // round: bin counts, then their exclusive offsets
+    __shared__ uint64_t sk[kSub];
+    __shared__ uint32_t sv[kSub];
+    __shared__ uint32_t wsum[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t a0 = tile_a0[blockIdx.x];
     const int n = tile_n[blockIdx.x];
     const uint32_t *row = H + (int64_t)blockIdx.x * nbins;
-    for (int b = threadIdx.x; b < nbins; b += 256) c[b] = row[b];
-    __syncthreads();
+    for (int b = tid; b < nbins; b += 256) c[b] = row[b];
     const int64_t base = qoff[tile_q[blockIdx.x]];
-    for (int e0 = 0; e0 < n; e0 += 256) {
-        const int e = e0 + threadIdx.x;
-        const bool act = e < n;
-        const uint64_t k = act ? key[a0 + e] : 0;
-        const int64_t pos = base + lds_rank(c, (int)((k >> pb) & (nbins - 1)), act);
-        if (act) {
-            okey[pos] = k;
-            oval[pos] = val[a0 + e];
+    const int per = (nbins + 255) / 256, b0 = min(tid * per, nbins), b1 = min(b0 + per, nbins);
+    for (int r0 = 0; r0 < n; r0 += kSub) {
+        const int m = min(kSub, n - r0);
+        for (int b = tid; b < nbins; b += 256) lo[b] = 0;
+        __syncthreads();
+        uint64_t kk[kSub / 256];
+        uint32_t vv[kSub / 256], rk[kSub / 256];
+        int bn[kSub / 256];
+#pragma unroll
+        for (int j = 0; j < kSub / 256; j++) {  // every lane runs the loop (wave-level ballots inside)
+            const int e = j * 256 + tid;
+            const bool act = e < m;
+            kk[j] = act ? key[a0 + r0 + e] : 0;
+            vv[j] = act ? val[a0 + r0 + e] : 0;
+            bn[j] = (int)((kk[j] >> pb) & (uint64_t)(nbins - 1));
+            rk[j] = lds_rank(lo, bn[j], act);
         }
+        __syncthreads();
+        {  // exclusive scan of the bin counts: per-thread spans, then a block scan of span sums
+            uint32_t sum = 0;
+            for (int b = b0; b < b1; b++) sum += lo[b];
+            uint32_t inc = sum;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+                if (lane >= d) inc += o;
+            }
+            if (lane == 63) wsum[w] = inc;
+            __syncthreads();
+            uint32_t ex = inc - sum;
+            for (int k = 0; k < w; k++) ex += wsum[k];
+            for (int b = b0; b < b1; b++) {
+                const uint32_t t = lo[b];
+                lo[b] = ex;
+                ex += t;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kSub / 256; j++)
+            if (j * 256 + tid < m) {
+                const uint32_t slot = lo[bn[j]] + rk[j];
+                sk[slot] = kk[j];
+                sv[slot] = vv[j];
+            }
+        __syncthreads();
+        for (int s = tid; s < m; s += 256) {
+            const uint64_t k = sk[s];
+            const int b = (int)((k >> pb) & (uint64_t)(nbins - 1));
+            const int64_t pos = base + c[b] + (s - lo[b]);
+            okey[pos] = k;
+            oval[pos] = sv[s];
+        }
+        __syncthreads();
+        for (int b = tid; b < nbins; b += 256) c[b] += (b + 1 < nbins ? lo[b + 1] : (uint32_t)m) - lo[b];
+        __syncthreads();
     }
 }
 
