@@ -573,7 +573,8 @@ struct ZParams {
     int32_t *z_cnt;        // per group: number of z entries
     int32_t *z_runs;       // per group: ascending runs (0 when empty)
     int32_t *run_start;    // per group, kZRuns entries: run starts relative to g_start
-    int32_t *lists;        // [0] split, [1] mid count, [2] big count, [4..5] big total (i64, 8-byte aligned)
+    int32_t *lists;        // [0] split, [1] mid count, [2] big count, [3] merge count, [4..5] big total (i64)
+    int32_t *merge_list;   // groups of 2..max_runs runs, for the merge
     int32_t *mid_list;     // groups for the block sort
     int32_t *big_list;     // groups for the radix path
     int64_t *big_off;      // their offsets in the radix arrays
@@ -644,6 +645,7 @@ __global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
             rs[0] = 0;
             P.z_cnt[g] = m;
             P.z_runs[g] = runs;
+            if (runs > 1 && runs <= P.max_runs) P.merge_list[atomicAdd(P.lists + 3, 1)] = g;
             if (runs > P.max_runs) {
                 if (m <= kZs) {
                     P.mid_list[atomicAdd(P.lists + 1, 1)] = g;
@@ -684,35 +686,37 @@ __global__ __launch_bounds__(256) void zorder_lane_kernel(ZParams P) {
     P.z_runs[g] = m > 0 ? 1 : 0;  // complete
 }
 
-// groups of 2..max_runs ascending runs: merge by ranks (flat over the anchor positions)
-__global__ void zmerge_kernel(ZParams P, const int32_t *gid, int64_t n) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const int g = gid[p];
-    const int K = P.z_runs[g];
-    if (K <= 1 || K > P.max_runs) return;
-    const int64_t z0 = P.g_start[g];
-    const int q = (int)(p - z0), m = P.z_cnt[g];
-    if (q >= m) return;
-    const int32_t *rs = P.run_start + (int64_t)g * kZRuns;
-    const uint64_t *zk = P.zkey + z0;
-    const uint64_t key = zk[q];
-    int pos = 0;
-    for (int k = 0; k < K; k++) {
-        const int s0 = rs[k], s1 = k + 1 < K ? rs[k + 1] : m;
-        if (q >= s0 && q < s1) {  // own run
-            pos += q - s0;
-            continue;
+// groups of 2..max_runs ascending runs: merge by ranks, one block per listed group (grid-stride
+// over the list; a flat pass over every anchor position read each one's group first)
+__global__ __launch_bounds__(256) void zmerge_kernel(ZParams P) {
+    const int n_list = P.lists[3];
+    for (int w = blockIdx.x; w < n_list; w += gridDim.x) {
+        const int g = P.merge_list[w];
+        const int K = P.z_runs[g];
+        const int64_t z0 = P.g_start[g];
+        const int m = P.z_cnt[g];
+        const int32_t *rs = P.run_start + (int64_t)g * kZRuns;
+        const uint64_t *zk = P.zkey + z0;
+        for (int q = threadIdx.x; q < m; q += blockDim.x) {
+            const uint64_t key = zk[q];
+            int pos = 0;
+            for (int k = 0; k < K; k++) {
+                const int s0 = rs[k], s1 = k + 1 < K ? rs[k + 1] : m;
+                if (q >= s0 && q < s1) {  // own run
+                    pos += q - s0;
+                    continue;
+                }
+                int lo = s0, hi = s1;  // first entry >= key
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (zk[mid] < key) lo = mid + 1;
+                    else hi = mid;
+                }
+                pos += lo - s0;
+            }
+            P.z_idx[z0 + pos] = (int32_t)(uint32_t)key;
         }
-        int lo = s0, hi = s1;  // first entry >= key
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (zk[mid] < key) lo = mid + 1;
-            else hi = mid;
-        }
-        pos += lo - s0;
     }
-    P.z_idx[z0 + pos] = (int32_t)(uint32_t)key;
 }
 
 // one block per listed group of <= kZs z entries (grid-stride over the list)
@@ -1194,13 +1198,14 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
                           opt->rmq_inner_dist, bw, opt->max_chain_skip, opt->rmq_size_cap, pen_gap, pen_skip, n, G);
         if (rc) return rc;
         // z = anchors with f >= min_sc ordered by (group, f, idx), inside each group's range
-        DevBuf zkey, zidx, z_cnt, z_runs, run_start, zlists, mid_list, big_list, big_off;
+        DevBuf zkey, zidx, z_cnt, z_runs, run_start, zlists, merge_list, mid_list, big_list, big_off;
         HY_HIP(zkey.alloc(8 * (size_t)n, ctx->stream));
         HY_HIP(zidx.alloc(4 * (size_t)n, ctx->stream));
         HY_HIP(z_cnt.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(z_runs.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(run_start.alloc(4 * (size_t)G * kZRuns, ctx->stream));
         HY_HIP(zlists.alloc(32, ctx->stream));
+        HY_HIP(merge_list.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(mid_list.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(big_list.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(big_off.alloc(8 * (size_t)G, ctx->stream));
@@ -1213,7 +1218,7 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
             const int max_runs = ev ? std::max(1, std::min(kZRuns, atoi(ev))) : kZRuns;
             ZParams Z{f.as<int32_t>(), g_start.as<int64_t>(), (const int32_t *)vp, (int32_t)G, opt->min_chain_score,
                       max_runs, zkey.as<uint64_t>(), zidx.as<int32_t>(), z_cnt.as<int32_t>(), z_runs.as<int32_t>(),
-                      run_start.as<int32_t>(), zlists.as<int32_t>(), mid_list.as<int32_t>(), big_list.as<int32_t>(),
+                      run_start.as<int32_t>(), zlists.as<int32_t>(), merge_list.as<int32_t>(), mid_list.as<int32_t>(), big_list.as<int32_t>(),
                       big_off.as<int64_t>()};
             hipLaunchKernelGGL(zsplit_kernel, dim3(1), dim3(64), 0, ctx->stream, Z);
             HY_CHECK_LAUNCH("zsplit_kernel");
@@ -1221,8 +1226,9 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
             hipLaunchKernelGGL(zorder_wave_kernel, dim3((unsigned)std::max<int64_t>(nwb, 1)), dim3(256), 0, ctx->stream, Z);
             HY_CHECK_LAUNCH("zorder_wave_kernel");
             LAUNCH1(zorder_lane_kernel, G, Z);
-            LAUNCH1(zmerge_kernel, n, Z, (const int32_t *)gid.as<int32_t>(), n);
             const int64_t nb = std::min<int64_t>(G, (int64_t)ctx->n_cu * 8);
+            hipLaunchKernelGGL(zmerge_kernel, dim3((unsigned)nb), dim3(256), 0, ctx->stream, Z);
+            HY_CHECK_LAUNCH("zmerge_kernel");
             hipLaunchKernelGGL(zsort_block_kernel, dim3((unsigned)nb), dim3(256), 0, ctx->stream, Z);
             HY_CHECK_LAUNCH("zsort_block_kernel");
             int32_t hl[8];
