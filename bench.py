@@ -200,6 +200,9 @@ def bench_cami(args, comm, gpu, torch):
         if comm.rank == 0:
             with open(tsv_path, "wb") as f:             # classified_sequences.tsv written
                 f.write(res.tsv)
+    if comm.rank == 0 and args.tsv_out:
+        with open(args.tsv_out, "wb") as f:
+            f.write(res.tsv)
     torch.cuda.synchronize()
     if prof_host:
         import io
@@ -228,6 +231,8 @@ def bench_cami(args, comm, gpu, torch):
                                f"{refs_ss.total_bases/1e9:.2f} Gbp in {len(ix.parts)} -I2g parts; sketch DBs "
                                + " + ".join(f"{d.n_refs} refs" for d in pipe.dbs) + " x 1000",
                    "global_contigs": n_contigs, "parallelism": f"contig-shard x{comm.world}",
+                   "backend": (("nccl (RCCL over xGMI)" if comm.dist.get_backend() == "nccl" else comm.dist.get_backend())
+                               if comm.dist is not None else "none (1 rank)"),
                    "window": "FASTA bytes in host memory -> classified_sequences.tsv written + resultados.paf text in host "
                              "memory (ingest, H2D, screen, select, limit, map, LCA, text emit inside every step)"},
         "cold_run_s": cold,
@@ -238,7 +243,7 @@ def bench_cami(args, comm, gpu, torch):
         "roofline": roofline_from_prof(prof),
         "path_roofline": path_roofline(prof, args.steps, step, total_bases, total_bases, n_lines, len(ix.parts), comm.world),
     }
-    if comm.rank == 0 and not args.no_cpu:
+    if comm.rank == 0 and comm.world == 1 and not args.no_cpu:   # the CPU leg runs at N=1 only
         try:
             out["cpu_baseline"] = cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier)
         except Exception as e:  # the baseline is informative; never lose the GPU line
@@ -393,6 +398,62 @@ def bench_screen(args, comm, gpu, torch):
             "roofline": roofline_from_prof(prof, "screen_count")}
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the environment):
+    start N rank processes of this same command line, one per GPU, with the environment
+    torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR /
+    MASTER_PORT on 127.0.0.1), and return the first non-zero exit status.  This runs before
+    anything touches the GPU (the parent never initialises HIP) and starts children rather
+    than exec'ing into them."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            r = p.wait()
+            if r != 0 and rc == 0:
+                rc = r
+                for q in procs:          # one rank failed: the others would wait in a collective
+                    if q.poll() is None:
+                        q.send_signal(signal.SIGTERM)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    return rc
+
+
+def bench_dry(args, comm):
+    """CPU rehearsal of the multi-rank launch (no GPU, gloo): every rank builds the same
+    synthetic FASTA, takes its record shard exactly as Pipeline.ingest does
+    (FastaIndex.shard), and the ranks all-reduce their contig and base counts; rank 0
+    reports the world and checks the shards cover the input once."""
+    import torch
+    from hymet_amd import ingest, synth
+    from hymet_amd.ingest import FastaIndex
+    w = synth.make_cami(np.random.default_rng(1234), n_taxa=2, per_taxon=2, genome_mbp=(0.2, 0.3),
+                        contig_gbp=0.002, contig_rng=np.random.default_rng(5000), max_contigs=400)
+    fx = FastaIndex(ingest.to_fasta(list(w.contig_names), w.contigs))
+    r0, r1 = fx.shard(comm.rank, comm.world)
+    t = torch.tensor([r1 - r0, int(sum(len(w.contigs[i]) for i in range(r0, r1)))], dtype=torch.int64)
+    comm.allreduce_sum_(t)
+    spans = comm.allgather_np(np.array([r0, r1], np.int64))
+    ok = int(t[0]) == fx.n and int(t[1]) == w.contig_bases and all(int(a[1]) == int(b[0]) for a, b in zip(spans, spans[1:]))
+    return {"metric": METRIC, "value": None, "unit": "contigs/s", "n_gpus": comm.world, "dry_run": True,
+            "backend": comm.dist.get_backend() if comm.dist is not None else None, "shards": [[int(a[0]), int(a[1])] for a in spans],
+            "contigs": int(t[0]), "bases": int(t[1]), "covers_input_once": bool(ok)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -411,7 +472,15 @@ def main():
     ap.add_argument("--cand-max", type=int, default=5000, help="CAND_MAX (run_hymet_cami.sh:26)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16, help="CPU baseline threads (the GPU box's CPU share is 16)")
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="process-group backend for N > 1 (auto: nccl = RCCL over xGMI)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rank r uses GPU r %% device_count (rehearse N ranks on fewer GPUs; use with --backend gloo)")
+    ap.add_argument("--dry-run", action="store_true", help="CPU rehearsal of the N-rank launch and sharding (gloo, no GPU)")
+    ap.add_argument("--tsv-out", default=None, help="rank 0 writes the last step's classified_sequences.tsv here")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     # CAMI-high (C5, BASELINE.json configs[4]): 14 taxa (tools/generate_cami_subsets.py:343),
     # the full CAND_MAX of 5000 candidates (~20 Gbp, ten -I2g parts), ~2 Gbp of contigs,
     # three sketch DBs of 1e8 / 5e7 / 1e7 hashes
@@ -428,12 +497,24 @@ def main():
         # C4: 60 Mbp batches measured 2327 ms/step vs 2460 (30) and ~2390 (40); scratch 148 GB
         args.batch_mbp = args.batch_mbp or 60.0
         args.workload_name = "CAMI-medium (C4)"
-    import torch
-    from hymet_amd._lib import Gpu
     from hymet_amd.dist import Comm
     comm = Comm.from_env()
-    gpu = Gpu(int(os.environ.get("LOCAL_RANK", "0")))
-    comm.init_backend(gpu)
+    if comm.world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the launcher started {comm.world} rank(s)")
+    if args.dry_run:
+        comm.init_backend(None, "gloo")
+        res = bench_dry(args, comm)
+        if comm.rank == 0:
+            print(json.dumps(res), flush=True)
+        comm.close()
+        return
+    import torch
+    from hymet_amd._lib import Gpu
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.share_gpu:
+        local %= max(1, torch.cuda.device_count())
+    gpu = Gpu(local)
+    comm.init_backend(gpu, None if args.backend == "auto" else args.backend)
     res = bench_screen(args, comm, gpu, torch) if args.workload == "screen" else bench_cami(args, comm, gpu, torch)
     if comm.rank == 0:
         print(json.dumps(res), flush=True)

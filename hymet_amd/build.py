@@ -67,7 +67,10 @@ def build(verbose=False, jobs=8, extra=(), out=OUT, obj=OBJ):
         with open(o + ".sig", "w") as f:
             f.write(sig + "\n")
     lib_sig = hashlib.sha256(("\n".join(sigs) + "\0" + " ".join(LINK)).encode()).hexdigest()
-    if not os.path.exists(out) or _read(out + ".sig") != lib_sig:
+    # relink whenever an object was just compiled: the library's signature file alone is not
+    # trusted in place of the binary (a shipped .so with a matching .sig beside freshly
+    # compiled objects is relinked from those objects)
+    if procs or not os.path.exists(out) or _read(out + ".sig") != lib_sig:
         subprocess.check_call([*LINK, "-o", out, *objs])
         with open(out + ".sig", "w") as f:
             f.write(lib_sig + "\n")

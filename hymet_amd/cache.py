@@ -6,21 +6,23 @@ rest of HYMET consumes (`run_hymet_cami.sh:135-164`):
 * `detailed_taxonomy.tsv` -- one row per downloaded genome: GCF, TaxID (from the NCBI
   assembly summaries, "Unknown TaxID" when absent) and the genome's FASTA identifiers joined
   by ';' (`downloadDB.py:178-207`);
-* `combined_genomes.fasta` -- the downloaded genome files concatenated byte for byte
-  (`downloadDB.py:209-222`).
+* `combined_genomes.fasta` -- the downloaded genome files concatenated
+  (`downloadDB.py:209-222`), read and written in text mode, so CRLF and lone CR line ends
+  become LF (Python's universal newlines); other bytes are copied unchanged.
 
 This module builds both from files already on disk (no network: a genome that is not in
 the genome directory counts as a failed download).  Order: the reference iterates Python
 sets and `os.listdir`, so its row, identifier and genome orders vary between runs; here
 they are fixed -- .fna files in sorted name order, identifiers in first-appearance order,
 genomes in the selection file's order.  Parity with the reference is defined modulo those
-orders (tests/test_cache.py against fixtures the reference's own class wrote).
+orders.  The builder is unpinned: running the reference's class to write fixtures was refused
+(DESIGN.md §4), so tests/test_cache.py checks expectations derived by hand from
+`downloadDB.py:78-222`.
 """
 from __future__ import annotations
 
 import csv
 import os
-import shutil
 from typing import Dict, Iterable, List, Optional, Tuple
 
 UNKNOWN_TAXID = "Unknown TaxID"
@@ -72,17 +74,21 @@ def read_selection(genomes_file: str) -> List[str]:
 def resolve_downloads(gcfs: Iterable[str], assembly: Dict[str, dict], genome_dir: str) -> Tuple[List[str], List[str]]:
     """The reference's download step without the network (`downloadDB.py:113-142`): a GCF with
     summary metadata whose file is already in `genome_dir` succeeds, every other one fails.
-    Returns (file names in selection order, failed GCFs)."""
+    Returns (file names in selection order, failed GCFs).  The reference collects failures in
+    a set (`failed_downloads.add`, :124,127), so a GCF listed twice counts once; first-seen
+    order is kept here."""
     ok: List[str] = []
     failed: List[str] = []
     seen = set()
+    seen_failed = set()
     for gcf in gcfs:
         meta = assembly.get(gcf)
         if meta and os.path.exists(os.path.join(genome_dir, meta["file_name"])):
             if meta["file_name"] not in seen:
                 seen.add(meta["file_name"])
                 ok.append(meta["file_name"])
-        else:
+        elif gcf not in seen_failed:
+            seen_failed.add(gcf)
             failed.append(gcf)
     return ok, failed
 
@@ -121,18 +127,32 @@ def write_detailed_taxonomy(path: str, rows: Iterable[Tuple[str, str, str]]) -> 
 
 
 def concatenate_genomes(genome_dir: str, file_names: Iterable[str], output_file: str) -> List[str]:
-    """`downloadDB.py:209-222`: the files appended byte for byte; a missing file is skipped.
-    Returns the names actually written."""
+    """`downloadDB.py:209-222`: the files appended in order; a missing file is skipped.
+    The reference copies through text-mode file objects, so line ends are normalised to LF
+    (CRLF and lone CR, as universal newlines read them); the copy streams 16 MiB chunks and
+    carries a chunk-final CR into the next chunk.  Returns the names actually written."""
     written = []
     with open(output_file, "wb") as out:
         for name in file_names:
             p = os.path.join(genome_dir, name)
             try:
-                with open(p, "rb") as src:
-                    shutil.copyfileobj(src, out)
-                written.append(name)
+                src = open(p, "rb")
             except FileNotFoundError:
                 continue
+            with src:
+                carry = b""
+                while True:
+                    chunk = src.read(1 << 24)
+                    if not chunk:
+                        break
+                    chunk = carry + chunk
+                    carry = b""
+                    if chunk.endswith(b"\r"):
+                        chunk, carry = chunk[:-1], b"\r"
+                    out.write(chunk.replace(b"\r\n", b"\n").replace(b"\r", b"\n"))
+                if carry:
+                    out.write(b"\n")
+            written.append(name)
     return written
 
 

@@ -190,7 +190,7 @@ def cmd_map(argv: Sequence[str]) -> int:
             print("Creating index with minimap2...")
         else:
             print(f"Using cached minimap2 index: {index_path}")
-            loaded = mp.load_index(gpu, index_path)
+            loaded = mp.load_index(gpu, index_path, ref_fasta, split)
         if loaded is None:   # fresh, or a CPU minimap2 .mmi we keep untouched: build in HBM
             # HYMET_INDEX_MINI_BATCH: the index reader's mini-batch (minimap2's 50 Mbp chunking)
             mini = float(os.environ.get("HYMET_INDEX_MINI_BATCH", "50e6"))

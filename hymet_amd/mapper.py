@@ -216,11 +216,32 @@ def save_index(path_mmi: str, parts: List["IndexPart"], names, lens, part_first,
     os.replace(tmp, path_mmi)
 
 
-def load_index(gpu, path_mmi: str):
+def index_mismatch(man: dict, ref_fasta=None, split=None) -> List[str]:
+    """The manifest fields that disagree with the current reference FASTA / -I split.
+    minimap2.sh:10 reuses any non-empty index (`[ -s ]`), whatever the FASTA, and so does
+    load_index: these are reported as warnings, not acted on."""
+    import os
+    out = []
+    if ref_fasta and os.path.exists(ref_fasta) and man.get("reference_size") is not None:
+        st = os.stat(ref_fasta)
+        if os.path.abspath(ref_fasta) != man.get("reference"):
+            out.append(f"reference path {man.get('reference')} -> {os.path.abspath(ref_fasta)}")
+        if st.st_size != man.get("reference_size") or st.st_mtime != man.get("reference_mtime"):
+            out.append("reference size/mtime changed since the index was built")
+    if split is not None and man.get("split_idx") is not None and str(split) != str(man.get("split_idx")):
+        out.append(f"-I {man.get('split_idx')} -> {split}")
+    return out
+
+
+def load_index(gpu, path_mmi: str, ref_fasta=None, split=None, warn=None):
     """(parts, names, lens, part_first) of a persisted index, or None when PATH is not one
-    of ours (e.g. a real minimap2 .mmi) or its data file is missing."""
+    of ours (e.g. a real minimap2 .mmi) or its data file is missing.  The manifest's
+    reference path / size / mtime and split are checked against ref_fasta / split when
+    given; a mismatch is passed to `warn` (stderr by default) and the index is still used,
+    as the script's cache test does."""
     import json
     import os
+    import sys
     try:
         with open(path_mmi, "r") as f:
             man = json.loads(f.readline())
@@ -231,6 +252,8 @@ def load_index(gpu, path_mmi: str):
     data = os.path.join(os.path.dirname(os.path.abspath(path_mmi)), man["data"])
     if not os.path.exists(data):
         return None
+    for m in index_mismatch(man, ref_fasta, split):
+        (warn or (lambda t: print(t, file=sys.stderr)))(f"warning: cached index {path_mmi}: {m} (reused, as minimap2.sh does)")
     names, lens, first = man["names"], np.asarray(man["lens"], np.int64), man["part_first"]
     parts = []
     for i, off in enumerate(man["part_offsets"]):

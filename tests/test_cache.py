@@ -120,3 +120,19 @@ def test_dropin_script(tree):
     assert " - Successfully downloaded: 3" in r.stderr and " - Failed downloads: 2" in r.stderr
     r = subprocess.run([sys.executable, os.path.join(REPO, "scripts", "downloadDB.py"), "x"], capture_output=True, text=True)
     assert r.returncode == 1 and "Usage" in r.stdout
+
+
+def test_failed_downloads_counted_once_and_text_mode_line_ends(tmp_path):
+    """failed_downloads is a set (downloadDB.py:124,127): a GCF listed twice fails once.
+    concatenate_genomes copies through text-mode files (:215-218): CRLF / lone CR -> LF,
+    also across the 16 MiB chunk boundary."""
+    g = tmp_path / "g"
+    g.mkdir()
+    ok, failed = cache.resolve_downloads(["GCF_1.1", "GCF_2.1", "GCF_1.1"], {}, str(g))
+    assert ok == [] and failed == ["GCF_1.1", "GCF_2.1"]
+    big = b"A" * ((1 << 24) - 1) + b"\r\nCC\rGG\r"
+    (g / "a.fna").write_bytes(b">x\r\nACGT\r\n")
+    (g / "b.fna").write_bytes(big)
+    out = tmp_path / "c.fasta"
+    assert cache.concatenate_genomes(str(g), ["a.fna", "missing.fna", "b.fna"], str(out)) == ["a.fna", "b.fna"]
+    assert out.read_bytes() == b">x\nACGT\n" + b"A" * ((1 << 24) - 1) + b"\nCC\nGG\n"
