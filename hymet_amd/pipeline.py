@@ -47,6 +47,7 @@ class Config:
     map_batch_bases: int = 40_000_000  # query bases per device mapping batch (HBM budget)
     map_streams: int = 2              # concurrent mapping batches (library contexts / HIP streams)
     n_input_files: int = 1            # run_hymet_cami.sh copies one FASTA into input/
+    limit: bool = True                # run_hymet_cami.sh:101-126; main.pl has no limit step (False)
 
 
 @dataclass
@@ -302,6 +303,8 @@ class Pipeline:
             thr.append(t)
             selections.append(names)
         selected = sel.union_sorted(*selections)
+        if not self.cfg.limit:            # main.pl:94-104: the sort -u union goes to downloadDB.py
+            return selected, rows, thr
         scores = sel.best_scores(rows)
         limited = sel.limit(selected, scores, self.cfg.cand_max, self.cfg.dedupe)
         return limited, rows, thr

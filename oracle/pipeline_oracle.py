@@ -41,6 +41,8 @@ def select(pool_seqs, dbs, thresh="0.9", cand_max=5000, n_files=1):
                 continue
             if p[4] not in scores or s > scores[p[4]]:
                 scores[p[4]] = s
+    if cand_max is None:        # main.pl:94-104: no limit_candidates step, the sort -u union is used
+        return selected, sorted_tabs
     limited, _ = select_oracle.limit_candidates(selected, scores, cand_max)
     return limited, sorted_tabs
 
@@ -95,8 +97,9 @@ def map_paf(ref_names, ref_seqs, queries, part_bases=2e9, mini_batch=50e6, threa
 
 
 def run(queries, dbs, ref_lookup, taxonomy, hierarchy, thresh="0.9", cand_max=5000, part_bases=2e9, mini_batch=50e6,
-        threads=1):
-    """queries: list of (name, seq bytes).  Returns (selected, paf lines, tsv bytes)."""
+        threads=1, legacy=False):
+    """queries: list of (name, seq bytes).  Returns (selected, paf lines, tsv bytes).
+    cand_max=None, legacy=True: the main.pl path (no limit step, classification.py)."""
     selected, _ = select([q[1] for q in queries], dbs, thresh, cand_max)
     names, seqs = ref_lookup(selected)
     paf = map_paf(names, seqs, queries, part_bases, mini_batch, threads)
@@ -104,5 +107,6 @@ def run(queries, dbs, ref_lookup, taxonomy, hierarchy, thresh="0.9", cand_max=50
         p = os.path.join(td, "resultados.paf")
         with open(p, "w") as f:
             f.write("".join(l + "\n" for l in paf))
-        tsv = classify_oracle.classify_cami(p, taxonomy, hierarchy)
+        tsv = (classify_oracle.classify_legacy(p, taxonomy, hierarchy) if legacy
+               else classify_oracle.classify_cami(p, taxonomy, hierarchy))
     return selected, paf, tsv
