@@ -253,7 +253,7 @@ def bench_cami(args, comm, gpu, torch):
     return out
 
 
-def cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier, budget_s=20.0):
+def cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier, budget_s=None):
     """The CPU oracle restatement on a bounded sample of the same workload, on the host's
     cores, CHECKED against the GPU run: worker threads take 8-contig batches of a random
     sample and run the minimap2 asm10 restatement against the same candidate index parts
@@ -267,6 +267,7 @@ def cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier, budget_s=20.0):
     from concurrent.futures import ThreadPoolExecutor
     from hymet_amd.ingest import FastaIndex
     from oracle import classify_oracle, oracle_lib
+    budget_s = args.cpu_budget if budget_s is None else budget_s
     t0 = time.time()
     fx = FastaIndex(fasta)
     names = fx.names()
@@ -454,7 +455,9 @@ def bench_dry(args, comm):
             "contigs": int(t[0]), "bases": int(t[1]), "covers_input_once": bool(ok)}
 
 
-def main():
+def parse_args(argv=None):
+    """The command line, with the workload's defaults resolved (tests build the same
+    workloads through this)."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -472,15 +475,14 @@ def main():
     ap.add_argument("--cand-max", type=int, default=5000, help="CAND_MAX (run_hymet_cami.sh:26)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16, help="CPU baseline threads (the GPU box's CPU share is 16)")
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU mapping in the checked CPU leg")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend for N > 1 (auto: nccl = RCCL over xGMI)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rank r uses GPU r %% device_count (rehearse N ranks on fewer GPUs; use with --backend gloo)")
     ap.add_argument("--dry-run", action="store_true", help="CPU rehearsal of the N-rank launch and sharding (gloo, no GPU)")
     ap.add_argument("--tsv-out", default=None, help="rank 0 writes the last step's classified_sequences.tsv here")
-    args = ap.parse_args()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args.gpus))
+    args = ap.parse_args(argv)
     # CAMI-high (C5, BASELINE.json configs[4]): 14 taxa (tools/generate_cami_subsets.py:343),
     # the full CAND_MAX of 5000 candidates (~20 Gbp, ten -I2g parts), ~2 Gbp of contigs,
     # three sketch DBs of 1e8 / 5e7 / 1e7 hashes
@@ -497,6 +499,13 @@ def main():
         # C4: 60 Mbp batches measured 2327 ms/step vs 2460 (30) and ~2390 (40); scratch 148 GB
         args.batch_mbp = args.batch_mbp or 60.0
         args.workload_name = "CAMI-medium (C4)"
+    return args
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     from hymet_amd.dist import Comm
     comm = Comm.from_env()
     if comm.world != args.gpus:

@@ -1,27 +1,33 @@
-"""Parity at configuration size (BASELINE.json configs[1] and [2]).
+"""Parity at configuration size (BASELINE.json configs[0..2]; SURVEY.md §8(d) C1-C3;
+C4 / C5 in tests/test_configs_large_gpu.py).
 
-* C2 Zymo screen: 1,043 contigs with the exact query-length multiset of the reference's
-  Zymo PAF fixture (case/truth/zymo_mc/zymo_mc_vs_refs.paf col 2, committed as
-  tests/golden/classify/zymo.paf; 53.8 Mbp) against a sketch1-shaped DB of 2,000
-  references x 1,000 hashes (25 genome sketches + decoys, 2e6 hashes).  Counts, shared,
-  median, set size, screen.tab rows and the mash.sh selection must be bit-exact vs the CPU
-  oracle.
-* C3 CAMI-low: 8 taxa, 147 candidate genomes (bench/results_summary.md:90), 2,100 contigs,
-  one index part, end to end (screen -> select -> limit -> index -> map -> classify) vs
-  oracle/pipeline_oracle: selected candidates, PAF lines and TSV bytes identical, with one
-  mapping batch and again with seven.
+* C1 tiny, main.pl path: 60 contigs cut from three real Zymo chromosomes, legacy
+  classifier, no limit step; selected list, PAF and TSV identical to the oracle.
+* C2 Zymo screen: the 1,043 fixture contigs at their exact lengths, re-cut from the real
+  Zymo genomes (tests/_zymo.py), against the 25 real genome sketches + decoys (1e7 hashes).
+  Counts, shared, median, set size, screen.tab rows and the mash.sh selection bit-exact vs
+  the CPU oracle.
+* C3 CAMI-low: 8 taxa, 147 candidate genomes (bench/results_summary.md:90), 10,000
+  contigs, one index part, end to end (screen -> select -> limit -> index -> map ->
+  classify) vs oracle/pipeline_oracle: selected candidates, PAF lines and TSV bytes
+  identical, with one mapping batch and again with many.
 * A Pipeline reused on a second, repeat-rich candidate set resolves mid_occ from that set
   (options.c mm_mapopt_update in a fresh minimap2 process) and matches the oracle.
 * The run_hymet_cami.sh:182-206 fallback inside the fused path.
 
-Sequences are seeded synthetic stand-ins (the Zymo contig FASTA is absent from the
-reference); the oracle restates Mash / minimap2 (parity unpinned against the
-real tools)."""
+C1/C2 use the reference's real genomes; C3 is seeded synthetic (the CAMI data does not
+ship).  The oracle restates Mash / minimap2; its minimap2 part is pinned against the real
+minimap2 PAF the reference ships (tests/test_zymo_real.py), Mash stays unpinned
+(DESIGN.md §4)."""
+import functools
 import os
 from pathlib import Path
 
 import numpy as np
 import pytest
+
+from tests import _zymo as z
+from tests._data import mutate
 
 pytestmark = pytest.mark.gpu
 GOLD = Path(__file__).resolve().parent / "golden"
@@ -64,34 +70,40 @@ def _db(names, sketches, decoys, lengths):
                     hashes=np.concatenate(hl))
 
 
-def test_c2_zymo_screen_config_size(gpu):
+@functools.lru_cache(maxsize=1)
+def _zymo_sketches():
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle_lib
+    with ThreadPoolExecutor(THREADS) as ex:
+        return list(ex.map(lambda f: np.sort(oracle_lib.sketch([s for _, s in f[2]], 21, 42, 1000)), z.genome_files()))
+
+
+def _zymo_db(n_decoys, seed=1):
+    """sketch1-shaped DB: one Mash sketch per shipped Zymo genome FILE (mash sketch of a
+    multi-record file = one reference, named by the file) + seeded decoy references."""
+    from hymet_amd import synth
+    files = z.genome_files()
+    sk = _zymo_sketches()
+    return _db([f[1] for f in files], sk, synth.decoy_sketches(np.random.default_rng(seed), n_decoys, 1000),
+               [sum(len(s) for _, s in f[2]) for f in files])
+
+
+def test_config_c2_zymo_screen_real_contigs(gpu):
+    """BASELINE.json configs[1] "Zymo mock contigs: MinHash sketch+Jaccard vs sketch1.msh on 1
+    MI355X (screen stage only)" (SURVEY.md §8(d) C2): the 1,043 fixture contigs at their
+    exact lengths, re-cut from the real genomes at each contig's primary hit
+    (tests/_zymo.py; 726 Cryptococcus contigs from a seeded synthetic genome, that FASTA is
+    missing) against the 25 real genome sketches + 9,975 decoys (1e7 hashes)."""
     from hymet_amd import screen as scr
     from hymet_amd import select as sel
-    from hymet_amd import synth
     from hymet_amd.seqio import DevicePool, from_records
     from oracle import oracle_lib, select_oracle as so
-    qlens = zymo_qlens()
-    assert len(qlens) == 1043 and abs(sum(qlens) - 53.8e6) < 0.1e6
-    rng = np.random.default_rng(1)
-    sizes = [7_000_000] + [int(rng.uniform(2e6, 4.5e6)) for _ in range(9)]
-    base = [synth.random_codes(rng, n, gc=0.38 + 0.03 * i) for i, n in enumerate(sizes)]
-    genomes = base + [synth.mutate_codes(rng, base[i % 10], 0.002 + 0.002 * i) for i in range(15)]   # 25 "Zymo" refs
-    recs = []
-    for i, L in enumerate(qlens):
-        ok = [g for g in range(10) if len(base[g]) > L]
-        g = base[ok[int(rng.integers(len(ok)))]]
-        st = int(rng.integers(0, len(g) - L))
-        c = synth.mutate_codes(rng, g[st:st + L], 0.01)
-        if rng.random() < 0.5:
-            c = (3 - c)[::-1]
-        recs.append((f"ctg{i + 1}", "", synth.to_ascii(c)))
-    seqs = [r[2] for r in recs]
-    ref_ascii = [synth.to_ascii(g) for g in genomes]
-    sk = _sketch_all(ref_ascii)
-    db = _db([f"GCF_{i:09d}.1_zymo{i}_genomic.fna.gz" for i in range(25)], sk,
-             synth.decoy_sketches(rng, 1975, 1000), [len(g) for g in genomes])
-    assert len(db.hashes) >= 1_000_000
-    pool = DevicePool(gpu, from_records(recs), DevicePool.ALPHA_MASH)
+    recs = z.c2_contigs()
+    assert len(recs) == 1043 and sum(len(s) for _, s in recs) == 53_805_448
+    seqs = [s for _, s in recs]
+    db = _zymo_db(9975)
+    assert len(db.hashes) >= 10_000_000
+    pool = DevicePool(gpu, from_records([(n, "", s) for n, s in recs]), DevicePool.ALPHA_MASH)
     res = scr.screen(gpu, pool, [db])[0]
     sh, md, set_size, nk = oracle_lib.ScreenOracle(db).run(seqs)
     assert res.n_kmers == nk
@@ -101,6 +113,7 @@ def test_c2_zymo_screen_config_size(gpu):
     refs = [(db.names[i], db.comments[i], int(db.offsets[i + 1] - db.offsets[i])) for i in range(db.n_refs)]
     lines = res.lines(v_max=0.9)
     assert lines == so.screen_lines(refs, sh, md, set_size, 21)
+    # every shipped species is in the pool: all 25 genome files share hashes with it
     assert sum(1 for x in res.shared[:25] if x > 0) == 25
     rows = sel.sort_gr(sel.sort_unique_k5(lines))
     assert rows == so.sort_gr(so.sort_unique_k5(lines))
@@ -109,13 +122,59 @@ def test_c2_zymo_screen_config_size(gpu):
     assert got[:3] == exp[:3] and len(got[2]) >= 5
 
 
+@pytest.mark.timeout(600)
+def test_config_c1_tiny_main_pl_path(gpu, tmp_path):
+    """BASELINE.json configs[0] "testdataset/ tiny FASTA via main.pl" (SURVEY.md §8(d) C1):
+    60 contigs of U[5k, 50k] cut from three real Zymo chromosomes (E. coli GCF_000005845.2,
+    B. subtilis GCF_000009045.1, S. aureus GCF_000013425.1) with 1 % substitutions, seed 0,
+    through main.pl's sequence (main.pl:93-113): mash.sh on sketch1 (the 25 genomes) and a
+    decoy sketch2, sort -u union WITHOUT limit_candidates, minimap2 -I2g -d / -x asm10 over
+    the selected genome files, and the legacy classification.py.  Selected list, PAF and
+    TSV bytes identical to the oracle pipeline."""
+    from hymet_amd import classify as cls
+    from hymet_amd import pipeline, synth
+    from hymet_amd.seqio import from_records
+    from oracle import pipeline_oracle
+    rng = np.random.default_rng(0)
+    chrom = {f[1].split("_genomic")[0]: f[2][0] for f in z.genome_files()}
+    src = [chrom[k] for k in ("GCF_000005845.2_ASM584v2", "GCF_000009045.1_ASM904v1", "GCF_000013425.1_ASM1342v1")]
+    recs = []
+    for i in range(60):
+        name, g = src[i % 3]
+        L = int(rng.integers(5000, 50001))
+        st = int(rng.integers(0, len(g) - L))
+        recs.append((f"contig_{i + 1}", mutate(rng, g[st:st + L], 0.01)))
+    assert 1.0e6 < sum(len(c) for _, c in recs) < 2.2e6
+    db1 = _zymo_db(0)
+    db2 = _db([], [], synth.decoy_sketches(np.random.default_rng(5), 40, 1000), [])
+    by_file = {f[1]: f[2] for f in z.genome_files()}
+
+    def glook(names):
+        return from_records([(n, "", s) for f in names for n, s in by_file[f]])
+
+    def olook(names):
+        recs_ = [r for f in names for r in by_file[f]]
+        return [n for n, _ in recs_], [s for _, s in recs_]
+
+    tax, hier = str(GOLD / "classify" / "zymo_taxonomy.tsv"), str(GOLD / "classify" / "zymo_hierarchy_superkingdom.tsv")
+    p = pipeline.Pipeline(gpu, [db1, db2], glook, tax, hier, pipeline.Config(limit=False), variant=cls.LEGACY)
+    res = p.run(from_records([(n, "", s) for n, s in recs]), with_paf=True)
+    o_sel, o_paf, o_tsv = pipeline_oracle.run(recs, [db1, db2], olook, tax, hier, cand_max=None, threads=THREADS,
+                                              legacy=True)
+    assert res.selected == o_sel and len(o_sel) >= 3
+    assert res.selected == sorted(res.selected, key=lambda n: n.encode())      # the sort -u union, no limit
+    assert res.paf == o_paf and len(o_paf) >= 60
+    assert res.tsv == o_tsv
+    assert res.n_classified >= 55
+
+
 def _cami_low():
     from hymet_amd import synth
     rng = np.random.default_rng(2)
     per = [19, 19, 19, 18, 18, 18, 18, 18]
-    w = synth.make_cami(rng, n_taxa=8, per_taxon=per, genome_mbp=(0.6, 1.0), contig_gbp=0.05, max_contigs=2100,
+    w = synth.make_cami(rng, n_taxa=8, per_taxon=per, genome_mbp=(0.6, 1.0), contig_gbp=0.1, max_contigs=10_000,
                         name="cami-low")
-    assert len(w.refs) == 147 and len(w.contigs) == 2100
+    assert len(w.refs) == 147 and len(w.contigs) == 10_000
     return w, rng
 
 
@@ -150,8 +209,10 @@ def _lookups(*ws):
     return gpu_lookup, oracle_lookup
 
 
-@pytest.mark.timeout(600)
-def test_c3_cami_low_end_to_end(gpu, tmp_path):
+@pytest.mark.timeout(900)
+def test_config_c3_cami_low_end_to_end(gpu, tmp_path):
+    """BASELINE.json configs[2] "CAMI-low subset: full sketch->limit_candidates->
+    minimizer-chain->classify on 1 MI355X"."""
     from hymet_amd import pipeline
     from hymet_amd.seqio import from_records
     from oracle import pipeline_oracle
@@ -169,9 +230,9 @@ def test_c3_cami_low_end_to_end(gpu, tmp_path):
     assert res.selected == o_sel
     assert len(res.paf) == len(o_paf) and res.paf == o_paf
     assert res.tsv == o_tsv
-    assert res.n_classified >= 2000
-    # the same pool cut into seven mapping batches: identical bytes
-    p.cfg.map_batch_bases = 2_000_000
+    assert res.n_classified >= 9500
+    # the same pool cut into many mapping batches on two streams: identical bytes
+    p.cfg.map_batch_bases = 7_000_000
     res2 = p.run(queries, with_paf=True)
     assert res2.paf == o_paf and res2.tsv == o_tsv
 
