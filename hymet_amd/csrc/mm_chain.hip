@@ -862,13 +862,15 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 int32_t gy = INT32_MAX, gj = INT32_MAX;
                 if (P.max_dist_inner > 0) Lb = min(Lb, kInnerCap - ni);
                 // B: the best pre-batch window entry with y <= Y, Y = y of the last batch anchor,
-                // a superset of every batch anchor's krmq range; the batch starts only if B is
-                // the predecessor of its first anchor
+                // a superset of the krmq range of every batch anchor with y <= Y (the others are
+                // not committed); the batch starts only if B is the predecessor of its first anchor
                 double b0p = 0.0;
                 int32_t b0j = -1;
+                int32_t batch_y = INT32_MAX;  // B's y bound: every committed anchor must lie at or below it
                 if (walk_ok && Lb >= 2) {
                     const int offl = (i - cb) + Lb - 1;
                     const int32_t ymax = (int32_t)(offl < 64 ? rl((int32_t)cy, offl) : rl((int32_t)ny, offl - 64));
+                    batch_y = ymax;
 #if HYMET_CHAIN_B0FAST
                     // the window's best ignoring y (head suffix, block deque front, tail argmin:
                     // the O(1) sources step 4 uses) is B when its y <= Y -- the colinear case;
@@ -908,8 +910,11 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     const int32_t px = shr1(kx, prev.x), py = shr1(ky, prev.y), psp = shr1(ksp, prev.sp());
                     int32_t ex = 1, wd = 0;
                     const int32_t s = comput_sc(kx, ky, px, py, psp, P.pen_gap, P.pen_skip, &ex, &wd);
+                    // ky <= batch_y: B covers y <= Y, Y = the y of the batch's LAST anchor, which is a
+                    // superset of anchor k's krmq range (y < ky) only while ky <= Y -- y rises along
+                    // the committed prefix (py < ky), but an anchor past it may fall below Y
                     bool ok = inb && kx != px && (int64_t)(uint32_t)kx <= (int64_t)(uint32_t)px + P.max_dist &&
-                              py > ky - P.max_dist && py < ky && wd <= P.bw;
+                              py > ky - P.max_dist && py < ky && ky <= batch_y && wd <= P.bw;
                     // f_k = max(span_k, f_{k-1} + s_k): maps f -> max(f + a, b), composed by scan
                     int a = s, bb = ksp;
                     scan_maxplus(a, bb);

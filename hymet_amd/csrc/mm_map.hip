@@ -650,9 +650,11 @@ __global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
                 if (m <= kZs) {
                     P.mid_list[atomicAdd(P.lists + 1, 1)] = g;
                 } else {
+                    // list rank only: the radix arrays' offsets are a scan of the counts in rank
+                    // order (zbig_count_kernel), since the sorted keys come out rank-major
                     const int r = atomicAdd(P.lists + 2, 1);
                     P.big_list[r] = g;
-                    P.big_off[r] = (int64_t)atomicAdd((unsigned long long *)(P.lists + 4), (unsigned long long)m);
+                    atomicAdd((unsigned long long *)(P.lists + 4), (unsigned long long)m);
                 }
             }
         }
@@ -750,7 +752,14 @@ __global__ __launch_bounds__(256) void zsort_block_kernel(ZParams P) {
     }
 }
 
-// entries of the large groups, list-major: key = rank << 32 | f, value = idx
+// z entries of each large group, in list-rank order (scanned into big_off)
+__global__ void zbig_count_kernel(ZParams P, int32_t n_big, uint32_t *cnt) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n_big) cnt[r] = (uint32_t)P.z_cnt[P.big_list[r]];
+}
+
+// entries of the large groups, list-major: key = rank << 32 | f, value = idx; group r's
+// entries start at big_off[r] both before and after the sort (offsets ascend with the rank)
 __global__ void zbig_gather_kernel(ZParams P, uint64_t *skey, uint32_t *sval) {
     const int r = blockIdx.x, g = P.big_list[r];
     const int64_t z0 = P.g_start[g], n = P.z_cnt[g], o = P.big_off[r];
@@ -1238,6 +1247,13 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
             int64_t nz_big = 0;
             std::memcpy(&nz_big, hl + 4, 8);
             if (n_big > 0) {
+                DevBuf bcnt;
+                HY_HIP(bcnt.alloc(4 * (size_t)(n_big + 1), ctx->stream));
+                LAUNCH1(zbig_count_kernel, n_big, Z, (int32_t)n_big, bcnt.as<uint32_t>());
+                int64_t nz_scan = 0;
+                rc = exclusive_scan_u32_i64(ctx, bcnt.as<uint32_t>(), big_off.as<int64_t>(), n_big, &nz_scan);
+                if (rc) return rc;
+                if (nz_scan != nz_big) return hymet::fail(HYMET_E_INTERNAL, "hymet_mm_map: z list count mismatch");
                 DevBuf sk, sk2, sv, sv2;
                 HY_HIP(sk.alloc(8 * (size_t)nz_big, ctx->stream));
                 HY_HIP(sk2.alloc(8 * (size_t)nz_big, ctx->stream));
@@ -1283,6 +1299,57 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
                               chain_ids.as<int64_t>(), chain_u.as<uint64_t>(), chain_first.as<int64_t>(),
                               n_chains.as<int32_t>(), n);
         if (rc) return rc;
+        if (getenv("HYMET_DEBUG_BT")) {  // diagnostic: z order and chain disjointness per group
+            HY_HIP(hipStreamSynchronize(ctx->stream));
+            std::vector<int64_t> gs(G + 1), hid(n), hcf(n);
+            std::vector<int32_t> zc(G), zi(n), hf(n), nch(G), zr(G);
+            std::vector<uint64_t> hcu(n);
+            HY_HIP(hipMemcpy(gs.data(), g_start.p, 8 * (size_t)(G + 1), hipMemcpyDeviceToHost));
+            HY_HIP(hipMemcpy(zc.data(), z_cnt.p, 4 * (size_t)G, hipMemcpyDeviceToHost));
+            HY_HIP(hipMemcpy(zr.data(), z_runs.p, 4 * (size_t)G, hipMemcpyDeviceToHost));
+            HY_HIP(hipMemcpy(zi.data(), zidx.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+            HY_HIP(hipMemcpy(hf.data(), f.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+            HY_HIP(hipMemcpy(nch.data(), n_chains.p, 4 * (size_t)G, hipMemcpyDeviceToHost));
+            HY_HIP(hipMemcpy(hid.data(), chain_ids.p, 8 * (size_t)n, hipMemcpyDeviceToHost));
+            HY_HIP(hipMemcpy(hcu.data(), chain_u.p, 8 * (size_t)n, hipMemcpyDeviceToHost));
+            HY_HIP(hipMemcpy(hcf.data(), chain_first.p, 8 * (size_t)n, hipMemcpyDeviceToHost));
+            std::vector<int32_t> seen(n, -1);
+            int64_t bad_z = 0, bad_c = 0;
+            for (int64_t g = 0; g < G; g++) {
+                const int64_t g0 = gs[g], gn = gs[g + 1] - g0;
+                int64_t want = 0;
+                for (int64_t a = g0; a < g0 + gn; a++) want += hf[a] >= opt->min_chain_score;
+                bool zok = zc[g] == want || gn < opt->min_cnt;
+                for (int64_t t = 0; zok && t < zc[g]; t++) {
+                    const int64_t a = zi[g0 + t];
+                    if (a < g0 || a >= g0 + gn || hf[a] < opt->min_chain_score) zok = false;
+                    else if (t > 0) {
+                        const int64_t b = zi[g0 + t - 1];
+                        if (!(hf[b] < hf[a] || (hf[b] == hf[a] && b < a))) zok = false;
+                    }
+                }
+                if (!zok && bad_z++ < 5)
+                    fprintf(stderr, "[bt] group %lld size %lld: z order wrong (z_cnt %d want %lld runs %d)\n", (long long)g,
+                            (long long)gn, zc[g], (long long)want, zr[g]);
+                for (int c = 0; c < nch[g]; c++) {
+                    const int64_t fo = hcf[g0 + c];
+                    const int32_t m = (int32_t)hcu[g0 + c];
+                    for (int32_t j = 0; j < m; j++) {
+                        const int64_t a = hid[fo + j];
+                        if (a < g0 || a >= g0 + gn || seen[a] == (int32_t)g) {
+                            if (bad_c++ < 5)
+                                fprintf(stderr, "[bt] group %lld size %lld chain %d/%d anchor %lld %s (z runs %d)\n",
+                                        (long long)g, (long long)gn, c, nch[g], (long long)a,
+                                        (a < g0 || a >= g0 + gn) ? "outside the group" : "in two chains", zr[g]);
+                        } else {
+                            seen[a] = (int32_t)g;
+                        }
+                    }
+                }
+            }
+            fprintf(stderr, "[bt] groups %lld anchors %lld: z errors %lld, chain overlaps %lld\n", (long long)G, (long long)n,
+                    (long long)bad_z, (long long)bad_c);
+        }
         if (getenv("HYMET_TRACE_BT")) {
             HY_HIP(hipStreamSynchronize(ctx->stream));
             fprintf(stderr, " bt=%.2f ms\n",
@@ -1817,7 +1884,26 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                 int64_t got = 0;
                 rc = exclusive_scan_u32_i64(ctx, tcnt.as<uint32_t>(), toff.as<int64_t>(), nt, &got);
                 if (rc) return rc;
-                if (got != A2 || got != lj.n2) return hymet::fail(HYMET_E_INTERNAL, "hymet_mm_map: long-join anchor count mismatch");
+                if (got != A2 || got != lj.n2) {
+                    if (getenv("HYMET_DEBUG_LJ2")) {  // diagnostic: per-query marks vs chain anchors
+                        std::vector<uint8_t> hm(n1);
+                        std::vector<int64_t> qo(n_q + 1);
+                        HY_HIP(hipMemcpy(hm.data(), mark.p, (size_t)n1, hipMemcpyDeviceToHost));
+                        HY_HIP(hipMemcpy(qo.data(), S1.d_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost));
+                        int shown = 0;
+                        for (int q = 0; q < n_q; q++) {
+                            int64_t mk = 0;
+                            for (int64_t a = qo[q]; a < qo[q + 1]; a++) mk += hm[a];
+                            const int64_t want = qb[q + 1] - qb[q];
+                            if ((h_flag[q] ? want : 0) != mk && shown++ < 10)
+                                fprintf(stderr, "[lj2] q %d flag %u anchors %lld marks %lld chain anchors %lld\n", q, h_flag[q],
+                                        (long long)(qo[q + 1] - qo[q]), (long long)mk, (long long)want);
+                        }
+                        fprintf(stderr, "[lj2] got %lld A2 %lld n2 %lld n1 %lld\n", (long long)got, (long long)A2,
+                                (long long)lj.n2, (long long)n1);
+                    }
+                    return hymet::fail(HYMET_E_INTERNAL, "hymet_mm_map: long-join anchor count mismatch");
+                }
                 HY_HIP(S2.ax.alloc(8 * (size_t)(A2 + 1), st));
                 HY_HIP(S2.ay.alloc(8 * (size_t)(A2 + 1), st));
                 hipLaunchKernelGGL(mark_compact_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<uint8_t>(), n1,

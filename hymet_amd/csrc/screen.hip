@@ -6,7 +6,8 @@
 //   screen_count<K>: one thread = one 64-position tile of the pooled, packed query bases.
 //                    Rolling 2-bit forward / reverse-complement words decide the canonical
 //                    strand by integer compare (== Mash's memcmp on ASCII, since A<C<G<T);
-//                    rolling ASCII byte windows feed MurmurHash3_x64_128 (seeded, word 0)
+//                    rolling ASCII byte windows feed MurmurHash3_x64_128 (seeded, word 0; or
+//                    MurmurHash3_x86_32 for k <= 16, Mash's 32-bit sketches, widened to 64 bits)
 //                    without re-expanding the k-mer; each hash probes up to 4 DB tables and
 //                    bumps a uint32 count; hashes under a threshold are appended as bottom-s
 //                    candidates for the pool set-size estimate (MinHashHeap::estimateSetSize).
@@ -69,6 +70,37 @@ __device__ __forceinline__ uint64_t murmur3_h0(const uint64_t (&w)[4], uint32_t 
     return h1 + h2;
 }
 
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+// MurmurHash3_x86_32 of a K-byte key (K <= 16) held little-endian in w[0..1], bytes past K zero.
+template <int K>
+__device__ __forceinline__ uint32_t murmur3_x86_32(const uint64_t (&w)[4], uint32_t seed) {
+    constexpr uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    constexpr int NB = K / 4, TAIL = K & 3;
+    uint32_t h1 = seed;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        uint32_t k1 = (uint32_t)(w[b >> 1] >> (32 * (b & 1)));
+        k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2;
+        h1 ^= k1; h1 = rotl32(h1, 13); h1 = h1 * 5 + 0xe6546b64u;
+    }
+    if constexpr (TAIL > 0) {
+        uint32_t k1 = (uint32_t)(w[NB >> 1] >> (32 * (NB & 1)));  // the K & 3 tail bytes, zero above
+        k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h1 ^= k1;
+    }
+    h1 ^= (uint32_t)K;
+    h1 ^= h1 >> 16; h1 *= 0x85ebca6bu;
+    h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u;
+    h1 ^= h1 >> 16;
+    return h1;
+}
+
+template <int K>
+__device__ __forceinline__ uint64_t mash_hash(const uint64_t (&w)[4], uint32_t seed) {
+    if constexpr (K <= 16) return (uint64_t)murmur3_x86_32<K>(w, seed);
+    else return murmur3_h0<K>(w, seed);
+}
+
 struct CountParams {
     const uint32_t *w2b;
     const uint32_t *wm;
@@ -125,7 +157,7 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
             if (run < K) continue;                                       // invalid base inside the k-mer
             const int64_t p = i - (K - 1);
             if (p < p0) continue;                                        // warm-up only
-            const uint64_t h = (rc < fwd) ? murmur3_h0<K>(R, P.seed) : murmur3_h0<K>(F, P.seed);
+            const uint64_t h = (rc < fwd) ? mash_hash<K>(R, P.seed) : mash_hash<K>(F, P.seed);
             nk++;
             if (h < P.cand_thr) {
                 unsigned long long idx = atomicAdd(P.cand_n, 1ull);
@@ -295,7 +327,7 @@ int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_m
                        const int64_t *h_n_slots, uint32_t *const *h_d_counts, uint64_t cand_thr, uint64_t *d_cand,
                        int64_t cand_cap, unsigned long long *d_cand_n, unsigned long long *d_nkmers) {
     HY_ARG(ctx && d_2b && d_mask && d_cand_n && d_nkmers, "hymet_screen_count: null argument");
-    HY_ARG(k >= 17 && k <= 32, "hymet_screen_count: k must be in 17..32 (64-bit Mash hashes)");
+    HY_ARG(k >= 1 && k <= 32, "hymet_screen_count: k must be in 1..32");
     HY_ARG(ndb >= 0 && ndb <= kMaxDb, "hymet_screen_count: ndb must be 0..4");
     HY_ARG(cand_cap == 0 || d_cand, "hymet_screen_count: d_cand is null");
     if (pos_end > n_bases - k + 1) pos_end = n_bases - k + 1;
@@ -328,6 +360,8 @@ int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_m
     switch (k) {
 #define HY_K(KK) \
     case KK: return launch_count<KK>(ctx, P, n_tiles);
+        HY_K(1) HY_K(2) HY_K(3) HY_K(4) HY_K(5) HY_K(6) HY_K(7) HY_K(8)
+        HY_K(9) HY_K(10) HY_K(11) HY_K(12) HY_K(13) HY_K(14) HY_K(15) HY_K(16)
         HY_K(17) HY_K(18) HY_K(19) HY_K(20) HY_K(21) HY_K(22) HY_K(23) HY_K(24)
         HY_K(25) HY_K(26) HY_K(27) HY_K(28) HY_K(29) HY_K(30) HY_K(31) HY_K(32)
 #undef HY_K

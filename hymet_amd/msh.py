@@ -17,6 +17,15 @@ PARITY-UNPINNED:
           hashes64 @6 :List(UInt64); length64 @7 :UInt64; counts32 @8 :List(UInt32);
           counts32Sorted @9 :Bool; } } }
 
+The ordinals of `referenceList` and `locusList` (@7 / @8) are the one detail this
+restatement cannot settle from memory alone; the product reader (csrc/msh.cpp, through
+`read_msh`) therefore takes whichever of pointers 1 and 2 holds Reference structs (Locus
+structs carry no pointers) and falls back to `referenceListOld` (pointer 0), as Mash does
+for old files.  Hand-assembled byte fixtures (tests/golden/msh/, written field by field by
+tests/golden/make_msh_fixtures.py, independent of write_msh) pin the reader on both
+layouts, multi-segment messages with far and double-far pointers, 32-bit sketches and
+unsorted hash lists.
+
 Resulting layouts (Cap'n Proto field-slot allocation): MinHash data = 3 words
 {kmerSize@0B, windowSize@4B, minHashesPerWindow@8B, concatenated bit96, noncanonical bit97,
 preserveCase bit98, error@16B, hashSeed@20B (xor 42)}, 4 pointers {refListOld, refList,
@@ -174,7 +183,43 @@ class _Struct:
         return [_Struct(self.m, s, t + 1 + j * step, dw, npt) for j in range(cnt)]
 
 
-def read_msh(path) -> SketchDB:
+def read_msh(path, threads: int = 16) -> SketchDB:
+    """.msh -> SketchDB through the library's native reader (hymet_msh_*: mmap, pointer walk
+    and a threaded hash gather; S1 of SURVEY.md §8a, on the timed path since `mash screen`
+    reads its DB on every call).  The library is required, like every product path."""
+    import ctypes
+    from ._lib import check, load
+    lib = load()
+    h = ctypes.c_void_p()
+    check(lib.hymet_msh_open(str(path).encode(), ctypes.byref(h)), "hymet_msh_open")
+    try:
+        raw = (ctypes.c_int64 * 9)()   # hymet_msh_info: 7 int32 (+4 pad) then 5 int64
+        check(lib.hymet_msh_info_get(h, ctypes.byref(raw)), "hymet_msh_info_get")
+        b = bytes(raw)
+        k, win, ss, seed, nonc, pc, use64 = struct.unpack_from("<iiiIiii", b, 0)
+        n_refs, n_hashes, nb, cb, al = struct.unpack_from("<qqqqq", b, 32)
+        hashes = np.empty(max(n_hashes, 1), np.uint64)
+        offsets = np.empty(n_refs + 1, np.int64)
+        lengths = np.empty(max(n_refs, 1), np.int64)
+        names = ctypes.create_string_buffer(max(nb, 1))
+        comments = ctypes.create_string_buffer(max(cb, 1))
+        alpha = ctypes.create_string_buffer(max(al, 1))
+        check(lib.hymet_msh_copy(h, int(threads), hashes.ctypes.data_as(ctypes.c_void_p),
+                                 offsets.ctypes.data_as(ctypes.c_void_p), lengths.ctypes.data_as(ctypes.c_void_p),
+                                 names, comments, alpha), "hymet_msh_copy")
+    finally:
+        lib.hymet_msh_close(h)
+
+    def split(buf, n):
+        return buf.raw[:-1].decode("utf-8", "replace").split("\0") if n else []
+
+    return SketchDB(k=k, seed=seed, sketch_size=ss, alphabet=alpha.raw[:al].decode() or "ACGT", preserve_case=bool(pc),
+                    noncanonical=bool(nonc), window_size=win, names=split(names, n_refs), comments=split(comments, n_refs),
+                    lengths=lengths[:n_refs].copy(), offsets=offsets, hashes=hashes[:n_hashes])
+
+
+def read_msh_py(path) -> SketchDB:
+    """Pure-Python reader of the same format (tests cross-check it against the native one)."""
     data = open(path, "rb").read()
     m = _Msg(data)
     root = m.struct_at(0, 0)

@@ -74,7 +74,8 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
     cand_n = gpu.zeros(1, torch.int64)
     nk = gpu.zeros(1, torch.int64)
     frac = 16.0 * s / span
-    thr = U64_MAX if frac >= 1.0 else int(frac * 2.0 ** 64)
+    top = hash_top(k)              # hashes are 64-bit for k > 16, 32-bit (x86_32) for k <= 16
+    thr = U64_MAX if frac >= 1.0 else int(frac * float(top))
     keys_arr = (ctypes.c_void_p * 4)(*[ptr(t.keys).value for t in tables])
     slots_arr = (ctypes.c_int64 * 4)(*[t.n_slots for t in tables])
     cnt_arr = (ctypes.c_void_p * 4)(*[ptr(c).value for c in counts])
@@ -101,7 +102,7 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
             break
         # fewer than s distinct hashes under the threshold (repetitive pool): raise it
         # monotonically and re-run the hash pass in candidates-only mode (ndb = 0)
-        thr = U64_MAX if thr > U64_MAX // 16 else thr * 16
+        thr = U64_MAX if thr > top // 16 else thr * 16
         cand = rerun(thr, cap)
     return counts, bottom, n_kmers
 
@@ -129,11 +130,17 @@ def reduce_partials(comm, counts, bottom: np.ndarray, nk: int, s: int, tables=No
     return counts, bottom, nk
 
 
-def set_size_from_bottom(bottom: np.ndarray) -> int:
-    """MinHashHeap::estimateSetSize: 2^64 * |heap| / max(heap), truncated to uint64."""
+def hash_top(k: int) -> int:
+    """2^bits of Mash's k-mer hash: 64-bit (MurmurHash3_x64_128 word 0) for k > 16, 32-bit
+    (MurmurHash3_x86_32) for k <= 16."""
+    return 1 << 64 if k > 16 else 1 << 32
+
+
+def set_size_from_bottom(bottom: np.ndarray, k: int = 21) -> int:
+    """MinHashHeap::estimateSetSize: 2^bits * |heap| / max(heap), truncated to uint64."""
     if len(bottom) == 0:
         return 0
-    return int(18446744073709551616.0 * float(len(bottom)) / float(int(bottom[-1])))
+    return int(float(hash_top(k)) * float(len(bottom)) / float(int(bottom[-1])))
 
 
 def table_stats(gpu, t: ScreenTable, counts):
@@ -152,8 +159,8 @@ def screen(gpu, pool, dbs: Sequence[SketchDB], tables: Optional[Sequence[ScreenT
     results: List[Optional[ScreenResult]] = [None] * len(dbs)
     groups = {}
     for i, db in enumerate(dbs):
-        if db.k <= 16 or db.k > 32:
-            raise ValueError(f"k={db.k}: only 64-bit Mash sketches (17 <= k <= 32) are supported")
+        if db.k < 1 or db.k > 32:
+            raise ValueError(f"k={db.k}: Mash k-mer sizes are 1..32")
         if db.noncanonical:
             raise ValueError("noncanonical sketches are not supported")
         groups.setdefault((db.k, db.seed, db.preserve_case), []).append(i)
@@ -171,7 +178,7 @@ def screen(gpu, pool, dbs: Sequence[SketchDB], tables: Optional[Sequence[ScreenT
             for ci, i in enumerate(chunk):
                 sh, md = table_stats(gpu, tables[i], counts[ci])
                 b_i = bottom[:dbs[i].sketch_size]
-                results[i] = ScreenResult(dbs[i], sh, md, set_size_from_bottom(b_i), nk)
+                results[i] = ScreenResult(dbs[i], sh, md, set_size_from_bottom(b_i, k), nk)
     return results
 
 

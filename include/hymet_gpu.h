@@ -110,8 +110,29 @@ int64_t hymet_screen_table_slots(int64_t n_hashes);
  * the reserved all-ones key).  Resets d_keys itself. */
 int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n_hashes,
                              uint64_t *d_keys, int64_t n_slots, int64_t *d_slot_of);
-/* Hash every valid canonical k-mer of the packed pool (k in 17..32, MurmurHash3_x64_128
- * word 0 with `seed`), probe ndb (<= 4) tables, count hits into d_counts[i] (n_slots[i]+1
+/* ---- Mash sketch databases (.msh) ----
+ * Replaces the .msh load inside `mash screen` (scripts/mash.sh:14; the DB files of
+ * run_hymet_cami.sh:52,85-97 and main.pl:44-46): the Cap'n Proto MinHash message is mapped
+ * and parsed natively.  hymet_msh_open maps + parses; hymet_msh_info_get
+ * reports the header and sizes; hymet_msh_copy fills any of: hashes (n_hashes uint64, each
+ * reference's list ascending, 32-bit hashes widened), offsets (n_refs + 1), lengths
+ * (n_refs), names / comments (NUL-separated, names_bytes / comments_bytes), alphabet
+ * (alphabet_len bytes, no NUL).  `threads` host threads gather the hashes. */
+typedef struct hymet_msh hymet_msh;
+typedef struct {
+    int32_t k, window_size, sketch_size;
+    uint32_t seed;
+    int32_t noncanonical, preserve_case, use64;
+    int64_t n_refs, n_hashes, names_bytes, comments_bytes, alphabet_len;
+} hymet_msh_info;
+int hymet_msh_open(const char *path, hymet_msh **out);
+int hymet_msh_info_get(const hymet_msh *m, hymet_msh_info *info);
+int hymet_msh_copy(const hymet_msh *m, int threads, uint64_t *hashes, int64_t *offsets, int64_t *lengths,
+                   char *names, char *comments, char *alphabet);
+void hymet_msh_close(hymet_msh *m);
+/* Hash every valid canonical k-mer of the packed pool (k in 1..32: MurmurHash3_x64_128
+ * word 0 with `seed` for k > 16, MurmurHash3_x86_32 widened to 64 bits for k <= 16, as
+ * Mash's 64- / 32-bit sketches), probe ndb (<= 4) tables, count hits into d_counts[i] (n_slots[i]+1
  * uint32 each, caller-zeroed), and append every hash < cand_thr to d_cand (bottom-s
  * candidates; d_cand_n counts appends, may exceed cand_cap).  d_nkmers += valid k-mers.
  * seq_begin/seq_end limit the k-mer START positions processed (for sharding). */

@@ -5,13 +5,15 @@
  *
  * Restates, from the public Mash 2.3 algorithm (third-party, unpinned: environment.yml:9;
  * called by scripts/mash.sh:14 as `mash screen -p 8 -v 0.9 DB input/ *.fna`):
- *   - MurmurHash3_x64_128 (Austin Appleby, public domain), word 0 kept (k > 16 => 64-bit)
+ *   - MurmurHash3_x64_128 (Austin Appleby, public domain), word 0 kept (k > 16 => 64-bit);
+ *     MurmurHash3_x86_32 for k <= 16 (Mash's 32-bit sketches, hashes32), widened to uint64
  *   - CommandScreen hashSequence: uppercase unless preserveCase; a k-mer is skipped if any
  *     base is outside the alphabet (ACGT); canonical = forward unless memcmp(rc, fwd) < 0;
  *     every occurrence of a table hash increments its count; every k-mer is offered to
  *     the pool bottom-s heap (distinct hashes)
  *   - per-reference shared / median depth (sorted depths[shared/2])
- *   - MinHashHeap::estimateSetSize = 2^64 * |heap| / max(heap)   (truncated to uint64)
+ *   - MinHashHeap::estimateSetSize = 2^64 (2^32 for 32-bit hashes) * |heap| / max(heap)
+ *     (truncated to uint64)
  * Parity with Mash itself is UNPINNED (no mash binary or .msh fixture in the container,
  * SURVEY.md §8c); the hash function is pinned by tests/golden/murmur3_kat.json, produced
  * from scikit-learn's vendored MurmurHash3.cpp (tests/golden/make_murmur_kat.py).
@@ -66,6 +68,38 @@ uint64_t oracle_murmur3_x64_128_h0(const uint8_t *data, int len, uint32_t seed) 
     h1 = fmix64(h1); h2 = fmix64(h2);
     h1 += h2;
     return h1;
+}
+
+static inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+uint32_t oracle_murmur3_x86_32(const uint8_t *data, int len, uint32_t seed) {
+    const int nblocks = len / 4;
+    uint32_t h1 = seed;
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    for (int i = 0; i < nblocks; i++) {
+        uint32_t k1;
+        memcpy(&k1, data + 4 * i, 4);
+        k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2;
+        h1 ^= k1; h1 = rotl32(h1, 13); h1 = h1 * 5 + 0xe6546b64u;
+    }
+    const uint8_t *tail = data + 4 * nblocks;
+    uint32_t k1 = 0;
+    switch (len & 3) {
+    case 3: k1 ^= (uint32_t)tail[2] << 16; /* fallthrough */
+    case 2: k1 ^= (uint32_t)tail[1] << 8;  /* fallthrough */
+    case 1: k1 ^= tail[0];
+            k1 *= c1; k1 = rotl32(k1, 15); k1 *= c2; h1 ^= k1;
+    }
+    h1 ^= (uint32_t)len;
+    h1 ^= h1 >> 16; h1 *= 0x85ebca6bu;
+    h1 ^= h1 >> 13; h1 *= 0xc2b2ae35u;
+    h1 ^= h1 >> 16;
+    return h1;
+}
+
+/* Mash's k-mer hash: 64-bit word 0 of x64_128 for k > 16, x86_32 for k <= 16 */
+static inline uint64_t mash_hash(const uint8_t *km, int k, uint32_t seed) {
+    return k > 16 ? oracle_murmur3_x64_128_h0(km, k, seed) : (uint64_t)oracle_murmur3_x86_32(km, k, seed);
 }
 
 /* ---- simple open-addressing set/map over uint64 keys ---- */
@@ -142,7 +176,7 @@ int oracle_screen_run(void *h, const char *seq, const int64_t *seq_off, int64_t 
                       int preserve_case, int64_t sketch_size, uint32_t *shared, uint32_t *median, uint64_t *set_size,
                       uint64_t *n_kmers) {
     oscreen_t *o = (oscreen_t *)h;
-    if (k < 17 || k > 32) return -1;
+    if (k < 1 || k > 32) return -1;
     omap_t *tab = &o->tab;
     for (uint64_t i = 0; i <= tab->mask; i++) tab->val[i] = 0;
     bottom_t bt;
@@ -174,7 +208,7 @@ int oracle_screen_run(void *h, const char *seq, const int64_t *seq_off, int64_t 
             if (!good) continue;
             const char *fw = up + j, *rv = rc + (L - j - k);
             const char *km = memcmp(rv, fw, (size_t)k) < 0 ? rv : fw;
-            uint64_t hh = oracle_murmur3_x64_128_h0((const uint8_t *)km, k, seed);
+            uint64_t hh = mash_hash((const uint8_t *)km, k, seed);
             nk++;
             bottom_offer(&bt, hh);
             uint64_t s = omap_slot(tab, hh);
@@ -185,7 +219,7 @@ int oracle_screen_run(void *h, const char *seq, const int64_t *seq_off, int64_t 
     bottom_compact(&bt);
     *n_kmers = nk;
     if (bt.n == 0) *set_size = 0;
-    else *set_size = (uint64_t)(18446744073709551616.0 * (double)bt.n / (double)bt.b[bt.n - 1]);
+    else *set_size = (uint64_t)((k > 16 ? 18446744073709551616.0 : 4294967296.0) * (double)bt.n / (double)bt.b[bt.n - 1]);
     uint32_t *dep = NULL;
     int64_t depcap = 0;
     for (int64_t r = 0; r < o->nrefs; r++) {
@@ -209,7 +243,7 @@ int oracle_screen(const char *seq, const int64_t *seq_off, int64_t nseq, int k, 
                   int preserve_case, int64_t sketch_size,
                   const uint64_t *ref_hashes, const int64_t *ref_off, int64_t nrefs,
                   uint32_t *shared, uint32_t *median, uint64_t *set_size, uint64_t *n_kmers) {
-    if (k < 17 || k > 32) return -1;
+    if (k < 1 || k > 32) return -1;
     void *h = oracle_screen_prepare(ref_hashes, ref_off, nrefs);
     int rc = oracle_screen_run(h, seq, seq_off, nseq, k, seed, preserve_case, sketch_size, shared, median, set_size, n_kmers);
     oracle_screen_free(h);
@@ -241,7 +275,7 @@ int64_t oracle_sketch(const char *seq, const int64_t *seq_off, int64_t nseq, int
             for (int t = 0; t < k; t++) { char c = up[j + t]; if (c != 'A' && c != 'C' && c != 'G' && c != 'T') { good = 0; break; } }
             if (!good) continue;
             const char *fw = up + j, *rv = rc + (L - j - k);
-            all[n++] = oracle_murmur3_x64_128_h0((const uint8_t *)(memcmp(rv, fw, (size_t)k) < 0 ? rv : fw), k, seed);
+            all[n++] = mash_hash((const uint8_t *)(memcmp(rv, fw, (size_t)k) < 0 ? rv : fw), k, seed);
         }
     }
     free(up); free(rc);

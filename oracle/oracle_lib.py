@@ -24,6 +24,8 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         L.oracle_murmur3_x64_128_h0.restype = ctypes.c_uint64
         L.oracle_murmur3_x64_128_h0.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32]
+        L.oracle_murmur3_x86_32.restype = ctypes.c_uint32
+        L.oracle_murmur3_x86_32.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32]
         L.oracle_screen.restype = ctypes.c_int
         L.oracle_sketch.restype = ctypes.c_int64
         _lib = L
@@ -36,6 +38,10 @@ def _p(a):
 
 def murmur3_h0(s: bytes, seed: int) -> int:
     return lib().oracle_murmur3_x64_128_h0(s, len(s), seed)
+
+
+def murmur3_x86_32(s: bytes, seed: int) -> int:
+    return lib().oracle_murmur3_x86_32(s, len(s), seed)
 
 
 def concat(seqs):

@@ -23,8 +23,9 @@ def _make_db(rng, genomes, k, seed, s, n_decoys=50):
     for i, g in enumerate(genomes):
         hl.append(np.sort(oracle_lib.sketch([g], k, seed, s)))
         names.append(f"GCF_{i:09d}.1_genome{i}.fna.gz")
+    top = 2**63 if k > 16 else 2**31     # 32-bit sketches (k <= 16) hold x86_32 hashes
     for j in range(n_decoys):
-        hl.append(np.sort(rng.integers(0, 2**63, size=s, dtype=np.int64).astype(np.uint64) * 2 + 1))
+        hl.append(np.sort(rng.integers(0, top, size=s, dtype=np.int64).astype(np.uint64) * 2 + 1))
         names.append(f"decoy_{j}")
     off = np.zeros(len(hl) + 1, dtype=np.int64)
     off[1:] = np.cumsum([len(h) for h in hl])
@@ -50,7 +51,8 @@ def _pool(rng, genomes, n_contigs, lo, hi, rate=0.01):
     return recs
 
 
-@pytest.mark.parametrize("k,seed,s", [(21, 42, 1000), (17, 7, 500), (32, 42, 200), (25, 0, 300)])
+@pytest.mark.parametrize("k,seed,s", [(21, 42, 1000), (17, 7, 500), (32, 42, 200), (25, 0, 300),
+                                      (16, 42, 1000), (13, 7, 400), (9, 42, 200)])
 def test_screen_matches_oracle(gpu, k, seed, s):
     from hymet_amd import screen as scr
     from hymet_amd.seqio import DevicePool, from_records
@@ -118,4 +120,20 @@ def test_gpu_hash_kat(gpu):
     pool = DevicePool(gpu, from_records([(f"q{i}", "", v["s"].encode()) for i, v in enumerate(vecs)]), DevicePool.ALPHA_MASH)
     r = scr.screen(gpu, pool, [db])[0]
     # duplicates among the vectors make some counts > 1; every vector must be found
+    assert (r.shared == 1).all()
+
+
+def test_gpu_hash_kat_x86_32(gpu):
+    """k <= 16: Mash's 32-bit sketches hash with MurmurHash3_x86_32 (KATs from an independent
+    implementation); every canonical 16-mer's hash must hit the table."""
+    from hymet_amd import screen as scr
+    from hymet_amd.msh import SketchDB
+    from hymet_amd.seqio import DevicePool, from_records
+    kat = json.loads((Path(__file__).resolve().parent / "golden" / "murmur3_kat.json").read_text())
+    vecs = kat["x86_32_zymo_canonical_k16_seed42"]
+    hs = np.array([int(v["h32"], 16) for v in vecs], dtype=np.uint64)
+    db = SketchDB(k=16, seed=42, sketch_size=len(vecs), names=[f"v{i}" for i in range(len(vecs))], comments=[""] * len(vecs),
+                  lengths=np.ones(len(vecs), np.int64), offsets=np.arange(len(vecs) + 1, dtype=np.int64), hashes=hs)
+    pool = DevicePool(gpu, from_records([(f"q{i}", "", v["s"].encode()) for i, v in enumerate(vecs)]), DevicePool.ALPHA_MASH)
+    r = scr.screen(gpu, pool, [db])[0]
     assert (r.shared == 1).all()
