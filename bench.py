@@ -4,9 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cami-medium|screen]
 
 One step = one pass of the HYMET hot path over one input, in the SURVEY.md §8(d) window:
-FASTA text in host memory -> record table -> host-to-device copy -> screen -> select ->
-limit -> map (both -I2g parts) -> LCA -> classified_sequences.tsv written (and the
-resultados.paf text emitted to host memory).  Default workload: CAMI-medium (C4,
+sketch DB files (.msh) parsed and their HBM tables built, detailed_taxonomy.tsv +
+taxonomy_hierarchy.tsv loaded, FASTA text in host memory -> record table -> host-to-device
+copy -> screen -> select -> limit -> map (both -I2g parts) -> LCA ->
+classified_sequences.tsv written (and the resultados.paf text emitted to host memory).  Default workload: CAMI-medium (C4,
 BASELINE.json configs[3]): 12 taxa, ~1 Gbp / ~151k contigs, 744 candidate genomes (~3 Gbp,
 two index parts), a sketch1-sized DB (1e5 refs x 1000 hashes).  The candidate-keyed index
 is built in the untimed cold run (run_hymet_cami.sh caches it the same way) and reported
@@ -117,7 +118,7 @@ def cpu_info():
 # ------------------------------------------------------------------ CAMI-medium
 def build_cami(args, comm, gpu):
     from hymet_amd import ingest, pipeline, screen as scr, synth
-    from hymet_amd.msh import SketchDB
+    from hymet_amd.msh import SketchDB, write_msh
     from hymet_amd.seqio import DevicePool, from_records
     t0 = time.time()
     # the same community and the same contig pool on every rank (strong scaling)
@@ -154,6 +155,14 @@ def build_cami(args, comm, gpu):
     log(f"sketch DBs: " + ", ".join(f"{x.n_refs} refs / {len(x.hashes)/1e6:.0f}M hashes" for x in dbs) +
         f" ({time.time()-t0:.1f}s)")
     td = tempfile.mkdtemp(prefix="hymet_bench_")
+    # the DBs as Mash .msh files (data/sketch{1,2,3}.msh): every step reads them, as every
+    # `mash screen` does (scripts/mash.sh:14), so S1 is inside the timed window
+    t0 = time.time()
+    db_paths = []
+    for d, x in enumerate(dbs):
+        db_paths.append(os.path.join(td, f"sketch{d + 1}.msh"))
+        write_msh(x, db_paths[-1])
+    log(f"wrote {len(db_paths)} .msh files ({sum(os.path.getsize(q) for q in db_paths)/1e9:.2f} GB, {time.time()-t0:.1f}s)")
     tax = os.path.join(td, "detailed_taxonomy.tsv")
     hier = os.path.join(td, "taxonomy_hierarchy.tsv")
     open(tax, "w").write(w.taxonomy_tsv())
@@ -165,7 +174,7 @@ def build_cami(args, comm, gpu):
 
     cfg = pipeline.Config(map_batch_bases=int(args.batch_mbp * 1e6), map_streams=args.map_streams,
                           cand_max=args.cand_max)
-    pipe = pipeline.Pipeline(gpu, dbs, ref_lookup, tax, hier, cfg, comm)
+    pipe = pipeline.Pipeline(gpu, db_paths, ref_lookup, tax, hier, cfg, comm)
     return w, db, pipe, fasta, refs_ss, tax, hier, td
 
 
@@ -195,8 +204,11 @@ def bench_cami(args, comm, gpu, torch):
         import cProfile
         cp = cProfile.Profile()
         cp.enable()
+    loads = {}
     for _ in range(args.steps):
-        res = pipe.run(fasta, with_paf=True)        # FASTA bytes in host memory -> TSV + PAF text
+        res = pipe.run(fasta, with_paf=True)        # .msh + taxonomy files, FASTA bytes in host memory -> TSV + PAF text
+        for k, v in pipe.timings.items():
+            loads[k] = loads.get(k, 0.0) + v
         if comm.rank == 0:
             with open(tsv_path, "wb") as f:             # classified_sequences.tsv written
                 f.write(res.tsv)
@@ -233,13 +245,18 @@ def bench_cami(args, comm, gpu, torch):
                    "global_contigs": n_contigs, "parallelism": f"contig-shard x{comm.world}",
                    "backend": (("nccl (RCCL over xGMI)" if comm.dist.get_backend() == "nccl" else comm.dist.get_backend())
                                if comm.dist is not None else "none (1 rank)"),
-                   "window": "FASTA bytes in host memory -> classified_sequences.tsv written + resultados.paf text in host "
-                             "memory (ingest, H2D, screen, select, limit, map, LCA, text emit inside every step)"},
+                   "window": "sketch{1..3}.msh + detailed_taxonomy.tsv + taxonomy_hierarchy.tsv read, FASTA bytes in host "
+                             "memory -> classified_sequences.tsv written + resultados.paf text in host memory (DB parse + "
+                             "table build, taxonomy load, ingest, H2D, screen, select, limit, map, LCA, text emit inside "
+                             "every step)"},
         "cold_run_s": cold,
         "scratch_cached_gb": gpu_scratch_gb(gpu),
         "paf_lines": n_lines,
         "kernel_ms_per_step_rank0": kern_ms,
         "stage_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
+        # host wall time of the per-step input loads (inside ms_per_step): S1 .msh parse and
+        # HBM table build, C1-C2 taxonomy + hierarchy load
+        "input_load_ms_per_step": {k.replace("_s", "_ms"): v * 1e3 / args.steps for k, v in loads.items()},
         "roofline": roofline_from_prof(prof),
         "path_roofline": path_roofline(prof, args.steps, step, total_bases, total_bases, n_lines, len(ix.parts), comm.world),
     }

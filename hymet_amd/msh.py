@@ -231,10 +231,15 @@ def read_msh_py(path) -> SketchDB:
     db.preserve_case = root.bit(98)
     db.seed = root.u32(20, default=42)
     db.alphabet = root.text(3) or "ACGT"
-    rl = m.struct_at(root.seg, root.ptr_word(1))
-    if rl is None:
-        rl = m.struct_at(root.seg, root.ptr_word(0))  # referenceListOld
-    refs = rl.struct_list(0) if rl is not None else []
+    refs = []
+    for pi in (1, 2, 0):   # referenceList (@7 or @8: the list of Reference structs), else referenceListOld
+        if pi >= root.np:
+            continue
+        rl = m.struct_at(root.seg, root.ptr_word(pi))
+        lst = rl.struct_list(0) if rl is not None and rl.np > 0 else []
+        if lst and lst[0].np > 0:
+            refs = lst
+            break
     names, comments, lengths, hl = [], [], [], []
     use64 = db.k > 16
     for r in refs:

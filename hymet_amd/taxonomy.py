@@ -20,7 +20,7 @@ from __future__ import annotations
 import csv
 import io
 import sys
-from collections import defaultdict
+from collections import Counter
 from typing import Dict, Iterable, List, Optional, Tuple
 
 CAMI_RANKS = ["superkingdom", "phylum", "class", "order", "family", "genus", "species"]
@@ -116,7 +116,7 @@ def reformat(d: TaxDump, taxids: Iterable[str], fmt_ranks=("domain|superkingdom"
     per taxid the names and the taxids of its ancestors (itself included) at those ranks,
     '|'-joined, empty where the lineage has no such rank; unknown taxids give no line."""
     out: Dict[str, Tuple[str, str]] = {}
-    want = [set(r.split("|")) for r in fmt_ranks]
+    want = [r.split("|") for r in fmt_ranks]   # alternatives in preference order
     for tid in taxids:
         if not tid or tid not in d.node:
             continue
@@ -137,63 +137,53 @@ def reformat(d: TaxDump, taxids: Iterable[str], fmt_ranks=("domain|superkingdom"
 
 
 # -------------------------------------------------------------------- hymet2cami
-def parse_lineage(lineage: str) -> Dict[str, str]:
-    """hymet2cami.py:40-52."""
-    out = {r: "" for r in CAMI_RANKS}
-    if not lineage:
-        return out
-    for part in lineage.split(";"):
-        part = part.strip()
-        if not part or ":" not in part:
+_SLOT = {r: i for i, r in enumerate(CAMI_RANKS)}
+
+
+def rank_names(lineage: str) -> List[str]:
+    """A Lineage cell -> the name at each CAMI rank ("" where absent): 'label:name' parts,
+    labels folded through CAMI_ALIAS (hymet2cami.py:15-32,46-58), a later part overriding an
+    earlier one at the same rank, other labels ignored."""
+    slots = [""] * len(CAMI_RANKS)
+    for part in (lineage or "").split(";"):
+        label, sep, name = part.strip().partition(":")
+        if not sep:
             continue
-        rk, name = part.split(":", 1)
-        rk = CAMI_ALIAS.get(rk.strip().lower(), rk.strip().lower())
-        if rk in out:
-            out[rk] = name.strip()
-    return out
+        key = label.strip().lower()
+        i = _SLOT.get(CAMI_ALIAS.get(key, key))
+        if i is not None:
+            slots[i] = name.strip()
+    return slots
+
+
+def parse_lineage(lineage: str) -> Dict[str, str]:
+    return dict(zip(CAMI_RANKS, rank_names(lineage)))
 
 
 def load_records(tsv_text: str) -> List[Dict[str, str]]:
-    """hymet2cami.py:104-112 (rows whose lineage names at least one CAMI rank)."""
-    recs = []
-    for row in csv.DictReader(io.StringIO(tsv_text), delimiter="\t"):
-        p = parse_lineage(row.get("Lineage", ""))
-        if any(p.values()):
-            recs.append(p)
-    return recs
+    """The rows (csv.DictReader over the TSV) whose Lineage names at least one CAMI rank,
+    as rank -> name (hymet2cami.py:104-112)."""
+    rows = (rank_names(r.get("Lineage", "")) for r in csv.DictReader(io.StringIO(tsv_text), delimiter="\t"))
+    return [dict(zip(CAMI_RANKS, slots)) for slots in rows if any(slots)]
 
 
 def cami_profile(records: List[Dict[str, str]], name2tid: Dict[str, str],
                  taxid2path: Dict[str, Tuple[str, str]], sample_id: str = "sample_0") -> str:
-    """hymet2cami.py:115-149: per rank, the share of records whose name at that rank maps
-    to a taxid, by count descending (stable), '%.6f' percentages."""
-    counts = {r: defaultdict(int) for r in CAMI_RANKS}
-    totals = {r: 0 for r in CAMI_RANKS}
-    for p in records:
-        for r in CAMI_RANKS:
-            name = p.get(r)
-            if not name:
-                continue
-            tid = name2tid.get(name)
-            if not tid:
-                continue
-            counts[r][tid] += 1
-            totals[r] += 1
-    out = io.StringIO()
-    out.write("#CAMI Submission for Taxonomic Profiling\n")
-    out.write(f"@Version:0.9.1 @Ranks:superkingdom|phylum|class|order|family|genus|species @SampleID:{sample_id}\n")
-    out.write("@@TAXID RANK TAXPATH TAXPATHSN PERCENTAGE\n")
-    for r in CAMI_RANKS:
-        total = totals[r]
-        if total <= 0:
-            continue
-        for tid, c in sorted(counts[r].items(), key=lambda kv: kv[1], reverse=True):
-            path = taxid2path.get(tid)
-            if not path:
-                continue
-            names, ids = path
-            out.write(f"{tid}\t{r}\t{ids}\t{names}\t{100.0 * c / total:.6f}\n")
-    return out.getvalue()
+    """The CAMI profile text (hymet2cami.py:115-149): for each rank, the records whose name
+    there maps to a taxid are tallied per taxid; each taxid with a reformat path is printed
+    with its share of the rank's tally, largest tally first (ties in first-seen order),
+    '%.6f'.  A rank without any mapped name prints nothing."""
+    lines = ["#CAMI Submission for Taxonomic Profiling",
+             f"@Version:0.9.1 @Ranks:{'|'.join(CAMI_RANKS)} @SampleID:{sample_id}",
+             "@@TAXID RANK TAXPATH TAXPATHSN PERCENTAGE"]
+    for rank in CAMI_RANKS:
+        tally = Counter(t for t in (name2tid.get(r.get(rank) or "") for r in records) if t)
+        total = sum(tally.values())
+        for tid, n in sorted(tally.items(), key=lambda kv: -kv[1]):
+            path = taxid2path.get(tid) if total > 0 else None
+            if path:
+                lines.append(f"{tid}\t{rank}\t{path[1]}\t{path[0]}\t{100.0 * n / total:.6f}")
+    return "\n".join(lines) + "\n"
 
 
 def hymet2cami(tsv_path: str, taxdb: str, log=sys.stderr) -> str:

@@ -1,0 +1,54 @@
+"""The .msh reader pinned by hand-assembled bytes it did not write
+(tests/golden/make_msh_fixtures.py): one and three segments, single- and double-far
+pointers, the current reference list in either pointer slot, the old list, 32-bit (k <= 16)
+and 64-bit hashes, unsorted hash lists, and older struct sizes.  The native reader
+(csrc/msh.cpp, the product path) and the pure-Python one must both return expect.json; a
+truncated file must fail loudly.  Host-only: no GPU call."""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from hymet_amd import msh
+
+MSH = Path(__file__).resolve().parent / "golden" / "msh"
+EXPECT = json.loads((MSH / "expect.json").read_text())
+
+
+def _view(db):
+    return {"k": db.k, "seed": db.seed, "sketch_size": db.sketch_size, "preserve_case": db.preserve_case,
+            "noncanonical": db.noncanonical, "alphabet": db.alphabet, "names": list(db.names),
+            "comments": list(db.comments), "lengths": [int(x) for x in db.lengths],
+            "hashes": [[int(v) for v in db.ref_hashes(i)] for i in range(db.n_refs)]}
+
+
+@pytest.mark.parametrize("name", sorted(EXPECT))
+@pytest.mark.parametrize("reader", [msh.read_msh, msh.read_msh_py])
+def test_hand_assembled_fixture(name, reader):
+    assert _view(reader(MSH / name)) == EXPECT[name]
+
+
+def test_truncated_file_fails_loudly(tmp_path):
+    from hymet_amd._lib import HymetError
+    data = (MSH / "v2_far32.msh").read_bytes()
+    for cut in (4, 40, len(data) - 8):
+        p = tmp_path / f"cut{cut}.msh"
+        p.write_bytes(data[:cut])
+        with pytest.raises(HymetError):
+            msh.read_msh(p)
+    with pytest.raises(HymetError):
+        msh.read_msh(tmp_path / "missing.msh")
+
+
+def test_writer_round_trip_native(tmp_path):
+    rng = np.random.default_rng(3)
+    hl = [np.sort(rng.integers(0, 2 ** 63, int(rng.integers(0, 50))).astype(np.uint64)) for _ in range(300)]
+    off = np.zeros(len(hl) + 1, np.int64)
+    off[1:] = np.cumsum([len(h) for h in hl])
+    db = msh.SketchDB(names=[f"r{i}.fna" for i in range(300)], comments=[f"c{i}" * (i % 3) for i in range(300)],
+                      lengths=np.arange(300, dtype=np.int64) * 7, offsets=off, hashes=np.concatenate(hl))
+    msh.write_msh(db, tmp_path / "w.msh")
+    got = msh.read_msh(tmp_path / "w.msh")
+    assert got.names == db.names and got.comments == db.comments
+    assert (got.offsets == db.offsets).all() and (got.hashes == db.hashes).all() and (got.lengths == db.lengths).all()
