@@ -1266,7 +1266,10 @@ struct BacktrackParams {
 // marks and its reset walk are not needed (p[i] < i: a path never revisits itself), and the
 // chain is path[0, best end), left in walk order (end -> start; chain_list / chain_copy read it
 // reversed).  Path nodes are marked as the walk passes them and the few past the best end
-// unmarked afterwards, so no pass re-reads the path.  Paths run mostly down consecutive anchors, so the walk keeps a
+// unmarked afterwards, so no pass re-reads the path.  t after the backtrack: 0 = free, 1 = used
+// by a walk whose chain was dropped (score or count below the minimum), 2 = in a kept chain
+// (the long join reads the 2s of its queries, mm_map.hip mark_count / mark_compact).
+// Paths run mostly down consecutive anchors, so the walk keeps a
 // window of kBtWin (p, f, t) triples below the current node, loaded together (one memory
 // round trip per window instead of one per step); the z scan batches its t probes the same
 // way.  Windows are refilled after every walk, since a walk's t marks make them stale.
@@ -1408,7 +1411,7 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             const int32_t zf = uni(zfsel);
             int64_t *buf = P.chain_ids + wpos;
             buf[0] = zi;  // every lane: same value, same address
-            P.t[zi] = 1;  // path nodes are marked as recorded; those past the best end are unmarked after
+            P.t[zi] = 2;  // path nodes are marked as recorded; those past the best end are unmarked after
             int64_t len = 1, nv = 0;  // recorded path nodes; chain = path[0, nv)
             int32_t max_s = 0;
             int64_t nxt = uni64(zpsel);
@@ -1479,7 +1482,7 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                 }
                 if (lane >= o && lane <= last) {
                     buf[len + (lane - o)] = j;
-                    P.t[j] = 1;  // the walk never re-reads a node it has passed (p[i] < i)
+                    P.t[j] = 2;  // the walk never re-reads a node it has passed (p[i] < i)
                 }
                 len += last - o + 1;
                 if (done) break;
@@ -1500,6 +1503,8 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                 P.chain_first[g0 + nc] = wpos;
                 nc++;
                 wpos += nv;
+            } else {
+                for (int64_t a = lane; a < nv; a += 64) P.t[ld_l2(buf + a)] = 1;  // used, but in no chain
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             if (P.prof) t_post += clock64() - t_w1;
@@ -1552,7 +1557,7 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
         int32_t wf[kBtWin], wt[kBtWin];
         for (;;) {
             buf[len++] = i;
-            P.t[i] = 1;  // no revisits: marking as we go cannot change this walk's reads
+            P.t[i] = 2;  // no revisits: marking as we go cannot change this walk's reads
             int32_t fn = 0, tn = 1;
             int64_t pn = -1;
             if (nxt >= 0) {
@@ -1589,6 +1594,8 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
             P.chain_first[g0 + nc] = wpos;
             nc++;
             wpos += nv;
+        } else {
+            for (int64_t a = 0; a < nv; a++) P.t[buf[a]] = 1;  // used, but in no chain
         }
     }
     P.n_chains[g] = nc;

@@ -832,12 +832,12 @@ __global__ void chain_qb_kernel(const int64_t *qc, const int64_t *bpos, int64_t 
     qb[q] = c < n_chain ? bpos[c] : nb;
 }
 
-// anchors of chain c in start -> end order, and c per anchor; or (mark != nullptr) only a mark
-// on every counted chain's anchors in the chained anchor set (the long join compacts by it)
+// anchors of chain c in start -> end order, and c per anchor (the chains of queries the long
+// join re-chains have no anchors here: cnt 0)
 __global__ __launch_bounds__(256) void chain_copy_kernel(const uint64_t *cu, const int64_t *cfirst, const int64_t *bpos,
                                                          const int64_t *chain_ids, const uint64_t *ax, const uint64_t *ay,
                                                          int64_t n_chain, int64_t nb, uint64_t *bx, uint64_t *by,
-                                                         int32_t *bchain, uint8_t *mark) {
+                                                         int32_t *bchain) {
     // flat over the output anchors: the block's first chain c0 by binary search over bpos; the
     // starts of the next 256 chains are staged in LDS and each lane finds its chain by an
     // 8-step search there (a forward walk per lane cost up to 255 dependent loads where chains
@@ -882,46 +882,81 @@ __global__ __launch_bounds__(256) void chain_copy_kernel(const uint64_t *cu, con
     }
     const int32_t m = (int32_t)cu[c];
     const int64_t a = chain_ids[cfirst[c] + m - 1 - (b - bpos[c])];  // backtrack stores end -> start
-    if (mark) {
-        mark[a] = 1;
-        return;
-    }
     bx[b] = ax[a];
     by[b] = ay[a];
     bchain[b] = (int32_t)c;
 }
 
-// marked anchors per 4096-anchor tile (16 per thread, one 16-byte load)
-__global__ __launch_bounds__(256) void mark_count_kernel(const uint8_t *mark, int64_t n, uint32_t *cnt) {
+// Long-join anchors: the first pass's chain anchors (t == 2 after the backtrack) of the
+// flagged queries.  Thread l of a 4096-anchor tile decides anchors [16 l, 16 l + 16) of the
+// tile (16-byte loads of t; the query of the first by a binary search over the query
+// offsets, then stepping over the few query starts inside the 16).
+__device__ __forceinline__ uint32_t keep_bits16(const int32_t *t, int64_t n, const uint32_t *qflag, const int64_t *qoff,
+                                                int n_q, int64_t e0) {
+    if (e0 >= n) return 0u;
+    int lo = 0, hi = n_q - 1;  // last q with qoff[q] <= e0
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (qoff[mid] <= e0) lo = mid;
+        else hi = mid - 1;
+    }
+    int q = lo;
+    int64_t qend = qoff[q + 1];
+    int32_t v[16];
+    if (e0 + 16 <= n) {
+        const int4 *p4 = reinterpret_cast<const int4 *>(t + e0);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int4 w = p4[u];
+            v[4 * u] = w.x, v[4 * u + 1] = w.y, v[4 * u + 2] = w.z, v[4 * u + 3] = w.w;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = e0 + u < n ? t[e0 + u] : 0;
+    }
+    uint32_t bits = 0, fl = qflag[q];
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        while (e0 + u >= qend && q + 1 < n_q) {  // a query starts here
+            q++;
+            qend = qoff[q + 1];
+            fl = qflag[q];
+        }
+        bits |= (uint32_t)(v[u] == 2 && fl != 0) << u;
+    }
+    return bits;
+}
+
+__global__ __launch_bounds__(256) void mark_count_kernel(const int32_t *t, int64_t n, const uint32_t *qflag,
+                                                         const int64_t *qoff, int n_q, uint32_t *cnt) {
     __shared__ uint32_t ws[4];
     const int64_t e0 = (int64_t)blockIdx.x * 4096 + threadIdx.x * 16;
-    uint32_t c = 0;
-    if (e0 + 16 <= n) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(mark + e0);
-        c = __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);  // marks are 0 / 1 bytes
-    } else {
-        for (int64_t e = e0; e < n && e < e0 + 16; e++) c += mark[e];
-    }
+    uint32_t c = __popc(keep_bits16(t, n, qflag, qoff, n_q, e0));
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor((int)c, o, 64);
     if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// stable compaction of the marked anchors (x, y): the first-pass set is sorted by (query, x,
-// y), so its marked subsequence is the long join's sorted anchor set -- no re-sort.
-// Rows of 256 anchors, lanes striped (coalesced), positions by ballot counts.
-__global__ __launch_bounds__(256) void mark_compact_kernel(const uint8_t *mark, int64_t n, const int64_t *tile_off,
+// stable compaction of the kept anchors (x, y): the first-pass set is sorted by (query, x,
+// y), so its kept subsequence is the long join's sorted anchor set -- no re-sort.  The keep
+// bits are decided per 16 consecutive anchors (as in the count) into LDS; rows of 256
+// anchors are then written lanes striped (coalesced), positions by ballot counts.
+__global__ __launch_bounds__(256) void mark_compact_kernel(const int32_t *t, int64_t n, const uint32_t *qflag,
+                                                           const int64_t *qoff, int n_q, const int64_t *tile_off,
                                                            const uint64_t *ax, const uint64_t *ay, uint64_t *ox,
                                                            uint64_t *oy) {
-    __shared__ uint32_t rc[64];  // marks per (row, wave), row-major
+    __shared__ uint32_t rc[64];       // kept per (row, wave), row-major
+    __shared__ uint16_t kb[256];      // keep bits of anchors [16 l, 16 l + 16) of the tile
     const int64_t t0 = (int64_t)blockIdx.x * 4096;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    kb[threadIdx.x] = (uint16_t)keep_bits16(t, n, qflag, qoff, n_q, t0 + threadIdx.x * 16);
+    __syncthreads();
     bool m[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-        const int64_t e = t0 + j * 256 + threadIdx.x;
-        m[j] = e < n && mark[e];
+        const int r = j * 256 + threadIdx.x;  // tile-relative anchor
+        m[j] = (kb[r >> 4] >> (r & 15)) & 1;
         const uint64_t b = __ballot(m[j]);
         if (lane == 0) rc[j * 4 + w] = (uint32_t)__popcll(b);
     }
@@ -1417,22 +1452,19 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         if (NC > 0 && NB > 0)
             LAUNCH1(chain_copy_kernel, NB, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), C.cboff.as<int64_t>(),
                     chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, NB, C.bx.as<uint64_t>(),
-                    C.by.as<uint64_t>(), C.bchain.as<int32_t>(), (uint8_t *)nullptr);
+                    C.by.as<uint64_t>(), C.bchain.as<int32_t>());
         HY_HIP(C.d_qb.alloc(8 * (size_t)(n_q + 1), ctx->stream));
         LAUNCH1(chain_qb_kernel, n_q + 1, C.d_qc.as<int64_t>(), C.cboff.as<int64_t>(), NC, NB, n_q, C.d_qb.as<int64_t>());
         HY_HIP(hipMemcpyAsync(C.h_qc.data(), C.d_qc.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, ctx->stream));
         HY_HIP(hipMemcpyAsync(C.h_qb.data(), C.d_qb.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, ctx->stream));
-        if (qflag) {  // the re-chained queries' chain anchors: marked in the chained set, per-query counts
+        if (qflag) {  // the re-chained queries' chain anchors: per-query counts, and t handed over
             DevBuf boff2, qb2;
             int64_t NB2 = 0;
             rc = scan_flags(ctx, ccnt2.as<uint32_t>(), NC, boff2, &NB2);
             if (rc) return rc;
-            HY_HIP(lj->mark.alloc((size_t)n + 16, ctx->stream));
-            HY_HIP(hipMemsetAsync(lj->mark.p, 0, (size_t)n + 16, ctx->stream));
-            if (NB2 > 0)
-                LAUNCH1(chain_copy_kernel, NB2, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), boff2.as<int64_t>(),
-                        chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, NB2, (uint64_t *)nullptr,
-                        (uint64_t *)nullptr, (int32_t *)nullptr, lj->mark.as<uint8_t>());
+            // the backtrack left t == 2 on every kept chain's anchors: the long join selects
+            // those of its queries straight from t (no pass over the chains)
+            lj->mark.swap(t);
             HY_HIP(qb2.alloc(8 * (size_t)(n_q + 1), ctx->stream));
             LAUNCH1(chain_qb_kernel, n_q + 1, C.d_qc.as<int64_t>(), boff2.as<int64_t>(), NC, NB2, n_q, qb2.as<int64_t>());
             lj->h_qb2.assign(n_q + 1, 0);
@@ -1871,29 +1903,29 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
             HY_HIP(S2.d_off.alloc(8 * (size_t)(n_q + 1), st));
             HY_HIP(hipMemcpyAsync(S2.d_off.p, S2.h_off.data(), 8 * (size_t)(n_q + 1), hipMemcpyHostToDevice, st));
             if (lj.mark_only) {
-                // the flagged queries' chain anchors (marked by chain_set), compacted out of the
-                // first-pass set in its (key, y) order -- already the long join's sorted anchor set
+                // the flagged queries' chain anchors (t == 2 from the backtrack), compacted out of
+                // the first-pass set in its (key, y) order -- already the long join's sorted set
                 const int64_t n1 = S1.n, nt = cdiv(n1, 4096);
                 DevBuf &mark = lj.mark;
                 DevBuf tcnt, toff;
                 HY_HIP(tcnt.alloc(4 * (size_t)(nt + 1), st));
                 HY_HIP(toff.alloc(8 * (size_t)(nt + 1), st));
-                hipLaunchKernelGGL(mark_count_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<uint8_t>(), n1,
-                                   tcnt.as<uint32_t>());
+                hipLaunchKernelGGL(mark_count_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<int32_t>(), n1,
+                                   flag.as<uint32_t>(), S1.d_off.as<int64_t>(), n_q, tcnt.as<uint32_t>());
                 HY_CHECK_LAUNCH("mark_count_kernel");
                 int64_t got = 0;
                 rc = exclusive_scan_u32_i64(ctx, tcnt.as<uint32_t>(), toff.as<int64_t>(), nt, &got);
                 if (rc) return rc;
                 if (got != A2 || got != lj.n2) {
                     if (getenv("HYMET_DEBUG_LJ2")) {  // diagnostic: per-query marks vs chain anchors
-                        std::vector<uint8_t> hm(n1);
+                        std::vector<int32_t> hm(n1);
                         std::vector<int64_t> qo(n_q + 1);
-                        HY_HIP(hipMemcpy(hm.data(), mark.p, (size_t)n1, hipMemcpyDeviceToHost));
+                        HY_HIP(hipMemcpy(hm.data(), mark.p, 4 * (size_t)n1, hipMemcpyDeviceToHost));
                         HY_HIP(hipMemcpy(qo.data(), S1.d_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost));
                         int shown = 0;
                         for (int q = 0; q < n_q; q++) {
                             int64_t mk = 0;
-                            for (int64_t a = qo[q]; a < qo[q + 1]; a++) mk += hm[a];
+                            for (int64_t a = qo[q]; a < qo[q + 1]; a++) mk += hm[a] == 2 && h_flag[q];
                             const int64_t want = qb[q + 1] - qb[q];
                             if ((h_flag[q] ? want : 0) != mk && shown++ < 10)
                                 fprintf(stderr, "[lj2] q %d flag %u anchors %lld marks %lld chain anchors %lld\n", q, h_flag[q],
@@ -1906,9 +1938,9 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                 }
                 HY_HIP(S2.ax.alloc(8 * (size_t)(A2 + 1), st));
                 HY_HIP(S2.ay.alloc(8 * (size_t)(A2 + 1), st));
-                hipLaunchKernelGGL(mark_compact_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<uint8_t>(), n1,
-                                   toff.as<int64_t>(), S1.ax.as<uint64_t>(), S1.ay.as<uint64_t>(), S2.ax.as<uint64_t>(),
-                                   S2.ay.as<uint64_t>());
+                hipLaunchKernelGGL(mark_compact_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<int32_t>(), n1,
+                                   flag.as<uint32_t>(), S1.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), S1.ax.as<uint64_t>(),
+                                   S1.ay.as<uint64_t>(), S2.ax.as<uint64_t>(), S2.ay.as<uint64_t>());
                 HY_CHECK_LAUNCH("mark_compact_kernel");
                 S2.n = A2;
                 rc = dump_anchors(getenv("HYMET_DUMP_ANCHORS2"), S2, dumped2);
