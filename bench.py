@@ -48,19 +48,22 @@ SCOPE_KERNEL = {"mm_chain": "chain_groups_kernel<0>", "mm_chain_long": "chain_gr
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # tools/pmc_summary.py output
 
 
-def pmc_traffic(scope):
+def pmc_traffic(scope, workload=None, batch_mbp=None):
     """HBM bytes per launch of the scope's kernel from the committed PMC passes (FETCH_SIZE /
-    WRITE_SIZE, gfx950-corrected: tools/pmc_summary.py), or None."""
+    WRITE_SIZE, gfx950-corrected: tools/pmc_summary.py), measured on THIS workload at THIS
+    mapping batch size (per-launch bytes scale with the batch), or None."""
     try:
         with open(PMC_FILE) as fh:
             tab = json.load(fh)
     except (OSError, ValueError):
         return None
-    r = tab.get(SCOPE_KERNEL.get(scope, ""), {})
-    return r.get("traffic_bytes")
+    w = tab.get(workload or "", {})
+    if batch_mbp is not None and w.get("batch_mbp") != batch_mbp:
+        return None
+    return w.get("kernels", {}).get(SCOPE_KERNEL.get(scope, ""), {}).get("traffic_bytes")
 
 
-def roofline_from_prof(prof, prefer=None):
+def roofline_from_prof(prof, prefer=None, workload=None, batch_mbp=None):
     """Dominant kernel = the largest summed device time among the scopes that time one main
     kernel (SCOPE_KERNEL; mm_chain also holds the small-group lane kernel, ~2 % of it).
     Multi-kernel sections with host syncs inside (mm_anchor_gsort, mm_z_order) are not
@@ -72,7 +75,7 @@ def roofline_from_prof(prof, prefer=None):
     ms, n, b = cand[name]
     achieved = b / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc_traffic(name), "kernel": name, "kernel_symbol": SCOPE_KERNEL.get(name),
+            "traffic": pmc_traffic(name, workload, batch_mbp), "kernel": name, "kernel_symbol": SCOPE_KERNEL.get(name),
             "kernel_avg_ms": ms / max(n, 1), "launches": n, "alg_bytes_per_launch": b / max(n, 1)}
 
 
@@ -257,7 +260,7 @@ def bench_cami(args, comm, gpu, torch):
         # host wall time of the per-step input loads (inside ms_per_step): S1 .msh parse and
         # HBM table build, C1-C2 taxonomy + hierarchy load
         "input_load_ms_per_step": {k.replace("_s", "_ms"): v * 1e3 / args.steps for k, v in loads.items()},
-        "roofline": roofline_from_prof(prof),
+        "roofline": roofline_from_prof(prof, workload=args.workload, batch_mbp=args.batch_mbp),
         "path_roofline": path_roofline(prof, args.steps, step, total_bases, total_bases, n_lines, len(ix.parts), comm.world),
     }
     if comm.rank == 0 and comm.world == 1 and not args.no_cpu:   # the CPU leg runs at N=1 only
@@ -413,7 +416,7 @@ def bench_screen(args, comm, gpu, torch):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
             "mbp_per_s": comm.world * ss.total_bases / 1e6 / step,
             "config": {"workload": f"C2 screen: {ss.n} contigs / {ss.total_bases/1e6:.1f} Mbp vs {db.n_refs} refs x 1000"},
-            "roofline": roofline_from_prof(prof, "screen_count")}
+            "roofline": roofline_from_prof(prof, "screen_count", workload="screen")}
 
 
 def launch_ranks(n: int) -> int:

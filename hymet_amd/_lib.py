@@ -34,6 +34,7 @@ _SIGS = {
     "hymet_fasta_names": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
     "hymet_fasta_compact": (_i32, [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp]),
     "hymet_name_hash": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp]),
+    "hymet_sort_pairs_u64": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32]),
     "hymet_msh_open": (_i32, [_c.c_char_p, _c.POINTER(_vp)]),
     "hymet_msh_info_get": (_i32, [_vp, _vp]),
     "hymet_msh_copy": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -13,7 +13,6 @@
 #include "common.hpp"
 #include "mm_common.hpp"
 
-#include <rocprim/device/device_scan.hpp>
 
 namespace {
 

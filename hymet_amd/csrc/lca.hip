@@ -16,9 +16,8 @@
 // "dicts" are arrays in a per-query scratch slice sized by its line count.
 #include "common.hpp"
 #include "mm_common.hpp"
+#include "sort.hpp"
 
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
 
 namespace {
 
@@ -297,12 +296,15 @@ int hymet_acc_classify(hymet_ctx *ctx, const hymet_paf_acc *acc, int mode, int32
     hipLaunchKernelGGL(acc_keys_kernel, dim3(gq), dim3(256), 0, st, first.as<int32_t>(), n_q, key.as<uint64_t>(),
                        nr.as<int32_t>());
     HY_CHECK_LAUNCH("acc_keys_kernel");
-    {
-        size_t tb = 0;
-        HY_HIP(rocprim::radix_sort_keys(nullptr, tb, key.as<uint64_t>(), key2.as<uint64_t>(), (size_t)n_q, 0, 64, st));
-        DevBuf tmp;
-        HY_HIP(tmp.alloc(tb, st));
-        HY_HIP(rocprim::radix_sort_keys(tmp.p, tb, key.as<uint64_t>(), key2.as<uint64_t>(), (size_t)n_q, 0, 64, st));
+    uint64_t *sorted_key = key.as<uint64_t>();
+    {  // rows by (first part, query); the values ride along unused
+        DevBuf dv, dv2;
+        HY_HIP(dv.alloc(4 * (size_t)n_q, st));
+        HY_HIP(dv2.alloc(4 * (size_t)n_q, st));
+        uint64_t *kka = key2.as<uint64_t>();
+        uint32_t *vv = dv.as<uint32_t>(), *vva = dv2.as<uint32_t>();
+        const int rc = hymet::mm::radix_sort_pairs(ctx, sorted_key, kka, vv, vva, n_q, 0, 64);
+        if (rc) return rc;
     }
     int32_t R = 0;
     HY_HIP(hipMemcpyAsync(&R, nr.p, 4, hipMemcpyDeviceToHost, st));
@@ -313,7 +315,7 @@ int hymet_acc_classify(hymet_ctx *ctx, const hymet_paf_acc *acc, int mode, int32
     HY_HIP(row_of.alloc(4 * (size_t)n_q, st));
     HY_HIP(row_cnt.alloc(4 * (size_t)(R + 1), st));
     HY_HIP(row_off.alloc(8 * (size_t)(R + 1), st));
-    hipLaunchKernelGGL(acc_rows_kernel, dim3((unsigned)hymet::cdiv(R, 256)), dim3(256), 0, st, key2.as<uint64_t>(), R,
+    hipLaunchKernelGGL(acc_rows_kernel, dim3((unsigned)hymet::cdiv(R, 256)), dim3(256), 0, st, sorted_key, R,
                        cnt.as<uint32_t>(), d_row_q, d_row_part, row_of.as<int32_t>(), row_cnt.as<uint32_t>());
     HY_CHECK_LAUNCH("acc_rows_kernel");
     {
@@ -332,20 +334,17 @@ int hymet_acc_classify(hymet_ctx *ctx, const hymet_paf_acc *acc, int mode, int32
     HY_CHECK_LAUNCH("acc_line_keys_kernel");
     int bits = 1;
     while ((1ll << bits) < R) bits++;
+    uint32_t *sorted_v = lv.as<uint32_t>();
     {
-        size_t tb = 0;
-        HY_HIP(rocprim::radix_sort_pairs(nullptr, tb, lk.as<uint32_t>(), lk2.as<uint32_t>(), lv.as<uint32_t>(),
-                                         lv2.as<uint32_t>(), (size_t)n, 0, bits, st));
-        DevBuf tmp;
-        HY_HIP(tmp.alloc(tb, st));
-        HY_HIP(rocprim::radix_sort_pairs(tmp.p, tb, lk.as<uint32_t>(), lk2.as<uint32_t>(), lv.as<uint32_t>(),
-                                         lv2.as<uint32_t>(), (size_t)n, 0, bits, st));
+        uint32_t *kk = lk.as<uint32_t>(), *kka = lk2.as<uint32_t>(), *vva = lv2.as<uint32_t>();
+        const int rc = hymet::mm::radix_sort_pairs(ctx, kk, kka, sorted_v, vva, n, 0, bits);
+        if (rc) return rc;
     }
     HY_HIP(lt.alloc(4 * (size_t)n, st));
     HY_HIP(lb.alloc(8 * (size_t)n, st));
     HY_HIP(lq.alloc(8 * (size_t)n, st));
     HY_HIP(le.alloc((size_t)n, st));
-    AccLineParams A{lv2.as<uint32_t>(), n, acc->regs.as<hymet_mm_reg>(), acc->q.as<int32_t>(), acc->t.as<int32_t>(), d_qlen,
+    AccLineParams A{sorted_v, n, acc->regs.as<hymet_mm_reg>(), acc->q.as<int32_t>(), acc->t.as<int32_t>(), d_qlen,
                     mode, d_qname_pool, d_qname_off, d_tname_pool, d_tname_off, lt.as<int32_t>(), lb.as<int64_t>(),
                     lq.as<int64_t>(), le.as<uint8_t>()};
     hipLaunchKernelGGL(acc_line_gather_kernel, dim3(gl), dim3(256), 0, st, A);

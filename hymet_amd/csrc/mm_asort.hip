@@ -26,6 +26,7 @@
 // falls back to the device sort of the whole batch (return 1) when the packed words would
 // not fit 64 bits.
 #include "mm_common.hpp"
+#include "sort.hpp"
 
 namespace hymet {
 namespace mm {
@@ -622,7 +623,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     if (hg[kLarge] > 0) {
         const int nbig = hg[kLarge];
         const Seg *big = glists.as<Seg>() + kLarge * (size_t)G;
-        DevBuf blen, bdst, tk, tk2, tv, tv2, tmp;
+        DevBuf blen, bdst, tk, tk2, tv, tv2;
         HY_HIP(blen.alloc(4 * (size_t)(nbig + 1), st));
         HY_HIP(bdst.alloc(8 * (size_t)(nbig + 1), st));
         hipLaunchKernelGGL(seg_len_kernel, dim3((unsigned)cdiv(nbig, 256)), dim3(256), 0, st, big, nbig, blen.as<uint32_t>());
@@ -639,14 +640,12 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
         HY_CHECK_LAUNCH("big_gather_kernel");
         const int end_bit = gb + bits_of(nbig);
         HY_ARG(end_bit <= 64, "grouped_anchor_sort: group rank and key bits exceed 64");
-        size_t tb = 0;
-        HY_HIP(rocprim::radix_sort_pairs(nullptr, tb, tk.as<uint64_t>(), tk2.as<uint64_t>(), tv.as<uint32_t>(), tv2.as<uint32_t>(),
-                                         (size_t)NB, 0, end_bit, st));
-        HY_HIP(tmp.alloc(tb, st));
-        HY_HIP(rocprim::radix_sort_pairs(tmp.p, tb, tk.as<uint64_t>(), tk2.as<uint64_t>(), tv.as<uint32_t>(), tv2.as<uint32_t>(),
-                                         (size_t)NB, 0, end_bit, st));
+        uint64_t *kk = tk.as<uint64_t>(), *kka = tk2.as<uint64_t>();
+        uint32_t *vv = tv.as<uint32_t>(), *vva = tv2.as<uint32_t>();
+        rc = radix_sort_pairs(ctx, kk, kka, vv, vva, NB, 0, end_bit);
+        if (rc) return rc;
         hipLaunchKernelGGL(big_put_kernel, dim3((unsigned)nbig), dim3(256), 0, st, big, bdst.as<int64_t>(), gb, okey,
-                           tk2.as<uint64_t>(), tv2.as<uint32_t>(), out);
+                           kk, vv, out);
         HY_CHECK_LAUNCH("big_put_kernel");
     }
     return HYMET_OK;

@@ -3,8 +3,6 @@
 #include "common.hpp"
 
 #include <cstring>
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
 #include <vector>
 
 namespace hymet {
@@ -100,6 +98,10 @@ int exclusive_scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int
 // the same, asynchronous: `part` (scratch, kept alive by the caller) ends with the total at
 // index ceil(n / 4096)
 int scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, DevBuf &part);
+// exclusive scan of n uint64 values (asynchronous; part ends with the total at ceil(n / 4096))
+int scan_u64(hymet_ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n, DevBuf &part);
+// inclusive running maximum of n int32 values (asynchronous)
+int inclusive_max_scan_i32(hymet_ctx *ctx, const int32_t *in, int32_t *out, int64_t n, DevBuf &part);
 
 // Per-query grouped sort of anchor keys (mm_asort.hip): key/val (n, query-major, query offsets
 // d_qoff[n_q + 1]) into the sorted anchor set okey (k1) / ax / ay (oval: scratch).  Returns 1

@@ -15,17 +15,12 @@
 //     mm_filter_strand_retained, mm_set_mapq
 // Canonical tie-breaks T1-T4 are those of oracle/mm_oracle.c.
 #include "mm_common.hpp"
+#include "sort.hpp"
 
 #include <algorithm>
 #include <type_traits>
 #include <utility>
 
-#ifndef HYMET_ANCHOR_RB  // digit bits of the anchor-key radix sort (0: rocPRIM's default, 8)
-#define HYMET_ANCHOR_RB 0
-#endif
-#ifndef HYMET_ANCHOR_HIST_BLOCK
-#define HYMET_ANCHOR_HIST_BLOCK 512
-#endif
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -1029,31 +1024,14 @@ struct PhaseTrace {
     }
 };
 
-// RB > 0: onesweep with RB-bit digits (fewer passes over the data) instead of rocPRIM's
-// gfx950 default (8)
-template <int RB>
-using OnesweepCfg = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<HYMET_ANCHOR_HIST_BLOCK, 16>, rocprim::kernel_config<512, 16>,
-                                        RB, rocprim::block_radix_rank_algorithm::match>>;
-
+// the library's stable LSD radix sort (sort.hpp), profiled under `tag`; keys / vals point at
+// the sorted data on return
 template <typename K, typename V, int RB = 0>
 static int sort_pairs(hymet_ctx *ctx, K *&keys, K *&keys_alt, V *&vals, V *&vals_alt, int64_t n, int begin_bit, int end_bit,
                       const char *tag = "radix_sort") {
     if (n <= 1) return HYMET_OK;
-    const int digit = RB > 0 ? RB : 8;
-    ProfScope _ps(ctx, tag, 2.0 * (double)n * (sizeof(K) + sizeof(V)) * (double)((end_bit - begin_bit + digit - 1) / digit));
-    using Cfg = std::conditional_t<(RB > 0), OnesweepCfg<(RB > 0 ? RB : 8)>, rocprim::default_config>;
-    size_t tmp = 0;
-    HY_HIP(rocprim::radix_sort_pairs<Cfg>(nullptr, tmp, keys, keys_alt, vals, vals_alt, (size_t)n, begin_bit, end_bit,
-                                          ctx->stream));
-    DevBuf t;
-    HY_HIP(t.alloc(tmp, ctx->stream));
-    HY_HIP(rocprim::radix_sort_pairs<Cfg>(t.p, tmp, keys, keys_alt, vals, vals_alt, (size_t)n, begin_bit, end_bit,
-                                          ctx->stream));
-    std::swap(keys, keys_alt);
-    std::swap(vals, vals_alt);
-    return HYMET_OK;
+    ProfScope _ps(ctx, tag, 2.0 * (double)n * (sizeof(K) + sizeof(V)) * (double)((end_bit - begin_bit + 7) / 8));
+    return radix_sort_pairs(ctx, keys, keys_alt, vals, vals_alt, n, begin_bit, end_bit);
 }
 
 static int scan_flags(hymet_ctx *ctx, const uint32_t *flag, int64_t n, DevBuf &pos, int64_t *total) {
@@ -1155,7 +1133,7 @@ static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n,
         if (rc == HYMET_OK) return HYMET_OK;
         if (rc != 1) return rc;
     }
-    int rc = sort_pairs<uint64_t, uint32_t, HYMET_ANCHOR_RB>(ctx, kk, kka, vv, vva, n, 0, end_bit, "radix_sort_anchors");
+    int rc = sort_pairs<uint64_t, uint32_t>(ctx, kk, kka, vv, vva, n, 0, end_bit, "radix_sort_anchors");
     if (rc) return rc;
     {
         ProfScope _ps(ctx, "mm_anchor_unpack", 28.0 * (double)n);  // key + value read, x + y write
@@ -1724,14 +1702,10 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
         HY_HIP(rank.alloc(8 * (size_t)(M + 1), st));
         LAUNCH1(seed_class_kernel, M, seed_n.as<uint32_t>(), M, opt->mid_occ, cls.as<uint64_t>());
         HY_HIP(hipMemsetAsync(cls.as<uint64_t>() + M, 0, 8, st));
+        DevBuf spart;
         {  // exclusive scan of packed (low, high) counts over M + 1 entries: rank[M] = totals
-            size_t tmp = 0;
-            HY_HIP(rocprim::exclusive_scan(nullptr, tmp, cls.as<uint64_t>(), rank.as<uint64_t>(), (uint64_t)0,
-                                           (size_t)(M + 1), rocprim::plus<uint64_t>(), st));
-            DevBuf t;
-            HY_HIP(t.alloc(tmp, st));
-            HY_HIP(rocprim::exclusive_scan(t.p, tmp, cls.as<uint64_t>(), rank.as<uint64_t>(), (uint64_t)0,
-                                           (size_t)(M + 1), rocprim::plus<uint64_t>(), st));
+            rc = scan_u64(ctx, cls.as<uint64_t>(), rank.as<uint64_t>(), M + 1, spart);
+            if (rc) return rc;
         }
         uint64_t tot = 0;
         HY_HIP(hipMemcpyAsync(&tot, rank.as<uint64_t>() + M, 8, hipMemcpyDeviceToHost, st));
@@ -1753,13 +1727,9 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
             HY_HIP(pmax.alloc(4 * (size_t)n_high, st));
             LAUNCH1(flt_mark_kernel, n_high, flt_high.as<uint32_t>(), n_high, vmax.as<int32_t>());
             {
-                size_t tmp = 0;
-                HY_HIP(rocprim::inclusive_scan(nullptr, tmp, vmax.as<int32_t>(), pmax.as<int32_t>(), (size_t)n_high,
-                                               rocprim::maximum<int32_t>(), st));
-                DevBuf t;
-                HY_HIP(t.alloc(tmp, st));
-                HY_HIP(rocprim::inclusive_scan(t.p, tmp, vmax.as<int32_t>(), pmax.as<int32_t>(), (size_t)n_high,
-                                               rocprim::maximum<int32_t>(), st));
+                DevBuf mpart;
+                rc = inclusive_max_scan_i32(ctx, vmax.as<int32_t>(), pmax.as<int32_t>(), n_high, mpart);
+                if (rc) return rc;
             }
             LAUNCH1(rep_len_kernel, n_high, flt_high.as<uint32_t>(), pmax.as<int32_t>(), high_idx.as<int32_t>(), n_high,
                     mx.as<uint64_t>(), my.as<uint64_t>(), qid.as<uint32_t>(), rep_len.as<int32_t>(), seed_n.as<uint32_t>());

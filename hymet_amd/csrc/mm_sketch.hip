@@ -20,6 +20,11 @@
 // two adjacent loads instead of a hash-table probe chain.
 #include "mm_common.hpp"
 
+// the cold index build keeps rocPRIM's onesweep for its one-off sorts of every reference
+// minimizer (hundreds of millions); the warm mapping path uses the library's own sort.hpp
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>

@@ -144,7 +144,146 @@ __global__ __launch_bounds__(kScanBlock) void scan_down_kernel(const uint32_t *_
     }
 }
 
+// uint64 -> uint64 variant (packed counters, e.g. two 32-bit counts per word): thread t of a
+// tile owns 16 consecutive entries
+__global__ __launch_bounds__(kScanBlock) void scan_reduce64_kernel(const uint64_t *__restrict__ in, int64_t n,
+                                                                   uint64_t *__restrict__ part) {
+    __shared__ uint64_t ws[kScanBlock / 64];
+    const int64_t b = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) s += b + j < n ? in[b + j] : 0ull;
+    uint64_t total;
+    (void)block_excl<kScanBlock / 64>(s, ws, &total);
+    if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_down64_kernel(const uint64_t *__restrict__ in, int64_t n,
+                                                                 const uint64_t *__restrict__ part,
+                                                                 uint64_t *__restrict__ out) {
+    __shared__ uint64_t ws[kScanBlock / 64];
+    const int64_t b = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+    uint64_t v[kScanItems], s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        v[j] = b + j < n ? in[b + j] : 0ull;
+        s += v[j];
+    }
+    uint64_t total;
+    uint64_t run = part[blockIdx.x] + block_excl<kScanBlock / 64>(s, ws, &total);
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        if (b + j < n) out[b + j] = run;
+        run += v[j];
+    }
+}
+
+// inclusive running maximum of int32 values: per-tile maxima, one block scanning them
+// (exclusive, seeded with INT32_MIN), then every tile re-scanned with its carry
+__device__ __forceinline__ int32_t wave_incl_max(int32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int32_t o = __shfl_up(v, d, 64);
+        if (lane >= d) v = max(v, o);
+    }
+    return v;
+}
+
+// exclusive block max-scan of one value per thread (INT32_MIN before the first); *all = block max
+template <int NW>
+__device__ __forceinline__ int32_t block_excl_max(int32_t v, int32_t *ws, int32_t *all) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int32_t inc = wave_incl_max(v);
+    if (lane == 63) ws[w] = inc;
+    __syncthreads();
+    int32_t before = INT32_MIN, a = INT32_MIN;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        if (i < w) before = max(before, ws[i]);
+        a = max(a, ws[i]);
+    }
+    __syncthreads();
+    *all = a;
+    int32_t ex = __shfl_up(inc, 1, 64);
+    if (lane == 0) ex = INT32_MIN;
+    return max(before, ex);
+}
+
+__global__ __launch_bounds__(kScanBlock) void max_reduce_kernel(const int32_t *__restrict__ in, int64_t n,
+                                                                int32_t *__restrict__ part) {
+    __shared__ int32_t ws[kScanBlock / 64];
+    const int64_t b = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+    int32_t m = INT32_MIN;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++)
+        if (b + j < n) m = max(m, in[b + j]);
+    int32_t all;
+    (void)block_excl_max<kScanBlock / 64>(m, ws, &all);
+    if (threadIdx.x == 0) part[blockIdx.x] = all;
+}
+
+__global__ __launch_bounds__(1024) void max_parts_kernel(int32_t *part, int64_t nb) {
+    __shared__ int32_t ws[16];
+    int32_t carry = INT32_MIN;
+    for (int64_t b0 = 0; b0 < nb; b0 += 1024) {
+        const int64_t b = b0 + threadIdx.x;
+        const int32_t v = b < nb ? part[b] : INT32_MIN;
+        int32_t all;
+        const int32_t ex = block_excl_max<16>(v, ws, &all);
+        if (b < nb) part[b] = max(carry, ex);
+        carry = max(carry, all);
+    }
+}
+
+__global__ __launch_bounds__(kScanBlock) void max_down_kernel(const int32_t *__restrict__ in, int64_t n,
+                                                              const int32_t *__restrict__ part, int32_t *__restrict__ out) {
+    __shared__ int32_t ws[kScanBlock / 64];
+    const int64_t b = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+    int32_t v[kScanItems], m = INT32_MIN;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        v[j] = b + j < n ? in[b + j] : INT32_MIN;
+        m = max(m, v[j]);
+    }
+    int32_t all;
+    int32_t run = max(part[blockIdx.x], block_excl_max<kScanBlock / 64>(m, ws, &all));
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        run = max(run, v[j]);
+        if (b + j < n) out[b + j] = run;
+    }
+}
+
 }  // namespace
+
+int inclusive_max_scan_i32(hymet_ctx *ctx, const int32_t *in, int32_t *out, int64_t n, DevBuf &part) {
+    if (n <= 0) return HYMET_OK;
+    hipStream_t st = ctx->stream;
+    const int64_t nb = cdiv(n, kScanTile);
+    HY_HIP(part.alloc(4 * (size_t)(nb + 1), st));
+    hipLaunchKernelGGL(max_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<int32_t>());
+    HY_CHECK_LAUNCH("max_reduce_kernel");
+    hipLaunchKernelGGL(max_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<int32_t>(), nb);
+    HY_CHECK_LAUNCH("max_parts_kernel");
+    hipLaunchKernelGGL(max_down_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<int32_t>(), out);
+    HY_CHECK_LAUNCH("max_down_kernel");
+    return HYMET_OK;
+}
+
+int scan_u64(hymet_ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n, DevBuf &part) {
+    if (n <= 0) return HYMET_OK;
+    hipStream_t st = ctx->stream;
+    const int64_t nb = cdiv(n, kScanTile);
+    HY_HIP(part.alloc(8 * (size_t)(nb + 1), st));
+    hipLaunchKernelGGL(scan_reduce64_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>());
+    HY_CHECK_LAUNCH("scan_reduce64_kernel");
+    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<uint64_t>(), nb);
+    HY_CHECK_LAUNCH("scan_parts_kernel");
+    hipLaunchKernelGGL(scan_down64_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(), out);
+    HY_CHECK_LAUNCH("scan_down64_kernel");
+    return HYMET_OK;
+}
 
 int scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, DevBuf &part) {
     if (n <= 0) return HYMET_OK;
@@ -176,3 +315,28 @@ int exclusive_scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int
 
 }  // namespace mm
 }  // namespace hymet
+
+// ---- C ABI: the library's radix sort, for tests and callers that sort packed keys
+#include "sort.hpp"
+
+extern "C" int hymet_sort_pairs_u64(hymet_ctx *ctx, uint64_t *d_keys, uint32_t *d_vals, int64_t n, int begin_bit,
+                                    int end_bit) {
+    HY_ARG(ctx && (n == 0 || (d_keys && d_vals)), "hymet_sort_pairs_u64: null argument");
+    HY_ARG(begin_bit >= 0 && end_bit <= 64 && begin_bit <= end_bit, "hymet_sort_pairs_u64: bad bit range");
+    if (n <= 1) return HYMET_OK;
+    HY_HIP(hipSetDevice(ctx->device));
+    using namespace hymet::mm;
+    DevBuf k2, v2;
+    HY_HIP(k2.alloc(8 * (size_t)n, ctx->stream));
+    HY_HIP(v2.alloc(4 * (size_t)n, ctx->stream));
+    uint64_t *kk = d_keys, *kka = k2.as<uint64_t>();
+    uint32_t *vv = d_vals, *vva = v2.as<uint32_t>();
+    const int rc = radix_sort_pairs(ctx, kk, kka, vv, vva, n, begin_bit, end_bit);
+    if (rc) return rc;
+    if (kk != d_keys) {
+        HY_HIP(hipMemcpyAsync(d_keys, kk, 8 * (size_t)n, hipMemcpyDeviceToDevice, ctx->stream));
+        HY_HIP(hipMemcpyAsync(d_vals, vv, 4 * (size_t)n, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    HY_HIP(hipStreamSynchronize(ctx->stream));
+    return HYMET_OK;
+}

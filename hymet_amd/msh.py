@@ -183,10 +183,12 @@ class _Struct:
         return [_Struct(self.m, s, t + 1 + j * step, dw, npt) for j in range(cnt)]
 
 
-def read_msh(path, threads: int = 16) -> SketchDB:
+def read_msh(path, threads: int = 16, alloc=None) -> SketchDB:
     """.msh -> SketchDB through the library's native reader (hymet_msh_*: mmap, pointer walk
     and a threaded hash gather; S1 of SURVEY.md §8a, on the timed path since `mash screen`
-    reads its DB on every call).  The library is required, like every product path."""
+    reads its DB on every call).  alloc(n) may supply the uint64 array the hashes are
+    gathered into (e.g. a view of pinned memory, so the table upload is one DMA).  The
+    library is required, like every product path."""
     import ctypes
     from ._lib import check, load
     lib = load()
@@ -198,7 +200,7 @@ def read_msh(path, threads: int = 16) -> SketchDB:
         b = bytes(raw)
         k, win, ss, seed, nonc, pc, use64 = struct.unpack_from("<iiiIiii", b, 0)
         n_refs, n_hashes, nb, cb, al = struct.unpack_from("<qqqqq", b, 32)
-        hashes = np.empty(max(n_hashes, 1), np.uint64)
+        hashes = alloc(max(n_hashes, 1)) if alloc is not None else np.empty(max(n_hashes, 1), np.uint64)
         offsets = np.empty(n_refs + 1, np.int64)
         lengths = np.empty(max(n_refs, 1), np.int64)
         names = ctypes.create_string_buffer(max(nb, 1))

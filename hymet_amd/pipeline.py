@@ -262,6 +262,7 @@ class Pipeline:
         self.ref_lookup = ref_lookup
         self.taxonomy, self.hierarchy, self.variant = taxonomy, hierarchy, variant
         self.timings: Dict[str, float] = {}   # host wall seconds of the last run's input loads
+        self._pin: Dict[int, object] = {}     # pinned host buffers of the DB hashes (S1 upload)
         self._load_classifier()
         if self.db_paths:
             self._load_dbs()
@@ -273,12 +274,23 @@ class Pipeline:
         self._bufs: Dict[str, object] = {}
         self._ran = False   # the constructor's loads serve the first run
 
+    def _pinned_hashes(self, i, n):
+        """Reusable pinned host buffer for DB i's hashes (grown, never shrunk)."""
+        torch = self.gpu.torch
+        b = self._pin.get(i)
+        if b is None or b.numel() < n:
+            b = torch.empty(int(n), dtype=torch.int64, pin_memory=True)
+            self._pin[i] = b
+        return b
+
     def _load_dbs(self):
-        """S1: each sketch DB file parsed (csrc/msh.cpp) and its hash table built in HBM."""
+        """S1: each sketch DB file parsed (csrc/msh.cpp), its hashes gathered into pinned
+        memory and uploaded by DMA, and its hash table built in HBM."""
         t0 = time.perf_counter()
-        self.dbs = [read_msh(p) for p in self.db_paths]
+        self.dbs = [read_msh(p, alloc=lambda n, i=i: self._pinned_hashes(i, n).numpy().view(np.uint64)[:n])
+                    for i, p in enumerate(self.db_paths)]
         t1 = time.perf_counter()
-        self.tables = [scr.ScreenTable(self.gpu, db) for db in self.dbs]
+        self.tables = [scr.ScreenTable(self.gpu, db, pinned=self._pin[i]) for i, db in enumerate(self.dbs)]
         self.gpu.sync()
         self.timings["msh_read_s"] = t1 - t0
         self.timings["screen_table_s"] = time.perf_counter() - t1

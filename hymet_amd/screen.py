@@ -28,7 +28,9 @@ U64_MAX = (1 << 64) - 1
 class ScreenTable:
     """One sketch DB resident in HBM: open-addressing key table + slot map + CSR offsets."""
 
-    def __init__(self, gpu, db: SketchDB):
+    def __init__(self, gpu, db: SketchDB, pinned=None):
+        """pinned: a pinned host int64 tensor whose first len(db.hashes) entries ARE the
+        hashes (read_msh gathered them there): uploaded by one asynchronous DMA."""
         torch = gpu.torch
         self.gpu, self.db = gpu, db
         n = int(len(db.hashes))
@@ -36,7 +38,12 @@ class ScreenTable:
         self.n_slots = int(gpu.lib.hymet_screen_table_slots(n))
         self.keys = gpu.empty(self.n_slots, torch.int64)
         self.slot_of = gpu.empty(max(n, 1), torch.int64)
-        d_h = torch.from_numpy(np.ascontiguousarray(db.hashes).view(np.int64)).to(gpu.dev) if n else gpu.empty(1, torch.int64)
+        if not n:
+            d_h = gpu.empty(1, torch.int64)
+        elif pinned is not None:
+            d_h = pinned[:n].to(gpu.dev, non_blocking=True)
+        else:
+            d_h = torch.from_numpy(np.ascontiguousarray(db.hashes).view(np.int64)).to(gpu.dev)
         gpu.call("hymet_screen_table_build", ptr(d_h), n, ptr(self.keys), self.n_slots, ptr(self.slot_of))
         self.ref_off = torch.from_numpy(np.ascontiguousarray(db.offsets, dtype=np.int64)).to(gpu.dev)
         del d_h

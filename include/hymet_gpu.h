@@ -110,6 +110,11 @@ int64_t hymet_screen_table_slots(int64_t n_hashes);
  * the reserved all-ones key).  Resets d_keys itself. */
 int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n_hashes,
                              uint64_t *d_keys, int64_t n_slots, int64_t *d_slot_of);
+/* The library's stable LSD radix sort (8-bit digits) of device (key, value) pairs by key bits
+ * [begin_bit, end_bit), in place (the sort behind the mapper's minimizer, group, chain and
+ * anchor-segment orders and the LCA row order; no rocPRIM on the mapping path). */
+int hymet_sort_pairs_u64(hymet_ctx *ctx, uint64_t *d_keys, uint32_t *d_vals, int64_t n, int begin_bit, int end_bit);
+
 /* ---- Mash sketch databases (.msh) ----
  * Replaces the .msh load inside `mash screen` (scripts/mash.sh:14; the DB files of
  * run_hymet_cami.sh:52,85-97 and main.pl:44-46): the Cap'n Proto MinHash message is mapped

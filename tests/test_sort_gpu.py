@@ -1,0 +1,35 @@
+"""The library's stable LSD radix sort (csrc/sort.hpp, hymet_sort_pairs_u64) vs numpy's
+stable argsort on the key bits [begin, end): every tile-boundary size, partial bit ranges
+(bits outside the range are ignored, as the callers rely on), heavy ties (stability)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    from hymet_amd._lib import Gpu
+    return Gpu(0)
+
+
+@pytest.mark.parametrize("n,begin,end,distinct", [(2, 0, 64, 0), (2047, 0, 64, 0), (2048, 0, 40, 0), (2049, 0, 16, 50),
+                                                   (100_000, 8, 40, 0), (1_000_003, 0, 64, 1000), (300_000, 0, 3, 0),
+                                                   (5_000_000, 0, 38, 0)])
+def test_radix_sort_matches_stable_argsort(gpu, n, begin, end, distinct):
+    torch = gpu.torch
+    rng = np.random.default_rng(n + end)
+    keys = rng.integers(0, 2 ** 63, n, dtype=np.int64).astype(np.uint64) * np.uint64(2) + np.uint64(rng.integers(0, 2))
+    if distinct:
+        keys = rng.choice(keys[:distinct], n)
+    vals = np.arange(n, dtype=np.uint32)
+    dk = torch.from_numpy(keys.view(np.int64)).to(gpu.dev)
+    dv = torch.from_numpy(vals.view(np.int32)).to(gpu.dev)
+    gpu.call("hymet_sort_pairs_u64", ctypes.c_void_p(dk.data_ptr()), ctypes.c_void_p(dv.data_ptr()), n, begin, end)
+    mask = np.uint64(((1 << (end - begin)) - 1) if end - begin < 64 else (1 << 64) - 1)
+    sub = (keys >> np.uint64(begin)) & mask
+    order = np.argsort(sub, kind="stable")
+    np.testing.assert_array_equal(dv.cpu().numpy().view(np.uint32), order.astype(np.uint32))
+    np.testing.assert_array_equal(dk.cpu().numpy().view(np.uint64), keys[order])
