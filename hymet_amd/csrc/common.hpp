@@ -20,6 +20,14 @@ struct hymet_ctx {
     // pinned staging for hymet_copy_to_host (two chunks, allocated on first use)
     void *stage[2] = {nullptr, nullptr};
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    // mailbox: pinned, device-mapped, coherent host words that kernels store small results
+    // into (scan totals, list counts, maxima) -- read on the host after a stream sync, with
+    // no copy dispatch (hymet::mb_dev / mb_read)
+    int64_t *mbox_h = nullptr;
+    int64_t *mbox_d = nullptr;
+    // device counters that kernels leave zeroed (hymet::mm::publish_counters), so counting
+    // kernels need no memset before them
+    int32_t *dctr = nullptr;
 };
 
 namespace hymet {
@@ -41,6 +49,14 @@ struct ProfScope {
         }
     }
 };
+}  // namespace hymet
+
+namespace hymet {
+constexpr int kMbox = 64;  // mailbox words per context
+// device address of mailbox word i (kernels store into it)
+inline int64_t *mb_dev(hymet_ctx *c, int i) { return c->mbox_d + i; }
+// host read of mailbox word i, after the stream has been synchronised
+inline int64_t mb_read(const hymet_ctx *c, int i) { return __atomic_load_n(c->mbox_h + i, __ATOMIC_ACQUIRE); }
 }  // namespace hymet
 
 namespace hymet {

@@ -142,7 +142,16 @@ int hymet_init(int device, hymet_ctx **out) {
     c->n_cu = prop.multiProcessorCount;
     HY_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->own_stream = true;
-
+    if (hipHostMalloc((void **)&c->mbox_h, 8 * hymet::kMbox, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&c->mbox_d, c->mbox_h, 0) != hipSuccess) {
+        hymet_destroy(c);
+        return hymet::fail(HYMET_E_HIP, "hymet_init: mailbox allocation failed");
+    }
+    for (int i = 0; i < hymet::kMbox; i++) c->mbox_h[i] = 0;
+    if (hipMalloc((void **)&c->dctr, 4 * hymet::kMbox) != hipSuccess || hipMemset(c->dctr, 0, 4 * hymet::kMbox) != hipSuccess) {
+        hymet_destroy(c);
+        return hymet::fail(HYMET_E_HIP, "hymet_init: counter allocation failed");
+    }
     *out = c;
     return HYMET_OK;
 }
@@ -154,6 +163,8 @@ int hymet_destroy(hymet_ctx *ctx) {
         if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);
         if (ctx->stage_ev[k]) (void)hipEventDestroy(ctx->stage_ev[k]);
     }
+    if (ctx->mbox_h) (void)hipHostFree(ctx->mbox_h);
+    if (ctx->dctr) (void)hipFree(ctx->dctr);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return HYMET_OK;

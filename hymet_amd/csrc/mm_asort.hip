@@ -105,7 +105,7 @@ __device__ __forceinline__ void block_append(const Seg (&sg)[ITEMS], const int (
 
 // queries by size class (large: tiles counted)
 __global__ __launch_bounds__(256) void query_class_kernel(const int64_t *qoff, int n_q, Seg *lists, int64_t cap, int32_t *cnt,
-                                                          uint32_t *nt) {
+                                                          uint32_t *nt, int64_t *mail) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     const bool ok = q < n_q;
     const int64_t s = ok ? qoff[q] : 0, n = ok ? qoff[q + 1] - s : 0;
@@ -113,6 +113,7 @@ __global__ __launch_bounds__(256) void query_class_kernel(const int64_t *qoff, i
     const Seg sg[1] = {Seg{s, (int32_t)n, q}};
     const int cls[1] = {n > 0 ? seg_class(n) : -1};
     block_append<1>(sg, cls, lists, cap, cnt);
+    publish_counters(cnt, kClasses, mail);
 }
 
 // LDS atomicAdd(&h[bin], 1) for the active lanes, returning the old values: the lanes of up
@@ -170,7 +171,8 @@ __global__ __launch_bounds__(256) void tile_hist_kernel(const uint64_t *__restri
 // one block per large query: H[t][b] <- offset (within the query) of tile t's bin-b run;
 // every non-empty bin appended to the group list
 __global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const int64_t *tpos, int nbins,
-                                                         uint32_t *__restrict__ H, Seg *groups, int32_t *n_groups) {
+                                                         uint32_t *__restrict__ H, Seg *groups, int32_t *n_groups,
+                                                         int64_t *mail) {
     __shared__ uint32_t part[256];
     __shared__ uint32_t carry;
     const Seg S = large[blockIdx.x];
@@ -208,6 +210,7 @@ __global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const
         if (threadIdx.x == 255) carry += part[255];
         __syncthreads();
     }
+    publish_counters(n_groups, 1, mail);
 }
 
 // The scatter of a large query's tile to its (tile, bin) runs.  Consecutive anchors of a tile
@@ -294,7 +297,8 @@ __global__ __launch_bounds__(256) void tile_scatter_kernel(const uint64_t *__res
 
 // groups by size class, 4 per thread; a single-anchor group is final where the scatter put it
 __global__ __launch_bounds__(256) void group_class_kernel(const Seg *groups, int64_t G, Seg *lists, int64_t cap, int32_t *cnt,
-                                                          const uint64_t *key, const uint32_t *val, AnchorOut out) {
+                                                          const uint64_t *key, const uint32_t *val, AnchorOut out,
+                                                          int64_t *mail) {
     Seg sg[4];
     int cls[4];
 #pragma unroll
@@ -305,6 +309,7 @@ __global__ __launch_bounds__(256) void group_class_kernel(const Seg *groups, int
         cls[j] = sg[j].n > 1 ? seg_class(sg[j].n) : -1;
     }
     block_append<4>(sg, cls, lists, cap, cnt);
+    publish_counters(cnt, kClasses, mail);
 }
 
 // one thread per segment of <= 8 anchors: sorting network on (key, y) in registers
@@ -557,17 +562,15 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     hipStream_t st = ctx->stream;
     const AnchorOut out{ax, ay, rb, pb, yhi};
     // 1 queries by size
-    DevBuf qlists, qcnt, nt;
+    DevBuf qlists, nt;
     HY_HIP(qlists.alloc(sizeof(Seg) * kClasses * (size_t)n_q, st));
-    HY_HIP(qcnt.alloc(4 * kClasses, st));
     HY_HIP(nt.alloc(4 * (size_t)(n_q + 1), st));
-    HY_HIP(hipMemsetAsync(qcnt.p, 0, 4 * kClasses, st));
     hipLaunchKernelGGL(query_class_kernel, dim3((unsigned)cdiv(n_q, 256)), dim3(256), 0, st, d_qoff, n_q, qlists.as<Seg>(),
-                       (int64_t)n_q, qcnt.as<int32_t>(), nt.as<uint32_t>());
+                       (int64_t)n_q, ctx->dctr + kCtrQClass, nt.as<uint32_t>(), mb_dev(ctx, kMbQClass));
     HY_CHECK_LAUNCH("query_class_kernel");
-    int32_t hq[kClasses] = {};
-    HY_HIP(hipMemcpyAsync(hq, qcnt.p, 4 * kClasses, hipMemcpyDeviceToHost, st));
     HY_HIP(hipStreamSynchronize(st));
+    int32_t hq[kClasses] = {};
+    for (int c = 0; c < kClasses; c++) hq[c] = (int32_t)mb_read(ctx, kMbQClass + c);
     ProfScope _ps(ctx, "mm_anchor_gsort", 52.0 * (double)n);  // key+y read, scatter write, sort read, x+y write
     // 2 small queries: sorted whole
     int rc = sort_segments(ctx, qlists.as<Seg>(), n_q, hq, key, val, 1 + rb + pb, ybits, out);
@@ -593,31 +596,26 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     HY_CHECK_LAUNCH("tile_hist_kernel");
     const int64_t gcap = std::min<int64_t>(n, NT * (int64_t)nbins);  // a group holds >= 1 anchor
     HY_ARG(gcap < INT32_MAX, "grouped_anchor_sort: too many groups in one batch");
-    DevBuf groups, ng;
+    DevBuf groups;
     HY_HIP(groups.alloc(sizeof(Seg) * (size_t)(gcap + 1), st));
-    HY_HIP(ng.alloc(4, st));
-    HY_HIP(hipMemsetAsync(ng.p, 0, 4, st));
     hipLaunchKernelGGL(query_scan_kernel, dim3((unsigned)nl), dim3(256), 0, st, large, tpos.as<int64_t>(), nbins,
-                       H.as<uint32_t>(), groups.as<Seg>(), ng.as<int32_t>());
+                       H.as<uint32_t>(), groups.as<Seg>(), ctx->dctr + kCtrGroups, mb_dev(ctx, kMbGroups));
     HY_CHECK_LAUNCH("query_scan_kernel");
     hipLaunchKernelGGL(tile_scatter_kernel, dim3((unsigned)NT), dim3(256), 0, st, key, val, ta0.as<int64_t>(), tq.as<int32_t>(),
                        tn.as<int32_t>(), d_qoff, gb, nbins, H.as<uint32_t>(), okey, oval);
     HY_CHECK_LAUNCH("tile_scatter_kernel");
     // 4 groups of the large queries, sorted in place by (rpos, y)
-    int32_t G = 0;
-    HY_HIP(hipMemcpyAsync(&G, ng.p, 4, hipMemcpyDeviceToHost, st));
     HY_HIP(hipStreamSynchronize(st));
+    const int32_t G = (int32_t)mb_read(ctx, kMbGroups);
     if (G == 0) return HYMET_OK;
-    DevBuf glists, gcnt;
+    DevBuf glists;
     HY_HIP(glists.alloc(sizeof(Seg) * kClasses * (size_t)G, st));
-    HY_HIP(gcnt.alloc(4 * kClasses, st));
-    HY_HIP(hipMemsetAsync(gcnt.p, 0, 4 * kClasses, st));
     hipLaunchKernelGGL(group_class_kernel, dim3((unsigned)cdiv(G, 1024)), dim3(256), 0, st, groups.as<Seg>(), (int64_t)G,
-                       glists.as<Seg>(), (int64_t)G, gcnt.as<int32_t>(), okey, oval, out);
+                       glists.as<Seg>(), (int64_t)G, ctx->dctr + kCtrGClass, okey, oval, out, mb_dev(ctx, kMbGClass));
     HY_CHECK_LAUNCH("group_class_kernel");
-    int32_t hg[kClasses] = {};
-    HY_HIP(hipMemcpyAsync(hg, gcnt.p, 4 * kClasses, hipMemcpyDeviceToHost, st));
     HY_HIP(hipStreamSynchronize(st));
+    int32_t hg[kClasses] = {};
+    for (int c = 0; c < kClasses; c++) hg[c] = (int32_t)mb_read(ctx, kMbGClass + c);
     rc = sort_segments(ctx, glists.as<Seg>(), (int64_t)G, hg, okey, oval, gb, ybits, out);
     if (rc) return rc;
     if (hg[kLarge] > 0) {

@@ -85,6 +85,11 @@ namespace {
 #ifndef HYMET_CHAIN_MONO
 #define HYMET_CHAIN_MONO 1
 #endif
+// Window-start probes read only (x, y): from the ring or the head cache, else with plain loads
+// of ax / ay -- not the f / p pair through L2 that a full entry needs.
+#ifndef HYMET_CHAIN_PROBE_XY
+#define HYMET_CHAIN_PROBE_XY 1
+#endif
 #ifndef HYMET_CHAIN_WPE  // waves per SIMD the register allocation targets (0: compiler's choice)
 #define HYMET_CHAIN_WPE 4
 #endif
@@ -103,6 +108,12 @@ constexpr size_t kChainLds = kRing * sizeof(int4) + kSumRing * kSumInts * sizeof
                              kInnerCap * (sizeof(int2) + sizeof(int32_t)) + kBdq * 2 * sizeof(int4) + kIdq * sizeof(int2);
 constexpr int kNegInf = -(1 << 29);
 
+// ISA section markers (static instruction counts by section: build with -DHYMET_CHAIN_MARKS -S)
+#ifdef HYMET_CHAIN_MARKS
+#define AMARK(name) asm volatile("; @@ " #name)
+#else
+#define AMARK(name)
+#endif
 // Section cycle counters for tools/chain_prof (built with -DHYMET_CHAIN_PROF); no-ops otherwise.
 #ifdef HYMET_CHAIN_PROF
 __device__ unsigned long long g_chain_prof[32];
@@ -404,7 +415,25 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             e.x = v.x, e.y = v.y, e.f = v.z, e.pw = v.w;
             return e;
         };
+        // (x, y) of anchor jl (local) at iteration i, for the window-start probes
+        auto fetch_xy = [&](int32_t jl) -> int2 {
+#if HYMET_CHAIN_PROBE_XY
+            if (i - jl <= kRing) {
+                const int4 v = ring[jl & kRingMask];
+                return make_int2(v.x, v.y);
+            }
+            if ((jl >> 6) == hb) {
+                const int4 v = hc[jl & 63];
+                return make_int2(v.x, v.y);
+            }
+            return make_int2((int32_t)P.ax[g0 + jl], (int32_t)P.ay[g0 + jl]);
+#else
+            const Ent e = fetch(jl);
+            return make_int2(e.x, e.y);
+#endif
+        };
         int32_t i0 = 0, st = 0, st_in = 0;
+        bool t_used = false;  // the overflow walk stamped t_global
         auto sum_at = [&](int32_t b, int k) -> int4 {  // word k of block b's summary
             if ((i0 >> 6) - b <= kSumRing) return ssum[(b & (kSumRing - 1)) * kSumInts + k];
             return ld_l2(gsum + (int64_t)b * kSumInts + k);
@@ -498,6 +527,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         // i.e. the entries better than every entry with y <= theirs, by y descending; the
         // best of (block, y < Y) is the first S with y < Y -- then the argmin joins the deque
         auto complete_block = [&](int32_t b) {
+            AMARK(cb_begin);
             const int32_t jl = (b << 6) + lane;
             const Ent e = fetch(jl);
             const double pl = prio(e.f, e.x, e.y, c);
@@ -582,9 +612,11 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             if (bt == bh) bf_pr = apr, bf_j = aj, bf_y = ay, bf_e = ex;
             bb_pr = apr, bb_j = aj;
             ++bt;
+            AMARK(cb_end);
         };
         // entry j (now final) enters the window: inner list, inner max-deque, tail argmin
         auto insert_one = [&](int32_t j, const Ent ej) {
+            AMARK(ins_begin);
             if (P.max_dist_inner > 0) {
                 if (!overflow && ni >= kInnerCap) overflow = true;
                 if (!overflow) {
@@ -646,6 +678,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             const double pr = prio(ej.f, ej.x, ej.y, c);
             if ((j & 63) == 0 || !(t_pr < pr)) t_pr = pr, t_j = j, t_y = ej.y;
             if ((j & 63) == 63) complete_block(j >> 6);
+            AMARK(ins_end);
         };
         int32_t cb = -128;  // base of the chunk in cx/cy; nx/ny hold the next one
         int32_t spec_next = 0, spec_gap = 2;  // next batch attempt (back-off after short batches)
@@ -694,13 +727,14 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             }
             CPROF(0);
             // ---- 2. outer window start: lane-parallel probe, one block at a time
+            AMARK(st_begin);
             for (;;) {
                 if (st >= i) break;
                 const int32_t bend = min(i, ((st >> 6) + 1) << 6);
                 const int32_t j = st + lane;
                 bool adv = false;
                 if (j < bend) {
-                    const Ent e = fetch(j);
+                    const int2 e = fetch_xy(j);
                     adv = (int64_t)(uint32_t)xi > (int64_t)(uint32_t)e.x + P.max_dist || i0 - j > P.cap_rmq_size;
                 }
                 const uint64_t m = __ballot(adv);
@@ -755,6 +789,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             }
             CPROF(1);
             // ---- 3. inner window start
+            AMARK(stin_begin);
             if (P.max_dist_inner > 0) {
                 for (;;) {
                     if (st_in >= i) break;
@@ -762,7 +797,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     bool adv = false;
                     int32_t yj = 0;
                     if (j < i) {
-                        const Ent e = fetch(j);
+                        const int2 e = fetch_xy(j);
                         yj = e.y;
                         adv = (int64_t)(uint32_t)xi > (int64_t)(uint32_t)e.x + P.max_dist_inner || i0 - j > P.cap_rmq_size;
                     }
@@ -846,6 +881,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 }
             }
             CPROF(6);
+            AMARK(stin_end);
             // ---- 3b. colinear batch: assume each of the next L anchors chains onto its
             // predecessor (max-plus scan for f), then verify, lane-parallel, every decision the
             // sequential DP would take: the predecessor is the window's best priority (it beats
@@ -899,6 +935,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 if (b0j != i - 1) CCOUNT(10);
                 if (!walk_ok) CCOUNT(11);
                 if (b0j == i - 1 && walk_ok && Lb >= 2) {
+                    AMARK(batch_begin);
                     // anchors k = i + lane from the chunk registers (cx: [cb, cb+64), nx: next 64)
                     const int off = (i - cb) + lane;
                     const uint64_t kx_lo = __shfl(cx, off & 63, 64), kx_hi = __shfl(nx, off & 63, 64);
@@ -983,6 +1020,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     } else {
                         spec_gap = 2;
                     }
+                    AMARK(batch_verified);
                     if (acc > 0) {
                         // commit anchors [i, i + acc): f, p, ring; insert entries [i, i + acc - 1)
                         const int32_t k = i + lane;
@@ -1086,6 +1124,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         const int l = acc - 1;
                         prev.x = rl(kx, l), prev.y = rl(ky, l), prev.f = rl(fk, l), prev.pw = rl(pw, l);
                         i += acc;
+                        AMARK(batch_end);
                         continue;
                     }
                 }
@@ -1220,10 +1259,12 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                                 if (sl > max_f) {
                                     max_f = sl, max_j = bjl;
                                     if (n_skip > 0) --n_skip;
-                                } else if (ld_l2(P.t_global + g0 + bjl) == i) {
+                                } else if (ld_l2(P.t_global + g0 + bjl) == i + 1) {
                                     if (++n_skip > P.max_chn_skip) break;
                                 }
-                                if (ej.p() >= 0) P.t_global[g0 + ej.p()] = i;  // every lane writes: program order
+                                // stamp i + 1 (t arrives zeroed); every lane writes: program order
+                                if (ej.p() >= 0) P.t_global[g0 + ej.p()] = i + 1;
+                                t_used = true;
                             }
                         }
                     }
@@ -1237,6 +1278,10 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             if (lane == 0) ring[i & kRingMask] = make_int4(prev.x, prev.y, prev.f, prev.pw);
             __builtin_amdgcn_wave_barrier();
             ++i;
+        }
+        if (t_used) {  // hand the backtrack a zeroed t again
+            __builtin_amdgcn_wave_barrier();
+            for (int32_t j = lane; j < n; j += 64) P.t_global[g0 + j] = 0;
         }
         CPROF_FLUSH;
         GTIME_STOP;
@@ -1320,6 +1365,7 @@ __global__ void bt_long_count_kernel(const int64_t *g_start, const int32_t *orde
         else hi = mid;
     }
     cnt[0] = lo;
+    cnt[1] = 0;  // the wave kernel's work counter
 }
 
 __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, const int32_t *list, const int32_t *cnt,
@@ -1617,8 +1663,11 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
 constexpr int kSmall = HYMET_CHAIN_SMALL;  // <= 32 (window sets are 32-bit masks)
 
 // first work item whose group has <= kSmall anchors (the list is size-descending)
-__global__ void chain_small_split_kernel(const int64_t *g_start, const int32_t *order, int32_t n_work, int32_t *split) {
+// (also zeroes the wave kernel's work counter)
+__global__ void chain_small_split_kernel(const int64_t *g_start, const int32_t *order, int32_t n_work, int32_t *split,
+                                         int32_t *counter) {
     if (threadIdx.x != 0) return;
+    *counter = 0;
     int32_t lo = 0, hi = n_work;
     while (lo < hi) {
         const int32_t mid = (lo + hi) >> 1;
@@ -1721,7 +1770,8 @@ __global__ __launch_bounds__(64) void chain_small_kernel(ChainParams P, const in
 // groups above kSmall anchors, the lane kernel on the rest.  `split` is device scratch.
 int launch_chain_raw(hipStream_t st, const ChainParams &P0, int64_t blocks, int32_t *split) {
     ChainParams P = P0;
-    hipLaunchKernelGGL(chain_small_split_kernel, dim3(1), dim3(64), 0, st, P.g_start, P.order, P.n_work, split);
+    hipLaunchKernelGGL(chain_small_split_kernel, dim3(1), dim3(64), 0, st, P.g_start, P.order, P.n_work, split,
+                       P.work_counter);
     HY_CHECK_LAUNCH("chain_small_split_kernel");
     P.work_end = split;
     const bool long_pass = P.max_dist > 10000;
@@ -1743,7 +1793,6 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
     HY_HIP(sum.alloc(16 * kSumInts * n_sum, ctx->stream));
     HY_HIP(cnt.alloc(4, ctx->stream));
     HY_HIP(split.alloc(4, ctx->stream));
-    HY_HIP(hipMemsetAsync(cnt.p, 0, 4, ctx->stream));
     if (max_dist < bw) max_dist = bw;
     if (max_dist_inner <= 0 || max_dist_inner >= max_dist) max_dist_inner = 0;
     ChainParams P{ax, ay, g_start, g_qfirst, order, n_work, cnt.as<int32_t>(), f, p, t_global, sum.as<int4>(), max_dist, max_dist_inner, bw, max_chn_skip, cap_rmq_size, pen_gap, pen_skip, nullptr};
@@ -1766,7 +1815,7 @@ int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, c
                      int min_cnt, int min_sc, int max_drop, int64_t *chain_ids, uint64_t *chain_u, int64_t *chain_first,
                      int32_t *n_chains, int64_t n_anchors) {
     if (n_groups <= 0) return HYMET_OK;
-    HY_HIP(hipMemsetAsync(t, 0, 4 * (size_t)n_anchors, ctx->stream));
+    // t arrives zeroed (group_write_kernel; the chaining kernels restore what they stamped)
     const char *ev = getenv("HYMET_BT_LONG");
     const int64_t long_min = ev ? atoll(ev) : kBtLong;
     const bool prof = getenv("HYMET_BT_PROF") != nullptr;
@@ -1778,8 +1827,7 @@ int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, c
     BacktrackParams P{g_start,  f,         p,       t,           z_cnt,    z_idx, n_groups, min_cnt, min_sc, max_drop,
                       long_min, (unsigned long long *)pbuf.p, chain_ids, chain_u, chain_first, n_chains};
     DevBuf cnt;
-    HY_HIP(cnt.alloc(8, ctx->stream));
-    HY_HIP(hipMemsetAsync(cnt.p, 0, 8, ctx->stream));
+    HY_HIP(cnt.alloc(8, ctx->stream));  // [0] long groups, [1] work counter: set by bt_long_count_kernel
     // z index + t probe + walked (p, f) + t mark + chain id write, per anchor
     ProfScope _ps(ctx, "mm_backtrack", 32.0 * (double)n_anchors);
     if (n_work > 0) {

@@ -97,9 +97,41 @@ int launch_sketch(hymet_ctx *ctx, int w, bool write, const SketchParams &P);
 int exclusive_scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, int64_t *total);
 // the same, asynchronous: `part` (scratch, kept alive by the caller) ends with the total at
 // index ceil(n / 4096)
-int scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, DevBuf &part);
+int scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, DevBuf &part, int64_t *mail = nullptr);
 // exclusive scan of n uint64 values (asynchronous; part ends with the total at ceil(n / 4096))
-int scan_u64(hymet_ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n, DevBuf &part);
+// mailbox words (hymet_ctx::mbox_h) by use; each is read right after the sync that follows
+// the kernel storing it, so uses that never overlap may share a word
+enum : int { kMbScan = 0, kMbGmax = 1, kMbZBig = 2, kMbZBigTotal = 3, kMbFlag = 4, kMbQClass = 8, kMbGroups = 16,
+             kMbGClass = 24 };
+// self-clearing device counters (hymet_ctx::dctr): counters at [base, base + n), ticket at base + n
+enum : int { kCtrQClass = 0, kCtrGroups = 16, kCtrGClass = 24 };
+
+// Called by every thread of every block after the block's last update of cnt[0, n): the last
+// block to arrive stores the totals into the mailbox words mail[0, n) and zeroes the counters
+// and the ticket, leaving them ready for the next launch (no memset, no copy back).
+__device__ __forceinline__ void publish_counters(int32_t *cnt, int n, int64_t *mail) {
+    __shared__ bool last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(reinterpret_cast<uint32_t *>(cnt + n), 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    if ((int)threadIdx.x < n) mail[threadIdx.x] = atomicExch(cnt + threadIdx.x, 0);
+    if (threadIdx.x == 0) atomicExch(cnt + n, 0);
+}
+
+// bits needed to hold v (at least 1)
+inline int bits_for(int64_t v) {
+    int b = 0;
+    while (b < 63 && (1ll << b) <= v) b++;
+    return b < 1 ? 1 : b;
+}
+// exclusive scan of uint32 counts into uint32 offsets (totals below 2^32)
+int scan_u32(hymet_ctx *ctx, const uint32_t *in, uint32_t *out, int64_t n, DevBuf &part, int64_t *mail = nullptr);
+int scan_u64(hymet_ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n, DevBuf &part, int64_t *mail = nullptr);
 // inclusive running maximum of n int32 values (asynchronous)
 int inclusive_max_scan_i32(hymet_ctx *ctx, const int32_t *in, int32_t *out, int64_t n, DevBuf &part);
 

@@ -57,9 +57,35 @@ __device__ __forceinline__ int upper_idx(const int64_t *off, int n, int64_t v) {
     return lo;
 }
 
-__global__ void fill_qid_kernel(const int64_t *off, int n_q, int64_t n, uint32_t *qid) {
+// qid[i] = query of entry i; also ones[i] = 1 (i < n) and zq[q] = 0 (q < n_q) when given
+// (grid: max(n, n_q) threads)
+__global__ void fill_qid_kernel(const int64_t *off, int n_q, int64_t n, uint32_t *qid, uint32_t *ones, int32_t *zq) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) qid[i] = (uint32_t)upper_idx(off, n_q, i);
+    if (i < n) {
+        qid[i] = (uint32_t)upper_idx(off, n_q, i);
+        if (ones) ones[i] = 1u;
+    }
+    if (zq && i < n_q) zq[i] = 0;
+}
+
+// mailbox flag: some query has more than lim minimizers (the host zeroes the word first)
+// per query: its chain anchors when the long join re-chains it, else 0; entry n_q = 0 (the
+// scan's total slot); *any = 1 when some query is flagged (the host zeroes the word first)
+__global__ void flagged_len_kernel(const uint32_t *flag, const int64_t *qb, int n_q, uint32_t *cnt, int64_t *any) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q > n_q) return;
+    if (q == n_q) {
+        cnt[q] = 0;
+        return;
+    }
+    const bool f = flag[q] != 0;
+    cnt[q] = f ? (uint32_t)(qb[q + 1] - qb[q]) : 0u;
+    if (f) *any = 1;
+}
+
+__global__ void any_over_kernel(const int64_t *off, int n_q, int64_t lim, int64_t *flag) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n_q && off[q + 1] - off[q] > lim) *flag = 1;
 }
 
 __global__ void iota_u32_kernel(uint32_t *a, int64_t n) {
@@ -75,7 +101,7 @@ __global__ void gather_kernel(const T *__restrict__ src, const uint32_t *__restr
 
 // seed.c mm_seed_mz_flt: runs of equal (query, x) in the sorted order
 __global__ void mzflt_runs_kernel(const uint32_t *sq, const uint64_t *sx, const uint32_t *sidx, const int64_t *qm_off,
-                                  int64_t n, int q_occ_max, float q_occ_frac, uint8_t *drop) {
+                                  int64_t n, int q_occ_max, float q_occ_frac, uint32_t *keep) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     if (p > 0 && sq[p] == sq[p - 1] && sx[p] == sx[p - 1]) return;  // not a run start
@@ -86,17 +112,14 @@ __global__ void mzflt_runs_kernel(const uint32_t *sq, const uint64_t *sx, const 
     if (nq <= q_occ_max) return;  // mm_seed_mz_flt returns early for this query
     const int32_t cnt = (int32_t)(e - p);
     if (cnt > q_occ_max && (float)cnt > (float)nq * q_occ_frac)
-        for (int64_t j = p; j < e; j++) drop[sidx[j]] = 1;
+        for (int64_t j = p; j < e; j++) keep[sidx[j]] = 0;
 }
 
-__global__ void flag_keep_kernel(const uint8_t *drop, int64_t n, uint32_t *keep) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) keep[i] = drop[i] ? 0u : 1u;
-}
-
-__global__ void compact_mz_kernel(const uint64_t *x, const uint64_t *y, const uint32_t *keep, const int64_t *pos, int64_t n,
+// (also completes the exclusive scan: pos[n] = the kept total)
+__global__ void compact_mz_kernel(const uint64_t *x, const uint64_t *y, const uint32_t *keep, int64_t *pos, int64_t n,
                                   uint64_t *ox, uint64_t *oy) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == n - 1) pos[n] = pos[i] + keep[i];
     if (i < n && keep[i]) {
         ox[pos[i]] = x[i];
         oy[pos[i]] = y[i];
@@ -135,7 +158,11 @@ constexpr uint32_t kFlt = 0x80000000u;  // filtered flag, kept in bit 31 of seed
 
 __global__ void seed_class_kernel(const uint32_t *seed_n, int64_t M, int max_occ, uint64_t *cls) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= M) return;
+    if (i > M) return;
+    if (i == M) {  // the scan's extra entry: rank[M] = the totals
+        cls[M] = 0;
+        return;
+    }
     const uint32_t n = seed_n[i];
     const bool hi = (int)n > max_occ, lo = n > 0 && !hi;
     cls[i] = (uint64_t)(hi ? 1u : 0u) << 32 | (lo ? 1u : 0u);
@@ -461,8 +488,11 @@ __global__ __launch_bounds__(256) void group_count_kernel(const uint64_t *x, int
     }
 }
 
+// also: t[i] = 0 for every anchor (the backtrack's initial marks; the chaining kernels'
+// overflow path stamps iterations as i + 1) and the g_start[G] = n sentinel
 __global__ __launch_bounds__(256) void group_write_kernel(const uint64_t *x, int64_t n, const int64_t *qoff, int n_q,
-                                                          const int64_t *tile_off, int64_t *g_start, int32_t *gid) {
+                                                          const int64_t *tile_off, int64_t *g_start, int32_t *gid,
+                                                          int32_t *t, int64_t G) {
     __shared__ uint32_t qs[kGTile / 32], rc[64];
     bool h[16];
     const int64_t t0 = (int64_t)blockIdx.x * kGTile;
@@ -486,9 +516,11 @@ __global__ __launch_bounds__(256) void group_write_kernel(const uint64_t *x, int
         const int64_t g = base + rc[j * 4 + w] + __popcll(b & ((2ull << lane) - 1)) - 1;  // inclusive - 1
         if (i < n) {
             gid[i] = (int32_t)g;
+            t[i] = 0;
             if (h[j]) g_start[g] = i;
         }
     }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) g_start[G] = n;
 }
 
 __global__ void group_start_kernel(const uint32_t *flag, const int64_t *gpos, int64_t n, int64_t *g_start, int32_t *gid) {
@@ -507,6 +539,7 @@ __global__ void group_qfirst_kernel(const int64_t *qoff, int n_q, const int32_t 
 
 // largest group: the first of the size-descending list, or, when sizes tie at the 16-bit
 // key's cap, the largest of that tied prefix
+// (out: a mailbox word)
 __global__ void max_group_kernel(const int64_t *g_start, const int32_t *order, int32_t G, int64_t *out) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     int64_t best = 0;
@@ -527,10 +560,13 @@ __global__ void nonwork_fp_kernel(const int64_t *g_start, int32_t G, int min_cnt
     for (int64_t a = a0; a < a1; a++) f[a] = 0, p[a] = -1;
 }
 
+// also clears the per-group query-first flags and the z-order list counters
 __global__ void group_size_kernel(const int64_t *g_start, int32_t G, int min_cnt, uint32_t *key, uint32_t *gidx,
-                                  uint32_t *is_work) {
+                                  uint32_t *is_work, uint8_t *qfirst, int32_t *zlists) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < 8) zlists[g] = 0;
     if (g >= G) return;
+    qfirst[g] = 0;
     const int64_t sz = g_start[g + 1] - g_start[g];
     // descending size in 16 bits (two radix passes): groups above 65535 anchors tie at the
     // front, non-work groups (< min_cnt <= 3 anchors) come after every work group
@@ -573,6 +609,7 @@ struct ZParams {
     int32_t *mid_list;     // groups for the block sort
     int32_t *big_list;     // groups for the radix path
     int64_t *big_off;      // their offsets in the radix arrays
+    int64_t *mail;         // mailbox words: big count, big total (published by zmerge_kernel)
 };
 
 // first list position whose group has <= kZLane anchors
@@ -687,6 +724,10 @@ __global__ __launch_bounds__(256) void zorder_lane_kernel(ZParams P) {
 // over the list; a flat pass over every anchor position read each one's group first)
 __global__ __launch_bounds__(256) void zmerge_kernel(ZParams P) {
     const int n_list = P.lists[3];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the lists are final (zorder_wave_kernel ran)
+        P.mail[0] = P.lists[2];
+        P.mail[1] = *reinterpret_cast<const int64_t *>(P.lists + 4);
+    }
     for (int w = blockIdx.x; w < n_list; w += gridDim.x) {
         const int g = P.merge_list[w];
         const int K = P.z_runs[g];
@@ -1039,11 +1080,6 @@ static int scan_flags(hymet_ctx *ctx, const uint32_t *flag, int64_t n, DevBuf &p
     return exclusive_scan_u32_i64(ctx, flag, pos.as<int64_t>(), n, total);
 }
 
-static int bits_for(int64_t v) {
-    int b = 0;
-    while ((1ll << b) <= v) b++;
-    return b < 1 ? 1 : b;
-}
 
 #define LAUNCH1(kern, n, ...)                                                                           \
     do {                                                                                                \
@@ -1057,7 +1093,6 @@ static int bits_for(int64_t v) {
 struct AnchorSet {
     DevBuf ax, ay;
     int64_t n = 0;
-    std::vector<int64_t> h_off;  // n_q + 1
     DevBuf d_off;
 };
 
@@ -1067,9 +1102,7 @@ struct ChainSet {
     DevBuf bx, by, cu, cboff;  // cboff: offset of each chain's anchors in bx/by
     DevBuf bchain, cq;         // chain of each compacted anchor; query of each chain
     int64_t n_anchor = 0, n_chain = 0;
-    std::vector<int64_t> h_qc;   // n_q + 1 chain offsets per query
-    std::vector<int64_t> h_qb;   // n_q + 1 anchor offsets per query
-    DevBuf d_qc, d_qb;
+    DevBuf d_qc, d_qb;  // n_q + 1 chain / compacted-anchor offsets per query
 };
 
 // A first pass followed by the long join (map.c's rmq rescue): chain_set flags the re-chained
@@ -1082,7 +1115,7 @@ struct LeanJoin {
     bool mark_only;
     DevBuf flag;                 // per query: re-chained
     DevBuf mark;                 // mark_only: per anchor of the set (+16 bytes for 16-byte loads)
-    std::vector<int64_t> h_qb2;  // mark_only: n_q + 1 offsets of the re-chained queries' chain anchors
+    DevBuf qb2;                  // mark_only: n_q + 1 offsets of the re-chained queries' chain anchors
     int64_t n2 = 0;
 };
 
@@ -1146,8 +1179,6 @@ static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n,
 static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, float pen_skip, int bw, AnchorSet &A,
                      int n_q, ChainSet &C, LeanJoin *lj = nullptr) {
     const int64_t n = A.n;
-    C.h_qc.assign(n_q + 1, 0);
-    C.h_qb.assign(n_q + 1, 0);
     if (n == 0) {
         HY_HIP(C.d_qc.alloc(8 * (size_t)(n_q + 1), ctx->stream));
         HY_HIP(C.d_qb.alloc(8 * (size_t)(n_q + 1), ctx->stream));
@@ -1166,23 +1197,25 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
     int64_t G = 0;
     int rc = exclusive_scan_u32_i64(ctx, tcnt.as<uint32_t>(), toff.as<int64_t>(), ntile, &G);
     if (rc) return rc;
-    DevBuf g_start;
+    DevBuf g_start, t;
     HY_HIP(g_start.alloc(8 * (size_t)(G + 1), ctx->stream));
     HY_HIP(gid.alloc(4 * (size_t)n, ctx->stream));
+    HY_HIP(t.alloc(4 * (size_t)n, ctx->stream));
     hipLaunchKernelGGL(group_write_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.ax.as<uint64_t>(), n,
-                       A.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), g_start.as<int64_t>(), gid.as<int32_t>());
+                       A.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), g_start.as<int64_t>(), gid.as<int32_t>(),
+                       t.as<int32_t>(), G);
     HY_CHECK_LAUNCH("group_write_kernel");
-    HY_HIP(hipMemcpyAsync(g_start.as<int64_t>() + G, &n, 8, hipMemcpyHostToDevice, ctx->stream));
     // work list: groups with >= min_cnt anchors, biggest first
-    DevBuf skey, sidx, swork, skey2, sidx2, gmax;
-    HY_HIP(gmax.alloc(8, ctx->stream));
+    DevBuf skey, sidx, swork, skey2, sidx2, qfirst, zlists;
     HY_HIP(skey.alloc(4 * (size_t)G, ctx->stream));
     HY_HIP(sidx.alloc(4 * (size_t)G, ctx->stream));
     HY_HIP(swork.alloc(4 * (size_t)G, ctx->stream));
     HY_HIP(skey2.alloc(4 * (size_t)G, ctx->stream));
     HY_HIP(sidx2.alloc(4 * (size_t)G, ctx->stream));
-    LAUNCH1(group_size_kernel, G, g_start.as<int64_t>(), (int32_t)G, opt->min_cnt, skey.as<uint32_t>(), sidx.as<uint32_t>(),
-            swork.as<uint32_t>());
+    HY_HIP(qfirst.alloc((size_t)G, ctx->stream));
+    HY_HIP(zlists.alloc(32, ctx->stream));
+    LAUNCH1(group_size_kernel, std::max<int64_t>(G, 8), g_start.as<int64_t>(), (int32_t)G, opt->min_cnt, skey.as<uint32_t>(),
+            sidx.as<uint32_t>(), swork.as<uint32_t>(), qfirst.as<uint8_t>(), zlists.as<int32_t>());
     // drop non-work groups: key of those = 0xffffffff (sorted last), count them on the host
     {
         DevBuf wpos;
@@ -1193,26 +1226,20 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 16, "radix_sort_groups");
         if (rc) return rc;
         {  // the chaining kernel packs local predecessor indices in 24 bits
-            int64_t big = 0;
-            LAUNCH1(max_group_kernel, 1, g_start.as<int64_t>(), (const int32_t *)vp, (int32_t)G, gmax.as<int64_t>());
-            HY_HIP(hipMemcpyAsync(&big, gmax.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+            LAUNCH1(max_group_kernel, 1, g_start.as<int64_t>(), (const int32_t *)vp, (int32_t)G, mb_dev(ctx, kMbGmax));
             HY_HIP(hipStreamSynchronize(ctx->stream));
+            const int64_t big = mb_read(ctx, kMbGmax);
             HY_ARG(big < (1ll << 24) - 1, "hymet_mm_map: an anchor group exceeds 2^24 anchors");
             static const bool stats = getenv("HYMET_CHAIN_STATS") != nullptr;  // profiling: tail size per launch
             if (stats) fprintf(stderr, "[chain] bw %d anchors %lld groups %lld work %lld largest %lld\n", bw, (long long)n,
                                (long long)G, (long long)n_work, (long long)big);
         }
-        DevBuf f, p, t;
+        DevBuf f, p;
         HY_HIP(f.alloc(4 * (size_t)n, ctx->stream));
         HY_HIP(p.alloc(8 * (size_t)n, ctx->stream));
-        HY_HIP(t.alloc(4 * (size_t)n, ctx->stream));
         // the chaining kernels write f/p of every anchor of a work group; the rest (groups of
         // fewer than min_cnt anchors) get f = 0, p = -1 here instead of memsets of all n
         LAUNCH1(nonwork_fp_kernel, G, g_start.as<int64_t>(), (int32_t)G, opt->min_cnt, f.as<int32_t>(), p.as<int64_t>());
-        HY_HIP(hipMemsetAsync(t.p, 0xFF, 4 * (size_t)n, ctx->stream));
-        DevBuf qfirst;
-        HY_HIP(qfirst.alloc((size_t)G, ctx->stream));
-        HY_HIP(hipMemsetAsync(qfirst.p, 0, (size_t)G, ctx->stream));
         LAUNCH1(group_qfirst_kernel, n_q, A.d_off.as<int64_t>(), n_q, gid.as<int32_t>(), qfirst.as<uint8_t>());
         rc = launch_chain(ctx, A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
                           (const int32_t *)vp,
@@ -1220,13 +1247,12 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
                           opt->rmq_inner_dist, bw, opt->max_chain_skip, opt->rmq_size_cap, pen_gap, pen_skip, n, G);
         if (rc) return rc;
         // z = anchors with f >= min_sc ordered by (group, f, idx), inside each group's range
-        DevBuf zkey, zidx, z_cnt, z_runs, run_start, zlists, merge_list, mid_list, big_list, big_off;
+        DevBuf zkey, zidx, z_cnt, z_runs, run_start, merge_list, mid_list, big_list, big_off;
         HY_HIP(zkey.alloc(8 * (size_t)n, ctx->stream));
         HY_HIP(zidx.alloc(4 * (size_t)n, ctx->stream));
         HY_HIP(z_cnt.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(z_runs.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(run_start.alloc(4 * (size_t)G * kZRuns, ctx->stream));
-        HY_HIP(zlists.alloc(32, ctx->stream));
         HY_HIP(merge_list.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(mid_list.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(big_list.alloc(4 * (size_t)G, ctx->stream));
@@ -1234,14 +1260,13 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         const int32_t *vi = zidx.as<int32_t>();
         {
             ProfScope _ps(ctx, "mm_z_order", 16.0 * (double)n);  // f read, key + idx written (z entries <= anchors)
-            HY_HIP(hipMemsetAsync(zlists.p, 0, 32, ctx->stream));
             // HYMET_Z_RUNS (tests): merge groups of at most that many runs, sort the others
             const char *ev = getenv("HYMET_Z_RUNS");
             const int max_runs = ev ? std::max(1, std::min(kZRuns, atoi(ev))) : kZRuns;
             ZParams Z{f.as<int32_t>(), g_start.as<int64_t>(), (const int32_t *)vp, (int32_t)G, opt->min_chain_score,
                       max_runs, zkey.as<uint64_t>(), zidx.as<int32_t>(), z_cnt.as<int32_t>(), z_runs.as<int32_t>(),
                       run_start.as<int32_t>(), zlists.as<int32_t>(), merge_list.as<int32_t>(), mid_list.as<int32_t>(), big_list.as<int32_t>(),
-                      big_off.as<int64_t>()};
+                      big_off.as<int64_t>(), mb_dev(ctx, kMbZBig)};
             hipLaunchKernelGGL(zsplit_kernel, dim3(1), dim3(64), 0, ctx->stream, Z);
             HY_CHECK_LAUNCH("zsplit_kernel");
             const int64_t nwb = std::min<int64_t>(cdiv(G, 4), (int64_t)ctx->n_cu * 8);
@@ -1253,12 +1278,8 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
             HY_CHECK_LAUNCH("zmerge_kernel");
             hipLaunchKernelGGL(zsort_block_kernel, dim3((unsigned)nb), dim3(256), 0, ctx->stream, Z);
             HY_CHECK_LAUNCH("zsort_block_kernel");
-            int32_t hl[8];
-            HY_HIP(hipMemcpyAsync(hl, zlists.p, 32, hipMemcpyDeviceToHost, ctx->stream));
             HY_HIP(hipStreamSynchronize(ctx->stream));
-            const int64_t n_big = hl[2];
-            int64_t nz_big = 0;
-            std::memcpy(&nz_big, hl + 4, 8);
+            const int64_t n_big = mb_read(ctx, kMbZBig), nz_big = mb_read(ctx, kMbZBigTotal);
             if (n_big > 0) {
                 DevBuf bcnt;
                 HY_HIP(bcnt.alloc(4 * (size_t)(n_big + 1), ctx->stream));
@@ -1433,24 +1454,18 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
                     C.by.as<uint64_t>(), C.bchain.as<int32_t>());
         HY_HIP(C.d_qb.alloc(8 * (size_t)(n_q + 1), ctx->stream));
         LAUNCH1(chain_qb_kernel, n_q + 1, C.d_qc.as<int64_t>(), C.cboff.as<int64_t>(), NC, NB, n_q, C.d_qb.as<int64_t>());
-        HY_HIP(hipMemcpyAsync(C.h_qc.data(), C.d_qc.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, ctx->stream));
-        HY_HIP(hipMemcpyAsync(C.h_qb.data(), C.d_qb.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, ctx->stream));
         if (qflag) {  // the re-chained queries' chain anchors: per-query counts, and t handed over
-            DevBuf boff2, qb2;
+            DevBuf boff2;
             int64_t NB2 = 0;
             rc = scan_flags(ctx, ccnt2.as<uint32_t>(), NC, boff2, &NB2);
             if (rc) return rc;
             // the backtrack left t == 2 on every kept chain's anchors: the long join selects
             // those of its queries straight from t (no pass over the chains)
             lj->mark.swap(t);
-            HY_HIP(qb2.alloc(8 * (size_t)(n_q + 1), ctx->stream));
-            LAUNCH1(chain_qb_kernel, n_q + 1, C.d_qc.as<int64_t>(), boff2.as<int64_t>(), NC, NB2, n_q, qb2.as<int64_t>());
-            lj->h_qb2.assign(n_q + 1, 0);
-            HY_HIP(hipMemcpyAsync(lj->h_qb2.data(), qb2.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, ctx->stream));
+            HY_HIP(lj->qb2.alloc(8 * (size_t)(n_q + 1), ctx->stream));
+            LAUNCH1(chain_qb_kernel, n_q + 1, C.d_qc.as<int64_t>(), boff2.as<int64_t>(), NC, NB2, n_q, lj->qb2.as<int64_t>());
             lj->n2 = NB2;
-            HY_HIP(hipStreamSynchronize(ctx->stream));
         }
-        HY_HIP(hipStreamSynchronize(ctx->stream));
     }
     return HYMET_OK;
 }
@@ -1620,27 +1635,29 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     int64_t M = 0;
     rc = sketch_sequences(ctx, d_2b, d_mask, h_starts, h_lens, n_q, w, k, 0, mx, my, &M, &qm_off);
     if (rc) return rc;
-    DevBuf d_qlen, d_hash;
+    DevBuf d_qlen, d_hash_buf;
     HY_HIP(d_qlen.alloc(8 * (size_t)n_q, st));
-    HY_HIP(d_hash.alloc(4 * (size_t)n_q, st));
     HY_HIP(hipMemcpyAsync(d_qlen.p, h_lens, 8 * (size_t)n_q, hipMemcpyHostToDevice, st));
-    if (d_name_hash)
-        HY_HIP(hipMemcpyAsync(d_hash.p, d_name_hash, 4 * (size_t)n_q, hipMemcpyDeviceToDevice, st));
-    else
-        HY_HIP(hipMemcpyAsync(d_hash.p, h_name_hash, 4 * (size_t)n_q, hipMemcpyHostToDevice, st));
-    std::vector<int64_t> h_qm(n_q + 1);
-    HY_HIP(hipMemcpyAsync(h_qm.data(), qm_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, st));
-    HY_HIP(hipStreamSynchronize(st));
-    tr.mark("sketch");
+    const uint32_t *d_hash = d_name_hash;  // the caller's device copy when it has one
+    if (!d_hash) {
+        HY_HIP(d_hash_buf.alloc(4 * (size_t)n_q, st));
+        HY_HIP(hipMemcpyAsync(d_hash_buf.p, h_name_hash, 4 * (size_t)n_q, hipMemcpyHostToDevice, st));
+        d_hash = d_hash_buf.as<uint32_t>();
+    }
     // ------------------------------------------------------- 2 mm_seed_mz_flt
     bool need_flt = false;
-    if (opt->q_occ_frac > 0.0f)
-        for (int q = 0; q < n_q; q++)
-            if (h_qm[q + 1] - h_qm[q] > opt->mid_occ) need_flt = true;
-    if (need_flt && M > 0) {
-        DevBuf qid, sx, sx2, sidx, sidx2, sq, sq2, drop, keep, kpos, nx, ny;
+    if (opt->q_occ_frac > 0.0f && M > 0) {  // only queries with more than mid_occ minimizers are filtered
+        ctx->mbox_h[kMbFlag] = 0;
+        LAUNCH1(any_over_kernel, n_q, qm_off.as<int64_t>(), n_q, (int64_t)opt->mid_occ, mb_dev(ctx, kMbFlag));
+        HY_HIP(hipStreamSynchronize(st));
+        need_flt = mb_read(ctx, kMbFlag) != 0;
+    }
+    tr.mark("sketch");
+    if (need_flt) {
+        DevBuf qid, sx, sx2, sidx, sidx2, sq, sq2, keep, kpos, nx, ny;
         HY_HIP(qid.alloc(4 * (size_t)M, st));
-        LAUNCH1(fill_qid_kernel, M, qm_off.as<int64_t>(), n_q, M, qid.as<uint32_t>());
+        HY_HIP(keep.alloc(4 * (size_t)M, st));
+        LAUNCH1(fill_qid_kernel, M, qm_off.as<int64_t>(), n_q, M, qid.as<uint32_t>(), keep.as<uint32_t>(), nullptr);
         HY_HIP(sx.alloc(8 * (size_t)M, st));
         HY_HIP(sx2.alloc(8 * (size_t)M, st));
         HY_HIP(sidx.alloc(4 * (size_t)M, st));
@@ -1658,11 +1675,7 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
         rc = sort_pairs(ctx, kq, kqa, vi, via, M, 0, bits_for(n_q), "radix_sort_mz");
         if (rc) return rc;
         LAUNCH1(gather_kernel<uint64_t>, M, mx.as<uint64_t>(), vi, kxa, M);  // x in (q, x) order
-        HY_HIP(drop.alloc((size_t)M, st));
-        HY_HIP(hipMemsetAsync(drop.p, 0, (size_t)M, st));
-        LAUNCH1(mzflt_runs_kernel, M, kq, kxa, vi, qm_off.as<int64_t>(), M, opt->mid_occ, opt->q_occ_frac, drop.as<uint8_t>());
-        HY_HIP(keep.alloc(4 * (size_t)M, st));
-        LAUNCH1(flag_keep_kernel, M, drop.as<uint8_t>(), M, keep.as<uint32_t>());
+        LAUNCH1(mzflt_runs_kernel, M, kq, kxa, vi, qm_off.as<int64_t>(), M, opt->mid_occ, opt->q_occ_frac, keep.as<uint32_t>());
         int64_t M2 = 0;
         rc = scan_flags(ctx, keep.as<uint32_t>(), M, kpos, &M2);
         if (rc) return rc;
@@ -1670,7 +1683,6 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
         HY_HIP(ny.alloc(8 * (size_t)(M2 + 1), st));
         LAUNCH1(compact_mz_kernel, M, mx.as<uint64_t>(), my.as<uint64_t>(), keep.as<uint32_t>(), kpos.as<int64_t>(), M,
                 nx.as<uint64_t>(), ny.as<uint64_t>());
-        HY_HIP(hipMemcpyAsync(kpos.as<int64_t>() + M, &M2, 8, hipMemcpyHostToDevice, st));
         DevBuf nqm;
         HY_HIP(nqm.alloc(8 * (size_t)(n_q + 1), st));
         hipLaunchKernelGGL(sample_off_kernel, dim3((unsigned)cdiv(n_q + 1, 256)), dim3(256), 0, st, kpos.as<int64_t>(),
@@ -1680,8 +1692,6 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
         my.swap(ny);
         qm_off.swap(nqm);
         M = M2;
-        HY_HIP(hipMemcpyAsync(h_qm.data(), qm_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, st));
-        HY_HIP(hipStreamSynchronize(st));
     }
     tr.mark("mz_flt");
     // ------------------------------------------------------------- 3 seeds
@@ -1689,8 +1699,8 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     HY_HIP(seed_n.alloc(4 * (size_t)(M + 1), st));
     HY_HIP(rep_len.alloc(4 * (size_t)n_q, st));
     HY_HIP(qid.alloc(4 * (size_t)(M + 1), st));
-    HY_HIP(hipMemsetAsync(rep_len.p, 0, 4 * (size_t)n_q, st));
-    LAUNCH1(fill_qid_kernel, M, qm_off.as<int64_t>(), n_q, M, qid.as<uint32_t>());
+    LAUNCH1(fill_qid_kernel, std::max<int64_t>(M, n_q), qm_off.as<int64_t>(), n_q, M, qid.as<uint32_t>(), nullptr,
+            rep_len.as<int32_t>());
     {
         ProfScope _ps(ctx, "mm_seed_count", (double)M * (8.0 + 8.0 + 4.0));  // minimizer, 2 offsets, count
         LAUNCH1(seed_count_kernel, M, mx.as<uint64_t>(), M, idx->d_koff, idx->n_buckets, seed_n.as<uint32_t>());
@@ -1700,16 +1710,14 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
         DevBuf cls, rank;
         HY_HIP(cls.alloc(8 * (size_t)(M + 1), st));
         HY_HIP(rank.alloc(8 * (size_t)(M + 1), st));
-        LAUNCH1(seed_class_kernel, M, seed_n.as<uint32_t>(), M, opt->mid_occ, cls.as<uint64_t>());
-        HY_HIP(hipMemsetAsync(cls.as<uint64_t>() + M, 0, 8, st));
+        LAUNCH1(seed_class_kernel, M + 1, seed_n.as<uint32_t>(), M, opt->mid_occ, cls.as<uint64_t>());
         DevBuf spart;
         {  // exclusive scan of packed (low, high) counts over M + 1 entries: rank[M] = totals
-            rc = scan_u64(ctx, cls.as<uint64_t>(), rank.as<uint64_t>(), M + 1, spart);
+            rc = scan_u64(ctx, cls.as<uint64_t>(), rank.as<uint64_t>(), M + 1, spart, mb_dev(ctx, kMbScan));
             if (rc) return rc;
         }
-        uint64_t tot = 0;
-        HY_HIP(hipMemcpyAsync(&tot, rank.as<uint64_t>() + M, 8, hipMemcpyDeviceToHost, st));
         HY_HIP(hipStreamSynchronize(st));
+        const uint64_t tot = (uint64_t)mb_read(ctx, kMbScan);
         const int64_t n_low = (uint32_t)tot, n_high = (int64_t)(tot >> 32);
         if (n_high > 0) {
             DevBuf low_idx, high_idx, flt_high, vmax, pmax;
@@ -1855,23 +1863,23 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     tr.mark("chain_set 1");
     ChainSet *CF = &C1;
     ChainSet C2;
-    std::vector<uint32_t> h_flag(n_q, 0);
     DevBuf flag;  // queries re-chained by the long join (their first-pass regions are not built)
     if (long_join && C1.n_chain > 0) {
         flag.swap(lj.flag);
-        HY_HIP(hipMemcpyAsync(h_flag.data(), flag.p, 4 * (size_t)n_q, hipMemcpyDeviceToHost, st));
-        HY_HIP(hipStreamSynchronize(st));
-        bool any = false;
-        for (int q = 0; q < n_q; q++) any |= h_flag[q] != 0;
+        // anchors of flagged queries only: their per-query offsets, built on the device (the
+        // total and whether any query is flagged come back through the mailbox)
+        const DevBuf &qbuf = lj.mark_only ? lj.qb2 : C1.d_qb;
+        AnchorSet S2;
+        DevBuf fcnt;
+        HY_HIP(fcnt.alloc(4 * (size_t)(n_q + 1), st));
+        ctx->mbox_h[kMbFlag] = 0;
+        LAUNCH1(flagged_len_kernel, n_q + 1, flag.as<uint32_t>(), qbuf.as<int64_t>(), n_q, fcnt.as<uint32_t>(),
+                mb_dev(ctx, kMbFlag));
+        int64_t A2 = 0;
+        rc = scan_flags(ctx, fcnt.as<uint32_t>(), n_q + 1, S2.d_off, &A2);  // (syncs the stream)
+        if (rc) return rc;
+        const bool any = mb_read(ctx, kMbFlag) != 0;
         if (any) {
-            // anchors of flagged queries only: new per-query offsets
-            AnchorSet S2;
-            S2.h_off.assign(n_q + 1, 0);
-            const std::vector<int64_t> &qb = lj.mark_only ? lj.h_qb2 : C1.h_qb;
-            for (int q = 0; q < n_q; q++) S2.h_off[q + 1] = S2.h_off[q] + (h_flag[q] ? qb[q + 1] - qb[q] : 0);
-            const int64_t A2 = S2.h_off[n_q];
-            HY_HIP(S2.d_off.alloc(8 * (size_t)(n_q + 1), st));
-            HY_HIP(hipMemcpyAsync(S2.d_off.p, S2.h_off.data(), 8 * (size_t)(n_q + 1), hipMemcpyHostToDevice, st));
             if (lj.mark_only) {
                 // the flagged queries' chain anchors (t == 2 from the backtrack), compacted out of
                 // the first-pass set in its (key, y) order -- already the long join's sorted set
@@ -1889,9 +1897,12 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                 if (got != A2 || got != lj.n2) {
                     if (getenv("HYMET_DEBUG_LJ2")) {  // diagnostic: per-query marks vs chain anchors
                         std::vector<int32_t> hm(n1);
-                        std::vector<int64_t> qo(n_q + 1);
+                        std::vector<int64_t> qo(n_q + 1), qb(n_q + 1);
+                        std::vector<uint32_t> h_flag(n_q);
                         HY_HIP(hipMemcpy(hm.data(), mark.p, 4 * (size_t)n1, hipMemcpyDeviceToHost));
                         HY_HIP(hipMemcpy(qo.data(), S1.d_off.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost));
+                        HY_HIP(hipMemcpy(qb.data(), qbuf.p, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost));
+                        HY_HIP(hipMemcpy(h_flag.data(), flag.p, 4 * (size_t)n_q, hipMemcpyDeviceToHost));
                         int shown = 0;
                         for (int q = 0; q < n_q; q++) {
                             int64_t mk = 0;
@@ -1959,24 +1970,22 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
         HY_HIP(nr.alloc(4 * (size_t)n_q, st));
         return launch_regions(ctx, C.bx.as<uint64_t>(), C.by.as<uint64_t>(), C.cu.as<uint64_t>(), C.cboff.as<int64_t>(),
                               C.d_qc.as<int64_t>(), C.d_qb.as<int64_t>(), mini_pos.as<uint64_t>(), mp_off.as<int64_t>(),
-                              d_qlen.as<int64_t>(), d_hash.as<uint32_t>(), rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
+                              d_qlen.as<int64_t>(), d_hash, rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
                               z.p, rg.as<hymet_mm_reg>(), wv.as<int32_t>(), cov.as<uint64_t>(), tmp.as<int32_t>(),
                               nr.as<int32_t>(), C.n_anchor, NC, NM, C.bchain.as<int32_t>(), C.cq.as<uint32_t>(),
                               pos_tab.as<int32_t>(), d_qbase.as<int64_t>(), skip_q);
     };
-    DevBuf rg1, nr1, rg2, nr2, d_flag;
+    DevBuf rg1, nr1, rg2, nr2;
     rc = run_regions(C1, rg1, nr1, CF ? nullptr : flag.as<uint32_t>());
     if (rc) return rc;
     if (!CF) {
         rc = run_regions(C2, rg2, nr2, nullptr);
         if (rc) return rc;
-        HY_HIP(d_flag.alloc(4 * (size_t)n_q, st));
-        HY_HIP(hipMemcpyAsync(d_flag.p, h_flag.data(), 4 * (size_t)n_q, hipMemcpyHostToDevice, st));
     }
     // PAF order within the batch: query by query, each query's regions as selected
     DevBuf cnt, off;
     HY_HIP(cnt.alloc(4 * (size_t)(n_q + 1), st));
-    const uint32_t *fl = CF ? nullptr : d_flag.as<uint32_t>();
+    const uint32_t *fl = CF ? nullptr : flag.as<uint32_t>();
     const int32_t *n2p = CF ? nr1.as<int32_t>() : nr2.as<int32_t>();
     const int64_t *qc2 = CF ? C1.d_qc.as<int64_t>() : C2.d_qc.as<int64_t>();
     const hymet_mm_reg *r2p = CF ? rg1.as<hymet_mm_reg>() : rg2.as<hymet_mm_reg>();
@@ -2130,11 +2139,12 @@ int hymet_mm_chain_dp(hymet_ctx *ctx, const uint64_t *h_x, const uint64_t *h_y, 
     LAUNCH1(group_start_kernel, n, flag.as<uint32_t>(), gpos.as<int64_t>(), n, g_start.as<int64_t>(), gid.as<int32_t>());
     HY_HIP(hipMemcpyAsync(g_start.as<int64_t>() + G, &n, 8, hipMemcpyHostToDevice, st));
     HY_HIP(qfirst.alloc((size_t)G, st));
-    HY_HIP(hipMemsetAsync(qfirst.p, 0, (size_t)G, st));
-    HY_HIP(hipMemsetAsync(qfirst.p, 1, 1, st));  // one query: group 0 holds anchor 0
+    DevBuf zl;
+    HY_HIP(zl.alloc(32, st));
     for (DevBuf *b : {&skey, &sidx, &swork, &skey2, &sidx2}) HY_HIP(b->alloc(4 * (size_t)G, st));
-    LAUNCH1(group_size_kernel, G, g_start.as<int64_t>(), (int32_t)G, 1, skey.as<uint32_t>(), sidx.as<uint32_t>(),
-            swork.as<uint32_t>());
+    LAUNCH1(group_size_kernel, std::max<int64_t>(G, 8), g_start.as<int64_t>(), (int32_t)G, 1, skey.as<uint32_t>(),
+            sidx.as<uint32_t>(), swork.as<uint32_t>(), qfirst.as<uint8_t>(), zl.as<int32_t>());
+    HY_HIP(hipMemsetAsync(qfirst.p, 1, 1, st));  // one query: group 0 holds anchor 0
     uint32_t *kp = skey.as<uint32_t>(), *ka = skey2.as<uint32_t>(), *vp = sidx.as<uint32_t>(), *va = sidx2.as<uint32_t>();
     rc = sort_pairs(ctx, kp, ka, vp, va, G, 0, 16, "radix_sort_groups");
     if (rc) return rc;
@@ -2152,7 +2162,7 @@ int hymet_mm_chain_dp(hymet_ctx *ctx, const uint64_t *h_x, const uint64_t *h_y, 
     HY_HIP(t.alloc(4 * (size_t)n, st));
     HY_HIP(hipMemsetAsync(f.p, 0, 4 * (size_t)n, st));
     HY_HIP(hipMemsetAsync(p.p, 0xFF, 8 * (size_t)n, st));
-    HY_HIP(hipMemsetAsync(t.p, 0xFF, 4 * (size_t)n, st));
+    HY_HIP(hipMemsetAsync(t.p, 0, 4 * (size_t)n, st));
     rc = launch_chain(ctx, x.as<uint64_t>(), y.as<uint64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
                       (const int32_t *)vp, (int32_t)G, f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(), max_dist,
                       max_dist_inner, bw, max_chn_skip, cap_rmq_size, pen_gap, pen_skip, n, G);

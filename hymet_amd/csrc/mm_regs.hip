@@ -409,6 +409,12 @@ __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
     P.n_regs[q] = n;
 }
 
+// per-chain stats accumulators: mlen = blen = 0, first-anchor minimum = 0x7f7f7f7f
+__global__ void chain_stats_init_kernel(int32_t *c_mlen, int32_t *c_blen, int32_t *c_fv, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) c_mlen[i] = 0, c_blen[i] = 0, c_fv[i] = 0x7f7f7f7f;
+}
+
 }  // namespace
 
 int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const uint64_t *cu, const int64_t *cboff,
@@ -429,8 +435,9 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
         AnchorStatParams A{bx, by, cu, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, bchain, cq,
                            c_mlen, c_blen, c_st, c_last, pos_tab, qbase, skip_q};
         if (NB > 0) {
-            HY_HIP(hipMemsetAsync(c_mlen, 0, 8 * (size_t)(NC + 1), st));  // c_mlen, c_blen
-            HY_HIP(hipMemsetAsync(c_fv, 0x7f, 4 * (size_t)(NC + 1), st));
+            hipLaunchKernelGGL(chain_stats_init_kernel, dim3((unsigned)cdiv(NC + 1, 256)), dim3(256), 0, st, c_mlen, c_blen,
+                               c_fv, NC + 1);
+            HY_CHECK_LAUNCH("chain_stats_init_kernel");
             hipLaunchKernelGGL(chain_stats_flat_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A, c_fv);
             HY_CHECK_LAUNCH("chain_stats_flat_kernel");
         }

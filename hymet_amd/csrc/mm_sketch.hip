@@ -22,8 +22,7 @@
 
 // the cold index build keeps rocPRIM's onesweep for its one-off sorts of every reference
 // minimizer (hundreds of millions); the warm mapping path uses the library's own sort.hpp
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
+#include "sort.hpp"
 
 #include <cstdio>
 #include <cstdlib>
@@ -155,12 +154,26 @@ __global__ void bucket_hist_kernel(const uint64_t *__restrict__ x, int64_t n, ui
     atomicAdd(&cnt[h], 1u);
 }
 
-__global__ void occ_hist_kernel(const uint32_t *__restrict__ koff, int64_t n_buckets, uint32_t *hist, int cap) {
+// per-key occurrence histogram: nearly every key occurs once or a few times, so small counts
+// go to a block-local LDS histogram (count 1 to a per-thread register) and only the rare
+// large ones to global atomics (one global counter for all of them stalled ~0.5 s on C4)
+__global__ __launch_bounds__(256) void occ_hist_kernel(const uint32_t *__restrict__ koff, int64_t n_buckets, uint32_t *hist,
+                                                       int cap) {
+    __shared__ uint32_t sh[256];
+    sh[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t ones = 0;
     for (int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n_buckets;
          h += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t c = koff[h + 1] - koff[h];
-        if (c) atomicAdd(&hist[c < (uint32_t)cap ? c : (uint32_t)cap], 1u);
+        if (c == 1) ones++;
+        else if (c > 1 && c < 256) atomicAdd(&sh[c], 1u);
+        else if (c >= 256) atomicAdd(&hist[c < (uint32_t)cap ? c : (uint32_t)cap], 1u);
     }
+    for (int o = 32; o > 0; o >>= 1) ones += __shfl_xor(ones, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&sh[1], ones);
+    __syncthreads();
+    if (sh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], sh[threadIdx.x]);
 }
 
 }  // namespace
@@ -343,30 +356,22 @@ int hymet_mm_index_build(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d
         if (hipGetLastError() != hipSuccess) return cleanup(fail(HYMET_E_HIP, "bucket_hist_kernel"));
     }
     {
-        size_t tmp = 0;
-        if (rocprim::exclusive_scan(nullptr, tmp, cnt.as<uint32_t>(), idx->d_koff, 0u, (size_t)(nb + 1),
-                                    rocprim::plus<uint32_t>(), st))
-            return cleanup(fail(HYMET_E_HIP, "scan size"));
-        DevBuf t;
-        if (t.alloc(tmp, st) || rocprim::exclusive_scan(t.p, tmp, cnt.as<uint32_t>(), idx->d_koff, 0u, (size_t)(nb + 1),
-                                                         rocprim::plus<uint32_t>(), st))
-            return cleanup(fail(HYMET_E_HIP, "scan"));
+        DevBuf part;
+        if (scan_u32(ctx, cnt.as<uint32_t>(), idx->d_koff, nb + 1, part)) return cleanup(fail(HYMET_E_HIP, "scan"));
     }
-    // sort (hash, y): y first, then a stable pass on the hash (2k bits)
+    // sort (hash, y): y first, then a stable pass on the hash (2k bits); y = seq << 32 | pos << 1 | strand
     if (n) {
-        size_t tmp1 = 0, tmp2 = 0;
-        if (rocprim::radix_sort_pairs(nullptr, tmp1, dy.as<uint64_t>(), pos2.as<uint64_t>(), hsh.as<uint32_t>(),
-                                      hsh2.as<uint32_t>(), (size_t)n, 0, 64, st) ||
-            rocprim::radix_sort_pairs(nullptr, tmp2, hsh2.as<uint32_t>(), idx->d_hash, pos2.as<uint64_t>(), idx->d_pos,
-                                      (size_t)n, 0, 2 * k, st))
-            return cleanup(fail(HYMET_E_HIP, "sort size"));
-        DevBuf t;
-        if (t.alloc(tmp1 > tmp2 ? tmp1 : tmp2, st) ||
-            rocprim::radix_sort_pairs(t.p, tmp1, dy.as<uint64_t>(), pos2.as<uint64_t>(), hsh.as<uint32_t>(),
-                                      hsh2.as<uint32_t>(), (size_t)n, 0, 64, st) ||
-            rocprim::radix_sort_pairs(t.p, tmp2, hsh2.as<uint32_t>(), idx->d_hash, pos2.as<uint64_t>(), idx->d_pos,
-                                      (size_t)n, 0, 2 * k, st))
-            return cleanup(fail(HYMET_E_HIP, "sort"));
+        uint64_t *ky = dy.as<uint64_t>(), *kya = pos2.as<uint64_t>();
+        uint32_t *vh = hsh.as<uint32_t>(), *vha = hsh2.as<uint32_t>();
+        const int ybits = 32 + bits_for(n_seq);
+        if (radix_sort_pairs(ctx, ky, kya, vh, vha, n, 0, std::min(64, ybits))) return cleanup(fail(HYMET_E_HIP, "sort"));
+        // hashes are keys now: the sorted ones in vh; the y's ride along
+        uint32_t *kh = vh, *kha = vha;
+        uint64_t *vy = ky, *vya = kya;
+        if (radix_sort_pairs(ctx, kh, kha, vy, vya, n, 0, 2 * k)) return cleanup(fail(HYMET_E_HIP, "sort"));
+        if (hipMemcpyAsync(idx->d_hash, kh, 4 * (size_t)n, hipMemcpyDeviceToDevice, st) ||
+            hipMemcpyAsync(idx->d_pos, vy, 8 * (size_t)n, hipMemcpyDeviceToDevice, st))
+            return cleanup(fail(HYMET_E_HIP, "copy"));
     }
     if (hipStreamSynchronize(st) != hipSuccess) return cleanup(fail(HYMET_E_HIP, "hymet_mm_index_build: sync"));
     *out = idx;

@@ -71,8 +71,9 @@ __global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint32_t 
     if (threadIdx.x == 0) part[blockIdx.x] = total;
 }
 
-// one block of 1024: tile sums -> exclusive tile offsets; part[nb] = grand total
-__global__ __launch_bounds__(1024) void scan_parts_kernel(uint64_t *part, int64_t nb) {
+// one block of 1024: tile sums -> exclusive tile offsets; part[nb] = grand total (and *mail,
+// a mailbox word, when given)
+__global__ __launch_bounds__(1024) void scan_parts_kernel(uint64_t *part, int64_t nb, int64_t *mail) {
     __shared__ uint64_t ws[16];
     uint64_t carry = 0;
     for (int64_t b0 = 0; b0 < nb; b0 += 1024) {
@@ -83,15 +84,20 @@ __global__ __launch_bounds__(1024) void scan_parts_kernel(uint64_t *part, int64_
         if (b < nb) part[b] = carry + ex;
         carry += total;
     }
-    if (threadIdx.x == 0) part[nb] = carry;
+    if (threadIdx.x == 0) {
+        part[nb] = carry;
+        if (mail) *mail = (int64_t)carry;
+    }
 }
 
 __device__ __forceinline__ int pad16(int e) { return e + (e >> 4); }
 
+// O = int64_t (offsets) or uint32_t (the index's bucket offsets, sums below 2^32)
+template <typename O>
 __global__ __launch_bounds__(kScanBlock) void scan_down_kernel(const uint32_t *__restrict__ in, int64_t n,
-                                                               const uint64_t *__restrict__ part, int64_t *__restrict__ out) {
+                                                               const uint64_t *__restrict__ part, O *__restrict__ out) {
     __shared__ uint32_t sv[kScanTile + kScanTile / 16];
-    __shared__ int64_t so[kScanTile + kScanTile / 16];
+    __shared__ O so[kScanTile + kScanTile / 16];
     __shared__ uint64_t ws[kScanBlock / 64];
     const int64_t base = (int64_t)blockIdx.x * kScanTile;
     const int t = threadIdx.x;
@@ -124,16 +130,24 @@ __global__ __launch_bounds__(kScanBlock) void scan_down_kernel(const uint32_t *_
     uint64_t run = part[blockIdx.x] + block_excl<kScanBlock / 64>(s, ws, &total);
 #pragma unroll
     for (int j = 0; j < kScanItems; j++) {
-        so[pad16(t * kScanItems + j)] = (int64_t)run;
+        so[pad16(t * kScanItems + j)] = (O)run;
         run += v[j];
     }
     __syncthreads();
-    if (full) {  // 16-byte stores, striped
+    if (full && sizeof(O) == 8) {  // 16-byte stores, striped
         longlong2 *o = reinterpret_cast<longlong2 *>(out + base);
 #pragma unroll
         for (int j = 0; j < kScanItems / 2; j++) {
             const int q = j * kScanBlock + t, e = 2 * q;
-            o[q] = make_longlong2(so[pad16(e)], so[pad16(e) + 1]);
+            o[q] = make_longlong2((long long)so[pad16(e)], (long long)so[pad16(e) + 1]);
+        }
+    } else if (full) {
+        uint4 *o = reinterpret_cast<uint4 *>(out + base);
+#pragma unroll
+        for (int j = 0; j < kScanItems / 4; j++) {
+            const int q = j * kScanBlock + t, e = 4 * q;
+            o[q] = make_uint4((uint32_t)so[pad16(e)], (uint32_t)so[pad16(e) + 1], (uint32_t)so[pad16(e) + 2],
+                              (uint32_t)so[pad16(e) + 3]);
         }
     } else {
 #pragma unroll
@@ -271,30 +285,44 @@ int inclusive_max_scan_i32(hymet_ctx *ctx, const int32_t *in, int32_t *out, int6
     return HYMET_OK;
 }
 
-int scan_u64(hymet_ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n, DevBuf &part) {
+int scan_u64(hymet_ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n, DevBuf &part, int64_t *mail) {
     if (n <= 0) return HYMET_OK;
     hipStream_t st = ctx->stream;
     const int64_t nb = cdiv(n, kScanTile);
     HY_HIP(part.alloc(8 * (size_t)(nb + 1), st));
     hipLaunchKernelGGL(scan_reduce64_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>());
     HY_CHECK_LAUNCH("scan_reduce64_kernel");
-    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<uint64_t>(), nb);
+    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<uint64_t>(), nb, mail);
     HY_CHECK_LAUNCH("scan_parts_kernel");
     hipLaunchKernelGGL(scan_down64_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(), out);
     HY_CHECK_LAUNCH("scan_down64_kernel");
     return HYMET_OK;
 }
 
-int scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, DevBuf &part) {
+int scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, DevBuf &part, int64_t *mail) {
     if (n <= 0) return HYMET_OK;
     hipStream_t st = ctx->stream;
     const int64_t nb = cdiv(n, kScanTile);
     HY_HIP(part.alloc(8 * (size_t)(nb + 1), st));
     hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>());
     HY_CHECK_LAUNCH("scan_reduce_kernel");
-    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<uint64_t>(), nb);
+    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<uint64_t>(), nb, mail);
     HY_CHECK_LAUNCH("scan_parts_kernel");
-    hipLaunchKernelGGL(scan_down_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(), out);
+    hipLaunchKernelGGL(scan_down_kernel<int64_t>, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(), out);
+    HY_CHECK_LAUNCH("scan_down_kernel");
+    return HYMET_OK;
+}
+
+int scan_u32(hymet_ctx *ctx, const uint32_t *in, uint32_t *out, int64_t n, DevBuf &part, int64_t *mail) {
+    if (n <= 0) return HYMET_OK;
+    hipStream_t st = ctx->stream;
+    const int64_t nb = cdiv(n, kScanTile);
+    HY_HIP(part.alloc(8 * (size_t)(nb + 1), st));
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>());
+    HY_CHECK_LAUNCH("scan_reduce_kernel");
+    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<uint64_t>(), nb, mail);
+    HY_CHECK_LAUNCH("scan_parts_kernel");
+    hipLaunchKernelGGL(scan_down_kernel<uint32_t>, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(), out);
     HY_CHECK_LAUNCH("scan_down_kernel");
     return HYMET_OK;
 }
@@ -303,13 +331,10 @@ int exclusive_scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int
     *total = 0;
     if (n <= 0) return HYMET_OK;
     DevBuf part;
-    int rc = scan_u32_i64(ctx, in, out, n, part);
+    int rc = scan_u32_i64(ctx, in, out, n, part, mb_dev(ctx, kMbScan));
     if (rc) return rc;
-    const int64_t nb = cdiv(n, kScanTile);
-    uint64_t t = 0;
-    HY_HIP(hipMemcpyAsync(&t, part.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, ctx->stream));
     HY_HIP(hipStreamSynchronize(ctx->stream));
-    *total = (int64_t)t;
+    *total = mb_read(ctx, kMbScan);
     return HYMET_OK;
 }
 

@@ -232,3 +232,28 @@ def test_world2_pipeline_equals_world1(gpu, tmp_path):
     assert got[0][0] == one.tsv
     assert got[1][0] == b""
     assert got[0][1] + got[1][1] == one.paf_bytes
+
+
+def test_map_streams_one_and_two_identical(gpu, tmp_path):
+    """The default two-stream mapping (worker contexts, per-worker accumulators re-ordered
+    part-major by hymet_paf_acc_append) must give the same PAF and TSV bytes as one stream,
+    on an input of several index parts and several query batches per worker."""
+    from hymet_amd import pipeline
+    from hymet_amd.seqio import from_records
+    w, db, by_name, tax, hier = _setup(gpu, tmp_path)
+
+    def ref_lookup(names):
+        return from_records([(by_name[n][0], "", by_name[n][1]) for n in names])
+
+    queries = from_records([(n, "", s) for n, s in zip(w.contig_names, w.contigs)])
+    out = {}
+    for ms in (1, 2):
+        cfg = pipeline.Config(split_idx="2m", index_mini_batch=1e6, map_batch_bases=60_000, map_streams=ms)
+        p = pipeline.Pipeline(gpu, [db], ref_lookup, tax, hier, cfg)
+        res = p.run(queries, with_paf=True)
+        assert len(p.index_for(res.selected).parts) >= 2
+        out[ms] = res
+    assert out[1].selected == out[2].selected
+    assert out[1].paf == out[2].paf
+    assert out[1].tsv == out[2].tsv
+    assert len(out[1].paf) > 50

@@ -106,7 +106,7 @@ int main(int argc, char **argv) {
         CK(hipMemset(cnt, 0, 4));
         CK(hipMemset(df, 0, 4 * n));
         CK(hipMemset(dp, 0xFF, 8 * n));
-        CK(hipMemset(dt, 0xFF, 4 * n));
+        CK(hipMemset(dt, 0, 4 * n));  // t arrives zeroed (overflow stamps are i + 1)
         ChainParams P{dx, dy, gs, qf, order, nwork, cnt, df, dp, dt, sum, max_dist, 1000, bw, 25, 100000, 0.12f, 0.0f, nullptr};
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
