@@ -26,8 +26,9 @@
 //     entries of the partial head/tail blocks and of blocks whose argmin is out of range;
 //   * the inner window (x within rmq_inner_dist) is a (y, idx) sorted ring-deque in LDS (the
 //     krmq inner tree's in-order sequence; colinear inserts append, colinear erases pop the
-//     front) plus an LDS ring of "visited in this iteration" stamps (the t[] array
-//     restricted to the window, the only part the skip heuristic reads).  A candidate of the
+//     front); the walk's "visited in this iteration" stamps (lchain.c's t[]) go to t_global
+//     as i + 1 (the walk is rare on real anchors; t arrives zeroed and is re-zeroed after a
+//     group that stamped it).  A candidate of the
 //     inner walk scores at most f_j + span_j, so when a monotone max-deque over the window
 //     says max(f_j + span_j) <= max_f the walk cannot change max_f/max_j and is skipped.
 //     Otherwise the walk is evaluated 64 candidates at a time: scores lane-parallel, the
@@ -85,10 +86,10 @@ namespace {
 #ifndef HYMET_CHAIN_MONO
 #define HYMET_CHAIN_MONO 1
 #endif
-// Window-start probes read only (x, y): from the ring or the head cache, else with plain loads
-// of ax / ay -- not the f / p pair through L2 that a full entry needs.
-#ifndef HYMET_CHAIN_PROBE_XY
-#define HYMET_CHAIN_PROBE_XY 1
+// Head cache prefetch: when the head cache takes block b, block b + 1's entries are loaded
+// into registers, so the next window-start block change does not wait on HBM.
+#ifndef HYMET_CHAIN_HCPF
+#define HYMET_CHAIN_HCPF 0
 #endif
 #ifndef HYMET_CHAIN_WPE  // waves per SIMD the register allocation targets (0: compiler's choice)
 #define HYMET_CHAIN_WPE 4
@@ -101,11 +102,12 @@ constexpr int kSumRing = HYMET_CHAIN_SUMRING;  // LDS ring of the last complete 
 #ifndef HYMET_CHAIN_INNER
 #define HYMET_CHAIN_INNER 256
 #endif
-constexpr int kInnerCap = HYMET_CHAIN_INNER;  // LDS inner-window list (ring-deque) + stamps: 3 KB at 256
+constexpr int kInnerCap = HYMET_CHAIN_INNER;  // LDS inner-window list (ring-deque): 2 KB at 256
+constexpr int kXRing = 256;  // LDS ring of the last 256 anchors' x (1 KB): the window-start probes
 constexpr int kBdq = HYMET_CHAIN_BDQ;  // block-argmin deque, 2 int4 per element (1 KB)
 constexpr int kIdq = HYMET_CHAIN_IDQ;  // inner max-deque (idx, f + span) (0.5 KB)
 constexpr size_t kChainLds = kRing * sizeof(int4) + kSumRing * kSumInts * sizeof(int4) + 64 * 2 * sizeof(int4) +
-                             kInnerCap * (sizeof(int2) + sizeof(int32_t)) + kBdq * 2 * sizeof(int4) + kIdq * sizeof(int2);
+                             kInnerCap * sizeof(int2) + kXRing * sizeof(int32_t) + kBdq * 2 * sizeof(int4) + kIdq * sizeof(int2);
 constexpr int kNegInf = -(1 << 29);
 
 // ISA section markers (static instruction counts by section: build with -DHYMET_CHAIN_MARKS -S)
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
     sp += kInnerCap * sizeof(int2);
     int2 *idq = reinterpret_cast<int2 *>(sp);  // (idx, f + span)
     sp += kIdq * sizeof(int2);
-    int32_t *stamp = reinterpret_cast<int32_t *>(sp);
+    int32_t *xring = reinterpret_cast<int32_t *>(sp);  // x of anchor j at [j & (kXRing - 1)]
     const double c = 0.5 * (double)P.pen_gap;
     const int32_t n_work = P.work_end ? min(P.n_work, *P.work_end) : P.n_work;
     for (;;) {
@@ -415,25 +417,44 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             e.x = v.x, e.y = v.y, e.f = v.z, e.pw = v.w;
             return e;
         };
-        // (x, y) of anchor jl (local) at iteration i, for the window-start probes
-        auto fetch_xy = [&](int32_t jl) -> int2 {
-#if HYMET_CHAIN_PROBE_XY
-            if (i - jl <= kRing) {
-                const int4 v = ring[jl & kRingMask];
-                return make_int2(v.x, v.y);
-            }
-            if ((jl >> 6) == hb) {
-                const int4 v = hc[jl & 63];
-                return make_int2(v.x, v.y);
-            }
-            return make_int2((int32_t)P.ax[g0 + jl], (int32_t)P.ay[g0 + jl]);
-#else
-            const Ent e = fetch(jl);
-            return make_int2(e.x, e.y);
-#endif
+        // x of anchor jl (local) at iteration i, for the window-start probes: the x ring (last
+        // kXRing anchors), the head cache, else a plain load of ax
+        auto fetch_x = [&](int32_t jl) -> int32_t {
+            if (i - jl <= kXRing) return xring[jl & (kXRing - 1)];
+            if ((jl >> 6) == hb) return hc[jl & 63].x;
+            return (int32_t)P.ax[g0 + jl];
+        };
+        auto fetch_y = [&](int32_t jl) -> int32_t {
+            if (i - jl <= kRing) return ring[jl & kRingMask].y;
+            if ((jl >> 6) == hb) return hc[jl & 63].y;
+            return (int32_t)P.ay[g0 + jl];
         };
         int32_t i0 = 0, st = 0, st_in = 0;
         bool t_used = false;  // the overflow walk stamped t_global
+#if HYMET_CHAIN_HCPF
+        int32_t pfb = -1, pf_x = 0, pf_ylo = 0, pf_yhi = 0, pf_f = 0;  // block pfb's entries (lane l: entry l)
+        int64_t pf_p = 0;
+        auto hc_take = [&](int32_t b) -> Ent {  // entry (b << 6) + lane for the head cache, then prefetch b + 1
+            Ent e;
+            if (b == pfb) {
+                e.x = pf_x, e.y = pf_ylo, e.f = pf_f;
+                e.pw = (int32_t)((pf_p < 0 ? 0u : (uint32_t)(pf_p - g0 + 1)) | ((uint32_t)pf_yhi & 0xff) << 24);
+            } else {
+                e = fetch((b << 6) + lane);
+            }
+            const int32_t jn = ((b + 1) << 6) + lane;
+            if (((b + 1) << 6) + 63 < i0) {
+                const int32_t *ax32 = reinterpret_cast<const int32_t *>(P.ax + g0 + jn);
+                const int32_t *ay32 = reinterpret_cast<const int32_t *>(P.ay + g0 + jn);
+                pf_x = ax32[0], pf_ylo = ay32[0], pf_yhi = ay32[1];
+                pf_f = ld_l2(P.f + g0 + jn), pf_p = ld_l2(P.p + g0 + jn);
+                pfb = b + 1;
+            }
+            return e;
+        };
+#else
+        auto hc_take = [&](int32_t b) -> Ent { return fetch((b << 6) + lane); };
+#endif
         auto sum_at = [&](int32_t b, int k) -> int4 {  // word k of block b's summary
             if ((i0 >> 6) - b <= kSumRing) return ssum[(b & (kSumRing - 1)) * kSumInts + k];
             return ld_l2(gsum + (int64_t)b * kSumInts + k);
@@ -515,7 +536,6 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         int ih = 0, it = 0;
         bool iok = true;
         int32_t if_v = 0, ib_v = 0;
-        for (int e = lane; e < kInnerCap; e += 64) stamp[e] = -1;
         __builtin_amdgcn_wave_barrier();
         // double-buffered anchor chunks: lane l holds anchor (chunk base + l)
         uint64_t nx = 0, ny = 0, cx = 0, cy = 0;
@@ -733,10 +753,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 const int32_t bend = min(i, ((st >> 6) + 1) << 6);
                 const int32_t j = st + lane;
                 bool adv = false;
-                if (j < bend) {
-                    const int2 e = fetch_xy(j);
-                    adv = (int64_t)(uint32_t)xi > (int64_t)(uint32_t)e.x + P.max_dist || i0 - j > P.cap_rmq_size;
-                }
+                if (j < bend) adv = (int64_t)(uint32_t)xi > (int64_t)(uint32_t)fetch_x(j) + P.max_dist || i0 - j > P.cap_rmq_size;
                 const uint64_t m = __ballot(adv);
                 const int t = ~m ? __ffsll((unsigned long long)~m) - 1 : 64;  // lanes [0, t) advance
                 st += min(t, bend - st);
@@ -744,7 +761,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 // st entered a new block: cache it if it sits beyond the ring
                 if (st < i && (st >> 6) < (i0 >> 6) && i - st > kRing && (st >> 6) != hb) {
                     const int32_t hb2 = st >> 6;
-                    const Ent e = fetch((hb2 << 6) + lane);
+                    const Ent e = hc_take(hb2);
                     __builtin_amdgcn_wave_barrier();
                     hc[lane] = make_int4(e.x, e.y, e.f, e.pw);
                     __builtin_amdgcn_wave_barrier();
@@ -795,12 +812,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     if (st_in >= i) break;
                     const int32_t j = st_in + lane;
                     bool adv = false;
-                    int32_t yj = 0;
-                    if (j < i) {
-                        const int2 e = fetch_xy(j);
-                        yj = e.y;
-                        adv = (int64_t)(uint32_t)xi > (int64_t)(uint32_t)e.x + P.max_dist_inner || i0 - j > P.cap_rmq_size;
-                    }
+                    if (j < i) adv = (int64_t)(uint32_t)xi > (int64_t)(uint32_t)fetch_x(j) + P.max_dist_inner || i0 - j > P.cap_rmq_size;
                     const uint64_t m = __ballot(adv);
                     const int t = ~m ? __ffsll((unsigned long long)~m) - 1 : 64;
                     if (t > 1 && !overflow && ni > 0) {
@@ -825,6 +837,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         if (t < 64) break;
                         continue;
                     }
+                    const int32_t yj = lane < t && j < i0 ? fetch_y(j) : 0;  // keys of the leaving entries
                     for (int l = 0; l < t; ++l) {  // erase the passed entries from the inner list
                         const int32_t jj = st_in + l;
                         if (jj >= i0 || overflow) continue;
@@ -1030,6 +1043,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                             P.f[g0 + k] = fk;
                             P.p[g0 + k] = pk_local < 0 ? -1 : g0 + pk_local;
                             ring[k & kRingMask] = make_int4(kx, ky, fk, pw);
+                            xring[k & (kXRing - 1)] = kx;
                         }
                         __builtin_amdgcn_wave_barrier();
                         CCOUNT(7);
@@ -1195,9 +1209,10 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                             const int LA = mA ? __ffsll((unsigned long long)mA) - 1 : nl;  // y-bound break
                             const bool valid = lane < LA && w_l <= P.bw;
                             // t[p[j]] = i marks (a mark always points later in walk order)
-                            if (valid && pj >= st_in && pj < i0) stamp[pj % kInnerCap] = i;
-                            __builtin_amdgcn_wave_barrier();
-                            const bool stamped = valid && stamp[jl % kInnerCap] == i;
+                            if (valid && pj >= st_in && pj < i0) P.t_global[g0 + pj] = i + 1;
+                            t_used = true;
+                            __builtin_amdgcn_s_waitcnt(0);  // the stamps are in L2 before any lane reads one
+                            const bool stamped = valid && ld_l2(P.t_global + g0 + jl) == i + 1;
                             // running max_f before each candidate: exclusive prefix max
                             int incl = valid ? sc_l : INT32_MIN;
                             for (int d = 1; d < 64; d <<= 1) {
@@ -1275,7 +1290,10 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             P.f[g0 + i] = max_f;
             P.p[g0 + i] = max_j < 0 ? -1 : g0 + max_j;
             prev.x = xi, prev.y = yi, prev.f = max_f, prev.pw = (int32_t)((uint32_t)(max_j + 1) | (uint32_t)span_i << 24);
-            if (lane == 0) ring[i & kRingMask] = make_int4(prev.x, prev.y, prev.f, prev.pw);
+            if (lane == 0) {
+                ring[i & kRingMask] = make_int4(prev.x, prev.y, prev.f, prev.pw);
+                xring[i & (kXRing - 1)] = prev.x;
+            }
             __builtin_amdgcn_wave_barrier();
             ++i;
         }
