@@ -66,12 +66,6 @@ namespace {
 #ifndef HYMET_CHAIN_IDQ
 #define HYMET_CHAIN_IDQ 64
 #endif
-// Three anchor chunks in registers (current, next, after next): a colinear batch reads the
-// next chunk, which was then loaded one chunk earlier instead of just now.  On real C4
-// anchors (tools/chain_prof, 16.8M anchors) 97 -> 61 ms, despite 24 B/lane more spill.
-#ifndef HYMET_CHAIN_PF3
-#define HYMET_CHAIN_PF3 1
-#endif
 // A colinear batch's pre-batch best B from the O(1) window sources when they decide it.
 #ifndef HYMET_CHAIN_B0FAST
 #define HYMET_CHAIN_B0FAST 1
@@ -85,6 +79,10 @@ namespace {
 // batch's monotone values in O(1) when f + span rises and the priority falls along the batch.
 #ifndef HYMET_CHAIN_MONO
 #define HYMET_CHAIN_MONO 1
+#endif
+// Batch f / p global stores issued at the end of the commit instead of its start.
+#ifndef HYMET_CHAIN_LATE_FP
+#define HYMET_CHAIN_LATE_FP 1
 #endif
 // Head cache prefetch: when the head cache takes block b, block b + 1's entries are loaded
 // into registers, so the next window-start block change does not wait on HBM.
@@ -340,6 +338,55 @@ __device__ __forceinline__ double scan_min_d(double v) {  // inclusive prefix mi
     return v;
 }
 
+// ---- constant-offset lane exchanges without ds_bpermute: the compiler hoists a bpermute's
+// lane-address computation out of the loops and keeps it live (or spills it) for the whole
+// kernel -- ~20 VGPRs here -- while DPP / permlane forms need no address register.
+// lane l + 1's value (lane 63: its own), as __shfl_down(v, 1): DPP wave_shl:1
+__device__ __forceinline__ int down1(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xF, 0xF, false); }
+__device__ __forceinline__ double down1d(double v) {
+    return __hiloint2double(down1(__double2hiint(v)), down1(__double2loint(v)));
+}
+// lane 63 - l's value: row_mirror inside rows of 16, then row r <- row 3 - r
+__device__ __forceinline__ int rev64(int v) { return xrow16(xrow32(dpp<0x140>(v))); }
+__device__ __forceinline__ double rev64d(double v) {
+    return __hiloint2double(rev64(__double2hiint(v)), rev64(__double2loint(v)));
+}
+// sum over the wave, in every lane (butterflies: quad swaps, half-row and row mirrors, row swaps)
+__device__ __forceinline__ int wave_sum(int v) {
+    v += xstep<0>(v);
+    v += xstep<1>(v);
+    v += xstep<2>(v);
+    v += xstep<3>(v);
+    v += xstep<4>(v);
+    v += xstep<5>(v);
+    return v;
+}
+// inclusive prefix argmin of (p, j, y) by better(): ties -> larger j, j < 0 = none
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ void pargmin_step(double &p, int32_t &j, int32_t &y) {
+    const int lo = dppu<CTRL, ROWMASK>(0, __double2loint(p)), hi = dppu<CTRL, ROWMASK>(0, __double2hiint(p));
+    const int oj = dppu<CTRL, ROWMASK>(-1, j), oy = dppu<CTRL, ROWMASK>(0, y);
+    const double op = __hiloint2double(hi, lo);
+    if (better(op, oj, p, j)) p = op, j = oj, y = oy;
+}
+__device__ __forceinline__ void prefix_argmin(double &p, int32_t &j, int32_t &y) {
+    pargmin_step<0x111>(p, j, y);
+    pargmin_step<0x112>(p, j, y);
+    pargmin_step<0x114>(p, j, y);
+    pargmin_step<0x118>(p, j, y);
+    pargmin_step<0x142, 0xA>(p, j, y);
+    pargmin_step<0x143, 0xC>(p, j, y);
+}
+// argmin over lanes [l, 64) (the suffix), in lane l
+__device__ __forceinline__ void suffix_argmin(double &p, int32_t &j, int32_t &y) {
+    double rp = rev64d(p);
+    int32_t rj = rev64(j), ry = rev64(y);
+    prefix_argmin(rp, rj, ry);
+    p = rev64d(rp), j = rev64(rj), y = rev64(ry);
+}
+// max over lanes [l, 64), in lane l
+__device__ __forceinline__ int suffix_max(int v) { return rev64(scan_max(rev64(v))); }
+
 struct Ent {
     int32_t x, y, f, pw;  // pw = (p_local + 1) | span << 24
     __device__ int32_t p() const { return (pw & 0xFFFFFF) - 1; }
@@ -387,7 +434,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
     for (;;) {
         int w = 0;
         if (lane == 0) w = atomicAdd(P.work_counter, 1);
-        w = __shfl(w, 0, 64);
+        w = __builtin_amdgcn_readfirstlane(w);
         if (w >= n_work) break;
         const int g = P.order[w];
         GTIME_START
@@ -537,11 +584,17 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         bool iok = true;
         int32_t if_v = 0, ib_v = 0;
         __builtin_amdgcn_wave_barrier();
-        // double-buffered anchor chunks: lane l holds anchor (chunk base + l)
-        uint64_t nx = 0, ny = 0, cx = 0, cy = 0;
-#if HYMET_CHAIN_PF3
-        uint64_t nnx = 0, nny = 0;
-#endif
+        // anchor chunks in registers, lane l holding anchor (chunk base + l): the current one
+        // (cx, cy), the next (nx, ny) and the one after (nnx, nny).  Only x's low word is kept
+        // (x >> 32 is the group's constant); y keeps the query span in bits 32..39.
+        int32_t cx = 0, nx = 0, nnx = 0;
+        uint64_t cy = 0, ny = 0, nny = 0;
+        // unconditional loads (index clamped to the group): a `b < n ? load : 0` select made
+        // the compiler land each prefetch in a temporary and wait for it (vmcnt) to copy it
+        // into place, so the prefetch was synchronous.  Lanes past the group end hold copies of
+        // its last anchor, which nothing reads (batches stop at the group end).
+        auto ldx = [&](int32_t b) -> int32_t { return reinterpret_cast<const int32_t *>(P.ax + g0 + min(b, n - 1))[0]; };
+        auto ldy = [&](int32_t b) -> uint64_t { return P.ay[g0 + min(b, n - 1)]; };
         Ent prev{0, 0, 0, 0};  // anchor i-1
         // block b complete: staircase summary -- S1 = argmin, S(k+1) = argmin over y < y(Sk),
         // i.e. the entries better than every entry with y <= theirs, by y descending; the
@@ -559,7 +612,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             // y <= y_l are lanes [0, l], so l is a record iff it is the prefix best there
             // (ties -> the larger index, i.e. l itself: pl equals the inclusive prefix min),
             // its rank is the number of records in higher lanes, and the y range is lanes 0, 63
-            const int32_t ynx = __shfl_down(e.y, 1, 64);
+            const int32_t ynx = down1(e.y);
             if (__ballot(lane == 63 || e.y < ynx) == ~0ull) {
 #if HYMET_CHAIN_CBFAST
                 rec = scan_min_d(pl) == pl;
@@ -661,7 +714,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                             CCOUNT(1);
                             int cnt = 0;
                             for (int k = lane; k < ni; k += 64) cnt += key_less(L(k).x, L(k).y, ej.y, j);
-                            for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                            cnt = wave_sum(cnt);
                             pos = cnt;
                         }
                         for (int top = ni - 1; top >= pos; top -= 64) {  // shift [pos, ni) right by one
@@ -706,36 +759,24 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             GCNT(x, 1);
             CPROF(7);
             if ((i >> 6) != (cb >> 6)) {
-#if HYMET_CHAIN_PF3
-                // three chunks in registers: the batch reads chunk c+1, loaded a chunk earlier
-                if ((i >> 6) == (cb >> 6) + 1) {
-                    cx = nx, cy = ny, nx = nnx, ny = nny;
-                } else {
+                // three chunks in registers: the batch reads chunk c+1, loaded a chunk earlier.
+                // The rotation is unconditional (a jump first reloads the chunks it shifts in),
+                // so the new loads can land in nnx / nny's own registers.
+                if ((i >> 6) != (cb >> 6) + 1) {
                     const int32_t b = (i & ~63) + lane;
-                    cx = b < n ? P.ax[g0 + b] : 0;
-                    cy = b < n ? P.ay[g0 + b] : 0;
-                    nx = b + 64 < n ? P.ax[g0 + b + 64] : 0;
-                    ny = b + 64 < n ? P.ay[g0 + b + 64] : 0;
+                    nx = ldx(b), ny = ldy(b), nnx = ldx(b + 64), nny = ldy(b + 64);
                 }
+                // the rotation as opaque moves ahead of the loads: as plain assignments they became
+                // the merge's phi copies, placed after the loads -- which then had to land in
+                // temporaries and be waited for (vmcnt) before the copy
+                asm volatile("v_mov_b32 %0, %1" : "=v"(cx) : "v"(nx));
+                asm volatile("v_mov_b64 %0, %1" : "=v"(cy) : "v"(ny));
+                asm volatile("v_mov_b32 %0, %1" : "=v"(nx) : "v"(nnx));
+                asm volatile("v_mov_b64 %0, %1" : "=v"(ny) : "v"(nny));
                 cb = i & ~63;
-                const int32_t b = cb + 128 + lane;
-                nnx = b < n ? P.ax[g0 + b] : 0;
-                nny = b < n ? P.ay[g0 + b] : 0;
-#else
-                if ((i >> 6) == (cb >> 6) + 1) {
-                    cx = nx, cy = ny;
-                } else {
-                    const int32_t b = (i & ~63) + lane;
-                    cx = b < n ? P.ax[g0 + b] : 0;
-                    cy = b < n ? P.ay[g0 + b] : 0;
-                }
-                cb = i & ~63;
-                const int32_t b = cb + 64 + lane;
-                nx = b < n ? P.ax[g0 + b] : 0;
-                ny = b < n ? P.ay[g0 + b] : 0;
-#endif
+                nnx = ldx(cb + 128 + lane), nny = ldy(cb + 128 + lane);
             }
-            const int32_t xi = rl((int32_t)cx, i & 63);
+            const int32_t xi = rl(cx, i & 63);
             const int32_t yi = rl((int32_t)cy, i & 63);
             const int32_t span_i = rl((int32_t)(cy >> 32 & 0xff), i & 63);
             int32_t max_f = span_i;
@@ -787,16 +828,12 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 int32_t pj = j, py = e.y;
 #if HYMET_CHAIN_MONO
                 // priorities non-increasing along the block: every suffix's argmin is lane 63
-                const double pnx = __shfl_down(pr, 1, 64);
+                const double pnx = down1d(pr);
                 if (__ballot(lane == 63 || !(pr < pnx)) == ~0ull) {
                     pr = rld(pr, 63), pj = (b << 6) + 63, py = rl(e.y, 63);
                 } else
 #endif
-                for (int d = 1; d < 64; d <<= 1) {
-                    const double op = __shfl_down(pr, d, 64);
-                    const int32_t oj = __shfl_down(pj, d, 64), oy = __shfl_down(py, d, 64);
-                    if (lane + d < 64 && better(op, oj, pr, pj)) pr = op, pj = oj, py = oy;
-                }
+                    suffix_argmin(pr, pj, py);
                 __builtin_amdgcn_wave_barrier();
                 hc[lane] = make_int4(e.x, e.y, e.f, e.pw);
                 hsuf[lane] = pack_st(pr, pj, py);
@@ -873,7 +910,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         CCOUNT(2);
                         int cnt = 0;
                         for (int k = lane; k < ni; k += 64) cnt += key_less(L(k).x, L(k).y, y, jj);
-                        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                        cnt = wave_sum(cnt);
                         for (int b = cnt; b < ni - 1; b += 64) {  // shift (cnt, ni) left by one
                             const int k = b + lane + 1;
                             int2 v;
@@ -951,10 +988,10 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     AMARK(batch_begin);
                     // anchors k = i + lane from the chunk registers (cx: [cb, cb+64), nx: next 64)
                     const int off = (i - cb) + lane;
-                    const uint64_t kx_lo = __shfl(cx, off & 63, 64), kx_hi = __shfl(nx, off & 63, 64);
+                    const int32_t kx_lo = __shfl(cx, off & 63, 64), kx_hi = __shfl(nx, off & 63, 64);
                     const uint64_t ky_lo = __shfl(cy, off & 63, 64), ky_hi = __shfl(ny, off & 63, 64);
                     const bool inb = lane < Lb;
-                    const int32_t kx = (int32_t)(off < 64 ? kx_lo : kx_hi);
+                    const int32_t kx = off < 64 ? kx_lo : kx_hi;
                     const uint64_t kyy = off < 64 ? ky_lo : ky_hi;
                     const int32_t ky = (int32_t)kyy, ksp = (int32_t)(kyy >> 32 & 0xff);
                     const int32_t px = shr1(kx, prev.x), py = shr1(ky, prev.y), psp = shr1(ksp, prev.sp());
@@ -1040,8 +1077,10 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         const int32_t pk_local = linked ? k - 1 : -1;
                         const int32_t pw = (int32_t)((uint32_t)(pk_local + 1) | (uint32_t)ksp << 24);
                         if (lane < acc) {
+#if !HYMET_CHAIN_LATE_FP
                             P.f[g0 + k] = fk;
                             P.p[g0 + k] = pk_local < 0 ? -1 : g0 + pk_local;
+#endif
                             ring[k & kRingMask] = make_int4(kx, ky, fk, pw);
                             xring[k & (kXRing - 1)] = kx;
                         }
@@ -1053,12 +1092,13 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         if (nins > 0) {
                             if (P.max_dist_inner > 0) {
                                 // list: shift [gpos, ni) right by nins, batch keys into [gpos, gpos + nins)
-                                {
+                                if (gpos < ni) {  // (the ring index is always in bounds: read unconditionally)
                                     const int kk = gpos + lane;
-                                    int2 v;
-                                    if (kk < ni) v = L(kk);
+                                    const int2 v = L(kk);
                                     __builtin_amdgcn_wave_barrier();
                                     if (kk < ni) L(kk + nins) = v;
+                                }
+                                {
                                     if (lane < nins) L(gpos + lane) = make_int2(ky, k);
                                     __builtin_amdgcn_wave_barrier();
                                 }
@@ -1073,18 +1113,15 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
 #if HYMET_CHAIN_MONO
                                 // f + span increasing along the batch (colinear): the last entry
                                 // is the only record and the maximum
-                                const int vnx = __shfl_down(v, 1, 64);
+                                const int vnx = down1(v);
                                 if (__ballot(lane >= nins - 1 || v < vnx) == ~0ull) {
                                     run = rl(v, nins - 1);
                                     sfx = lane < nins - 1 ? run : INT32_MIN;
                                 } else
 #endif
                                 {
-                                    for (int d = 1; d < 64; d <<= 1) {
-                                        const int o = __shfl_down(run, d, 64);
-                                        if (lane + d < 64) run = max(run, o);
-                                    }
-                                    sfx = __shfl_down(run, 1, 64);
+                                    run = suffix_max(run);
+                                    sfx = down1(run);
                                     if (lane == 63) sfx = INT32_MIN;
                                 }
                                 const int vmax = rl(run, 0);
@@ -1136,6 +1173,14 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                             i0 = i + nins;
                         }
                         const int l = acc - 1;
+#if HYMET_CHAIN_LATE_FP
+                        // the batch's f / p stores go last: a vector-memory wait inside the commit
+                        // (e.g. a spill reload) would otherwise wait for them too (vmcnt is in order)
+                        if (lane < acc) {
+                            P.f[g0 + k] = fk;
+                            P.p[g0 + k] = pk_local < 0 ? -1 : g0 + pk_local;
+                        }
+#endif
                         prev.x = rl(kx, l), prev.y = rl(ky, l), prev.f = rl(fk, l), prev.pw = rl(pw, l);
                         i += acc;
                         AMARK(batch_end);
@@ -1191,7 +1236,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         // walk the list downwards from the last entry with y <= yi - 1
                         int cnt = 0;
                         for (int e = lane; e < ni; e += 64) cnt += L(e).x < yi;
-                        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                        cnt = wave_sum(cnt);
                         int nsk = 0;
                         for (int top = cnt - 1; top >= 0; top -= 64) {
                             const int e = top - lane;
@@ -1214,25 +1259,13 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                             __builtin_amdgcn_s_waitcnt(0);  // the stamps are in L2 before any lane reads one
                             const bool stamped = valid && ld_l2(P.t_global + g0 + jl) == i + 1;
                             // running max_f before each candidate: exclusive prefix max
-                            int incl = valid ? sc_l : INT32_MIN;
-                            for (int d = 1; d < 64; d <<= 1) {
-                                const int o = __shfl_up(incl, d, 64);
-                                if (lane >= d) incl = max(incl, o);
-                            }
-                            int excl = __shfl_up(incl, 1, 64);
-                            if (lane == 0) excl = INT32_MIN;
-                            excl = max(excl, max_f);
+                            const int incl = scan_max(valid ? sc_l : INT32_MIN);
+                            const int excl = max(shr1(incl, INT32_MIN), max_f);
                             const bool imp = valid && sc_l > excl;
                             // n_skip: improve -> max(s-1, 0); stamped -> s+1; as max-plus maps s -> max(s+a, b)
                             int a = imp ? -1 : (valid && stamped ? 1 : 0);
                             int bb = imp ? 0 : kNegInf;
-                            for (int d = 1; d < 64; d <<= 1) {
-                                const int ao = __shfl_up(a, d, 64), bo = __shfl_up(bb, d, 64);
-                                if (lane >= d) {
-                                    bb = max(bo + a, bb);
-                                    a = ao + a;
-                                }
-                            }
+                            scan_maxplus(a, bb);
                             const int s = max(nsk + a, bb);
                             const uint64_t mB = __ballot(valid && !imp && stamped && s > P.max_chn_skip);
                             const int LB = mB ? __ffsll((unsigned long long)mB) - 1 : 64;
@@ -1259,10 +1292,15 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                                 const bool below = first ? (yj <= yi - 1) : key_less(yj, j, cy_, cj);
                                 if (below && (bjl == INT32_MIN || key_less(by, bjl, yj, j))) by = yj, bjl = j;
                             }
-                            for (int o = 32; o > 0; o >>= 1) {
-                                const int32_t oy = __shfl_xor(by, o, 64), oj = __shfl_xor(bjl, o, 64);
+                            auto take = [&](int32_t oy, int32_t oj) {
                                 if (oj != INT32_MIN && (bjl == INT32_MIN || key_less(by, bjl, oy, oj))) by = oy, bjl = oj;
-                            }
+                            };
+                            take(xstep<0>(by), xstep<0>(bjl));
+                            take(xstep<1>(by), xstep<1>(bjl));
+                            take(xstep<2>(by), xstep<2>(bjl));
+                            take(xstep<3>(by), xstep<3>(bjl));
+                            take(xstep<4>(by), xstep<4>(bjl));
+                            take(xstep<5>(by), xstep<5>(bjl));
                             if (bjl == INT32_MIN) break;
                             first = false;
                             cy_ = by, cj = bjl;

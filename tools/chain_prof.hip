@@ -28,9 +28,11 @@ int main(int argc, char **argv) {
     }
     FILE *fp = fopen(argv[1], "rb");
     if (!fp) return 2;
-    std::vector<uint64_t> a;
-    uint64_t v[2];
-    while (fread(v, 8, 2, fp) == 2) a.push_back(v[0]), a.push_back(v[1]);
+    fseek(fp, 0, SEEK_END);
+    const long bytes = ftell(fp);
+    fseek(fp, 0, SEEK_SET);
+    std::vector<uint64_t> a((size_t)bytes / 16 * 2);
+    if (fread(a.data(), 16, a.size() / 2, fp) != a.size() / 2) return 2;
     fclose(fp);
     const int64_t n = (int64_t)a.size() / 2;
     const int bw = atoi(argv[2]);
