@@ -830,21 +830,14 @@ __global__ void chain_list_kernel(const int64_t *g_start, const int32_t *n_chain
 
 // anchors per chain in the compacted copy; with a long join (qflag), chains of flagged
 // queries are left out of the copy and counted in cnt2 instead (they are only marked)
-// (with qflag: copied[i] = the chain is copied, for the list of copied chains)
 __global__ void chain_cnt_kernel(const uint64_t *cu, const uint32_t *cq, const uint32_t *qflag, int64_t n, uint32_t *cnt,
-                                 uint32_t *cnt2, uint32_t *copied) {
+                                 uint32_t *cnt2) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t m = (uint32_t)cu[i];
     const bool fl = qflag && qflag[cq[i]];
     cnt[i] = fl ? 0u : m;
     if (cnt2) cnt2[i] = fl ? m : 0u;
-    if (copied) copied[i] = fl ? 0u : 1u;
-}
-
-__global__ void copied_list_kernel(const uint32_t *copied, const int64_t *pos, int64_t n, int32_t *list) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && copied[i]) list[pos[i]] = (int32_t)i;
 }
 
 // long join, first pass (map.c's rmq rescue): a query is re-chained when it has more than one
@@ -880,31 +873,30 @@ __global__ void chain_qb_kernel(const int64_t *qc, const int64_t *bpos, int64_t 
 __global__ __launch_bounds__(256) void chain_copy_kernel(const uint64_t *cu, const int64_t *cfirst, const int64_t *bpos,
                                                          const int64_t *chain_ids, const uint64_t *ax, const uint64_t *ay,
                                                          int64_t n_chain, int64_t nb, uint64_t *bx, uint64_t *by,
-                                                         int32_t *bchain, const int32_t *clist) {
-    // flat over the output anchors: the block's first chain k0 by binary search over the chain
-    // starts; the starts of the next 256 chains are staged in LDS and each lane finds its chain
-    // by an 8-step search there (a forward walk per lane cost up to 255 dependent loads where
-    // chains are short).  With a list of the copied chains (clist, n_chain entries) every
-    // listed chain holds >= 1 anchor, so the 257 staged starts always cover the block; without
-    // one (every chain copied) the same holds.  The last fallback only guards the bounds.
-    __shared__ int64_t s_k0;
-    __shared__ int32_t s_st[257];  // block-relative starts of chains k0 .. k0 + 256 (clamped)
-    auto chain_at = [&](int64_t k) -> int64_t { return clist ? (int64_t)clist[k] : k; };
+                                                         int32_t *bchain) {
+    // flat over the output anchors (~48 B each, bandwidth-bound: C4 copies ~236 M per batch at
+    // ~3.8 TB/s): the block's first chain c0 by binary search over bpos; the starts of the next
+    // 256 chains are staged in LDS and each lane finds its chain by an 8-step search there (a
+    // forward walk per lane cost up to 255 dependent loads where chains are short).  Chains
+    // left out of the copy have no anchors, so more than 256 may start in the block: lanes
+    // past the staged ones search bpos itself.
+    __shared__ int64_t s_c0;
+    __shared__ int32_t s_st[257];  // block-relative starts of chains c0 .. c0 + 256 (clamped)
     const int64_t b0 = (int64_t)blockIdx.x * blockDim.x;
     if (threadIdx.x == 0) {
-        int64_t lo = 0, hi = n_chain - 1;  // last k with start(k) <= b0
+        int64_t lo = 0, hi = n_chain - 1;  // last c with bpos[c] <= b0
         while (lo < hi) {
             const int64_t mid = (lo + hi + 1) >> 1;
-            if (bpos[chain_at(mid)] <= b0) lo = mid;
+            if (bpos[mid] <= b0) lo = mid;
             else hi = mid - 1;
         }
-        s_k0 = lo;
+        s_c0 = lo;
     }
     __syncthreads();
-    const int64_t k0 = s_k0;
+    const int64_t c0 = s_c0;
     for (int i = threadIdx.x; i < 257; i += blockDim.x) {
-        const int64_t k = k0 + i;
-        s_st[i] = k < n_chain ? (int32_t)min(bpos[chain_at(k)] - b0, (int64_t)256) : 256;
+        const int64_t c = c0 + i;
+        s_st[i] = c < n_chain ? (int32_t)min(bpos[c] - b0, (int64_t)256) : 256;
     }
     __syncthreads();
     const int64_t b = b0 + threadIdx.x;
@@ -915,17 +907,16 @@ __global__ __launch_bounds__(256) void chain_copy_kernel(const uint64_t *cu, con
         if (s_st[mid] <= (int)threadIdx.x) lo = mid;
         else hi = mid - 1;
     }
-    int64_t k = k0 + lo;
-    if (lo == 256) {  // last k with start(k) <= b beyond the staged chains
-        int64_t l2 = k, h2 = n_chain - 1;
+    int64_t c = c0 + lo;
+    if (lo == 256) {  // last c with bpos[c] <= b beyond the staged chains
+        int64_t l2 = c, h2 = n_chain - 1;
         while (l2 < h2) {
             const int64_t mid = (l2 + h2 + 1) >> 1;
-            if (bpos[chain_at(mid)] <= b) l2 = mid;
+            if (bpos[mid] <= b) l2 = mid;
             else h2 = mid - 1;
         }
-        k = l2;
+        c = l2;
     }
-    const int64_t c = chain_at(k);
     const int32_t m = (int32_t)cu[c];
     const int64_t a = chain_ids[cfirst[c] + m - 1 - (b - bpos[c])];  // backtrack stores end -> start
     bx[b] = ax[a];
@@ -1446,31 +1437,22 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
             if (lj->mark_only) qflag = lj->flag.as<uint32_t>();
         }
         // anchors of every chain (but those only marked), compacted in chain order
-        DevBuf ccnt, ccnt2, copied, kpos, clist;
+        DevBuf ccnt, ccnt2;
         HY_HIP(ccnt.alloc(4 * (size_t)(NC + 1), ctx->stream));
-        if (qflag) {
-            HY_HIP(ccnt2.alloc(4 * (size_t)(NC + 1), ctx->stream));
-            HY_HIP(copied.alloc(4 * (size_t)(NC + 1), ctx->stream));
-        }
+        if (qflag) HY_HIP(ccnt2.alloc(4 * (size_t)(NC + 1), ctx->stream));
         LAUNCH1(chain_cnt_kernel, NC, C.cu.as<uint64_t>(), cq.as<uint32_t>(), qflag, NC, ccnt.as<uint32_t>(),
-                qflag ? ccnt2.as<uint32_t>() : nullptr, qflag ? copied.as<uint32_t>() : nullptr);
-        int64_t NB = 0, NCC = NC;
+                qflag ? ccnt2.as<uint32_t>() : nullptr);
+        int64_t NB = 0;
         rc = scan_flags(ctx, ccnt.as<uint32_t>(), NC, C.cboff, &NB);
         if (rc) return rc;
-        if (qflag && NB > 0) {  // most chains are only marked: list the copied ones for chain_copy
-            rc = scan_flags(ctx, copied.as<uint32_t>(), NC, kpos, &NCC);
-            if (rc) return rc;
-            HY_HIP(clist.alloc(4 * (size_t)(NCC + 1), ctx->stream));
-            LAUNCH1(copied_list_kernel, NC, copied.as<uint32_t>(), kpos.as<int64_t>(), NC, clist.as<int32_t>());
-        }
         C.n_anchor = NB;
         HY_HIP(C.bx.alloc(8 * (size_t)(NB + 1), ctx->stream));
         HY_HIP(C.by.alloc(8 * (size_t)(NB + 1), ctx->stream));
         HY_HIP(C.bchain.alloc(4 * (size_t)(NB + 1), ctx->stream));
         if (NC > 0 && NB > 0)
             LAUNCH1(chain_copy_kernel, NB, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), C.cboff.as<int64_t>(),
-                    chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NCC, NB, C.bx.as<uint64_t>(),
-                    C.by.as<uint64_t>(), C.bchain.as<int32_t>(), clist.p ? clist.as<int32_t>() : nullptr);
+                    chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, NB, C.bx.as<uint64_t>(),
+                    C.by.as<uint64_t>(), C.bchain.as<int32_t>());
         HY_HIP(C.d_qb.alloc(8 * (size_t)(n_q + 1), ctx->stream));
         LAUNCH1(chain_qb_kernel, n_q + 1, C.d_qc.as<int64_t>(), C.cboff.as<int64_t>(), NC, NB, n_q, C.d_qb.as<int64_t>());
         if (qflag) {  // the re-chained queries' chain anchors: per-query counts, and t handed over
