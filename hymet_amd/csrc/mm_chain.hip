@@ -754,28 +754,33 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             AMARK(ins_end);
         };
         int32_t cb = -128;  // base of the chunk in cx/cy; nx/ny hold the next one
+        // make chunk (ii >> 6) current.  Called at the end of each iteration for the next i,
+        // ahead of that iteration's f / p stores: the rotation's copies wait (vmcnt, counted in
+        // issue order) for the previous prefetch, and would otherwise wait for those stores too.
+        auto advance = [&](int32_t ii) {
+            if ((ii >> 6) == (cb >> 6) || ii >= n) return;
+            // three chunks in registers: the batch reads chunk c+1, loaded a chunk earlier.
+            // The rotation is unconditional (a jump first reloads the chunks it shifts in),
+            // so the new loads can land in nnx / nny's own registers.
+            if ((ii >> 6) != (cb >> 6) + 1) {
+                const int32_t b = (ii & ~63) + lane;
+                nx = ldx(b), ny = ldy(b), nnx = ldx(b + 64), nny = ldy(b + 64);
+            }
+            // the rotation as opaque moves ahead of the loads: as plain assignments they became
+            // the merge's phi copies, placed after the loads -- which then had to land in
+            // temporaries and be waited for (vmcnt) before the copy
+            asm volatile("v_mov_b32 %0, %1" : "=v"(cx) : "v"(nx));
+            asm volatile("v_mov_b64 %0, %1" : "=v"(cy) : "v"(ny));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(nx) : "v"(nnx));
+            asm volatile("v_mov_b64 %0, %1" : "=v"(ny) : "v"(nny));
+            cb = ii & ~63;
+            nnx = ldx(cb + 128 + lane), nny = ldy(cb + 128 + lane);
+        };
         int32_t spec_next = 0, spec_gap = 2;  // next batch attempt (back-off after short batches)
         for (; i < n;) {
             GCNT(x, 1);
             CPROF(7);
-            if ((i >> 6) != (cb >> 6)) {
-                // three chunks in registers: the batch reads chunk c+1, loaded a chunk earlier.
-                // The rotation is unconditional (a jump first reloads the chunks it shifts in),
-                // so the new loads can land in nnx / nny's own registers.
-                if ((i >> 6) != (cb >> 6) + 1) {
-                    const int32_t b = (i & ~63) + lane;
-                    nx = ldx(b), ny = ldy(b), nnx = ldx(b + 64), nny = ldy(b + 64);
-                }
-                // the rotation as opaque moves ahead of the loads: as plain assignments they became
-                // the merge's phi copies, placed after the loads -- which then had to land in
-                // temporaries and be waited for (vmcnt) before the copy
-                asm volatile("v_mov_b32 %0, %1" : "=v"(cx) : "v"(nx));
-                asm volatile("v_mov_b64 %0, %1" : "=v"(cy) : "v"(ny));
-                asm volatile("v_mov_b32 %0, %1" : "=v"(nx) : "v"(nnx));
-                asm volatile("v_mov_b64 %0, %1" : "=v"(ny) : "v"(nny));
-                cb = i & ~63;
-                nnx = ldx(cb + 128 + lane), nny = ldy(cb + 128 + lane);
-            }
+            advance(i);
             const int32_t xi = rl(cx, i & 63);
             const int32_t yi = rl((int32_t)cy, i & 63);
             const int32_t span_i = rl((int32_t)(cy >> 32 & 0xff), i & 63);
@@ -1072,6 +1077,9 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     }
                     AMARK(batch_verified);
                     if (acc > 0) {
+                        // the next iteration's chunks first: nothing below reads the chunk
+                        // registers, and the rotation then waits on no store of this commit
+                        advance(i + acc);
                         // commit anchors [i, i + acc): f, p, ring; insert entries [i, i + acc - 1)
                         const int32_t k = i + lane;
                         const int32_t pk_local = linked ? k - 1 : -1;
@@ -1324,6 +1332,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 }
             }
             CPROF(4);
+            advance(i + 1);
             // every lane stores the same values: later global loads by any lane see them
             P.f[g0 + i] = max_f;
             P.p[g0 + i] = max_j < 0 ? -1 : g0 + max_j;
