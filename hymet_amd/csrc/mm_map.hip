@@ -68,7 +68,6 @@ __global__ void fill_qid_kernel(const int64_t *off, int n_q, int64_t n, uint32_t
     if (zq && i < n_q) zq[i] = 0;
 }
 
-// mailbox flag: some query has more than lim minimizers (the host zeroes the word first)
 // per query: its chain anchors when the long join re-chains it, else 0; entry n_q = 0 (the
 // scan's total slot); *any = 1 when some query is flagged (the host zeroes the word first)
 __global__ void flagged_len_kernel(const uint32_t *flag, const int64_t *qb, int n_q, uint32_t *cnt, int64_t *any) {
@@ -81,11 +80,6 @@ __global__ void flagged_len_kernel(const uint32_t *flag, const int64_t *qb, int 
     const bool f = flag[q] != 0;
     cnt[q] = f ? (uint32_t)(qb[q + 1] - qb[q]) : 0u;
     if (f) *any = 1;
-}
-
-__global__ void any_over_kernel(const int64_t *off, int n_q, int64_t lim, int64_t *flag) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < n_q && off[q + 1] - off[q] > lim) *flag = 1;
 }
 
 __global__ void iota_u32_kernel(uint32_t *a, int64_t n) {
@@ -113,6 +107,64 @@ __global__ void mzflt_runs_kernel(const uint32_t *sq, const uint64_t *sx, const 
     const int32_t cnt = (int32_t)(e - p);
     if (cnt > q_occ_max && (float)cnt > (float)nq * q_occ_frac)
         for (int64_t j = p; j < e; j++) keep[sidx[j]] = 0;
+}
+
+// mm_seed_mz_flt screen, one block per query: its minimizers are counted into 4096 LDS
+// buckets by hash.  A bucket's count bounds the count of every x in it, so a query whose
+// buckets all stay at or below q_occ_max has no run to drop (exactly: the filter needs
+// cnt > q_occ_max); the others get cnt[q] = their minimizer count and go to the exact (q, x)
+// sort.  Also sets keep = 1 for every minimizer.  Block n_q writes the scan's total slot.
+constexpr int kMzBuckets = 4096;
+__global__ __launch_bounds__(256) void mzflt_screen_kernel(const uint64_t *mx, const int64_t *qm_off, int n_q, int q_occ_max,
+                                                           uint32_t *keep, uint32_t *cnt, int64_t *any) {
+    __shared__ uint32_t h[kMzBuckets];
+    __shared__ int hit;
+    const int q = blockIdx.x;
+    if (q == n_q) {
+        if (threadIdx.x == 0) cnt[q] = 0;
+        return;
+    }
+    const int64_t s = qm_off[q], nq = qm_off[q + 1] - s;
+    for (int64_t e = threadIdx.x; e < nq; e += 256) keep[s + e] = 1u;
+    if (nq <= q_occ_max) {  // mm_seed_mz_flt returns early for this query
+        if (threadIdx.x == 0) cnt[q] = 0;
+        return;
+    }
+    for (int b = threadIdx.x; b < kMzBuckets; b += 256) h[b] = 0;
+    if (threadIdx.x == 0) hit = 0;
+    __syncthreads();
+    bool over = false;
+    for (int64_t e = threadIdx.x; e < nq; e += 256)
+        over |= atomicAdd(&h[(uint32_t)(mx[s + e] >> 8) & (kMzBuckets - 1)], 1u) >= (uint32_t)q_occ_max;
+    if (over) hit = 1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        cnt[q] = hit ? (uint32_t)nq : 0u;
+        if (hit) *any = 1;
+    }
+}
+
+// the flagged queries' minimizers as one list: global index and query per list entry
+__global__ __launch_bounds__(256) void mzflt_list_kernel(const int64_t *qm_off, const uint32_t *cnt, const int64_t *coff,
+                                                         uint32_t *gidx, uint32_t *sq) {
+    const int q = blockIdx.x;
+    const uint32_t nq = cnt[q];
+    if (nq == 0) return;
+    const int64_t s = qm_off[q], d = coff[q];
+    for (uint32_t e = threadIdx.x; e < nq; e += 256) {
+        gidx[d + e] = (uint32_t)(s + e);
+        sq[d + e] = (uint32_t)q;
+    }
+}
+
+// out[i] = src[idx[i]] as u64 (x of a list entry) and gout[i] = gidx[perm[i]]
+__global__ void mzflt_gather_kernel(const uint32_t *perm, const uint32_t *gidx, const uint64_t *mx, uint32_t *gout,
+                                    uint64_t *xout, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t g = gidx[perm[i]];
+    gout[i] = g;
+    xout[i] = mx[g];
 }
 
 // (also completes the exclusive scan: pos[n] = the kept total)
@@ -1647,36 +1699,54 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     }
     // ------------------------------------------------------- 2 mm_seed_mz_flt
     bool need_flt = false;
-    if (opt->q_occ_frac > 0.0f && M > 0) {  // only queries with more than mid_occ minimizers are filtered
+    DevBuf keep, fcnt, fcoff;
+    int64_t MF = 0;  // minimizers of the queries the screen could not clear
+    if (opt->q_occ_frac > 0.0f && M > 0 && opt->mid_occ > 0) {  // only queries with more than mid_occ minimizers are filtered
+        HY_HIP(keep.alloc(4 * (size_t)M, st));
+        HY_HIP(fcnt.alloc(4 * (size_t)(n_q + 1), st));
         ctx->mbox_h[kMbFlag] = 0;
-        LAUNCH1(any_over_kernel, n_q, qm_off.as<int64_t>(), n_q, (int64_t)opt->mid_occ, mb_dev(ctx, kMbFlag));
+        hipLaunchKernelGGL(mzflt_screen_kernel, dim3((unsigned)n_q + 1), dim3(256), 0, st, mx.as<uint64_t>(), qm_off.as<int64_t>(),
+                           n_q, opt->mid_occ, keep.as<uint32_t>(), fcnt.as<uint32_t>(), mb_dev(ctx, kMbFlag));
+        HY_CHECK_LAUNCH("mzflt_screen_kernel");
         HY_HIP(hipStreamSynchronize(st));
-        need_flt = mb_read(ctx, kMbFlag) != 0;
+        if (mb_read(ctx, kMbFlag) != 0) {
+            HY_HIP(fcoff.alloc(8 * (size_t)(n_q + 1), st));
+            rc = exclusive_scan_u32_i64(ctx, fcnt.as<uint32_t>(), fcoff.as<int64_t>(), n_q + 1, &MF);
+            if (rc) return rc;
+        }
     }
     tr.mark("sketch");
-    if (need_flt) {
-        DevBuf qid, sx, sx2, sidx, sidx2, sq, sq2, keep, kpos, nx, ny;
-        HY_HIP(qid.alloc(4 * (size_t)M, st));
-        HY_HIP(keep.alloc(4 * (size_t)M, st));
-        LAUNCH1(fill_qid_kernel, M, qm_off.as<int64_t>(), n_q, M, qid.as<uint32_t>(), keep.as<uint32_t>(), nullptr);
-        HY_HIP(sx.alloc(8 * (size_t)M, st));
-        HY_HIP(sx2.alloc(8 * (size_t)M, st));
-        HY_HIP(sidx.alloc(4 * (size_t)M, st));
-        HY_HIP(sidx2.alloc(4 * (size_t)M, st));
-        HY_HIP(hipMemcpyAsync(sx.p, mx.p, 8 * (size_t)M, hipMemcpyDeviceToDevice, st));
-        LAUNCH1(iota_u32_kernel, M, sidx.as<uint32_t>(), M);
+    if (MF > 0) {
+        // the exact filter over the flagged queries' minimizers only: list entries sorted by x,
+        // then stably by query, runs of equal (q, x) counted
+        need_flt = true;
+        DevBuf gidx, sx, sx2, sidx, sidx2, sq0, sq, sq2, kpos, nx, ny, gx, gg;
+        HY_HIP(gidx.alloc(4 * (size_t)MF, st));
+        HY_HIP(sq0.alloc(4 * (size_t)MF, st));
+        hipLaunchKernelGGL(mzflt_list_kernel, dim3((unsigned)n_q), dim3(256), 0, st, qm_off.as<int64_t>(), fcnt.as<uint32_t>(),
+                           fcoff.as<int64_t>(), gidx.as<uint32_t>(), sq0.as<uint32_t>());
+        HY_CHECK_LAUNCH("mzflt_list_kernel");
+        HY_HIP(sx.alloc(8 * (size_t)MF, st));
+        HY_HIP(sx2.alloc(8 * (size_t)MF, st));
+        HY_HIP(sidx.alloc(4 * (size_t)MF, st));
+        HY_HIP(sidx2.alloc(4 * (size_t)MF, st));
+        LAUNCH1(gather_kernel<uint64_t>, MF, mx.as<uint64_t>(), gidx.as<uint32_t>(), sx.as<uint64_t>(), MF);
+        LAUNCH1(iota_u32_kernel, MF, sidx.as<uint32_t>(), MF);
         uint64_t *kx = sx.as<uint64_t>(), *kxa = sx2.as<uint64_t>();
         uint32_t *vi = sidx.as<uint32_t>(), *via = sidx2.as<uint32_t>();
-        rc = sort_pairs(ctx, kx, kxa, vi, via, M, 0, 2 * k + 8, "radix_sort_mz");
+        rc = sort_pairs(ctx, kx, kxa, vi, via, MF, 0, 2 * k + 8, "radix_sort_mz");
         if (rc) return rc;
-        HY_HIP(sq.alloc(4 * (size_t)M, st));
-        HY_HIP(sq2.alloc(4 * (size_t)M, st));
-        LAUNCH1(gather_kernel<uint32_t>, M, qid.as<uint32_t>(), vi, sq.as<uint32_t>(), M);
+        HY_HIP(sq.alloc(4 * (size_t)MF, st));
+        HY_HIP(sq2.alloc(4 * (size_t)MF, st));
+        LAUNCH1(gather_kernel<uint32_t>, MF, sq0.as<uint32_t>(), vi, sq.as<uint32_t>(), MF);
         uint32_t *kq = sq.as<uint32_t>(), *kqa = sq2.as<uint32_t>();
-        rc = sort_pairs(ctx, kq, kqa, vi, via, M, 0, bits_for(n_q), "radix_sort_mz");
+        rc = sort_pairs(ctx, kq, kqa, vi, via, MF, 0, bits_for(n_q), "radix_sort_mz");
         if (rc) return rc;
-        LAUNCH1(gather_kernel<uint64_t>, M, mx.as<uint64_t>(), vi, kxa, M);  // x in (q, x) order
-        LAUNCH1(mzflt_runs_kernel, M, kq, kxa, vi, qm_off.as<int64_t>(), M, opt->mid_occ, opt->q_occ_frac, keep.as<uint32_t>());
+        HY_HIP(gx.alloc(8 * (size_t)MF, st));
+        HY_HIP(gg.alloc(4 * (size_t)MF, st));
+        LAUNCH1(mzflt_gather_kernel, MF, vi, gidx.as<uint32_t>(), mx.as<uint64_t>(), gg.as<uint32_t>(), gx.as<uint64_t>(), MF);
+        LAUNCH1(mzflt_runs_kernel, MF, kq, gx.as<uint64_t>(), gg.as<uint32_t>(), qm_off.as<int64_t>(), MF, opt->mid_occ,
+                opt->q_occ_frac, keep.as<uint32_t>());
         int64_t M2 = 0;
         rc = scan_flags(ctx, keep.as<uint32_t>(), M, kpos, &M2);
         if (rc) return rc;

@@ -6,7 +6,7 @@ REPO=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$REPO/gpurun_out/chain_ab
 mkdir -p $OUT
 cd $REPO
-HYMET_DUMP_ANCHORS=/tmp/anchors.bin HYMET_DUMP_ANCHORS2=/tmp/anchors2.bin timeout -k 10 400 python3 bench.py --steps 1 --warmup 0 --no-cpu --contig-gbp 0.1 > $OUT/bench.json 2> $OUT/bench.err || exit $?
+HYMET_DUMP_MAX=${DUMP_MAX:-300000000} HYMET_DUMP_ANCHORS=/tmp/anchors.bin HYMET_DUMP_ANCHORS2=/tmp/anchors2.bin timeout -k 10 400 python3 bench.py --steps 1 --warmup 0 --no-cpu --contig-gbp 0.1 > $OUT/bench.json 2> $OUT/bench.err || exit $?
 for b in "$@"; do
   timeout -k 10 200 tools/$b /tmp/anchors.bin 1000 > $OUT/$b.txt 2>&1 || exit $?
   [ -z "$LONG" ] || timeout -k 10 200 tools/$b /tmp/anchors2.bin 100000 > $OUT/$b.long.txt 2>&1 || exit $?
