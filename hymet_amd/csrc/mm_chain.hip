@@ -80,6 +80,26 @@ namespace {
 #ifndef HYMET_CHAIN_MONO
 #define HYMET_CHAIN_MONO 1
 #endif
+// Window-start blocks passed whole are skipped by their last x (an LDS ring) instead of loaded.
+#ifndef HYMET_CHAIN_BLX
+#define HYMET_CHAIN_BLX 1
+#endif
+// A batch starts at any anchor whose window best B lies in its range (not only after B = i-1).
+#ifndef HYMET_CHAIN_B0ANY
+#define HYMET_CHAIN_B0ANY 1
+#endif
+// First back-off step of the batch attempts after a failed or short batch.
+#ifndef HYMET_CHAIN_SPEC_GAP0
+#define HYMET_CHAIN_SPEC_GAP0 2
+#endif
+// Inner-window entries leaving as a prefix of the (y, idx) list are popped, not compacted.
+#ifndef HYMET_CHAIN_IPOP
+#define HYMET_CHAIN_IPOP 1
+#endif
+// Colinear batches skip the prefix min of priorities and the prefix max of f + span.
+#ifndef HYMET_CHAIN_BMONO
+#define HYMET_CHAIN_BMONO 1
+#endif
 // Batch f / p global stores issued at the end of the commit instead of its start.
 #ifndef HYMET_CHAIN_LATE_FP
 #define HYMET_CHAIN_LATE_FP 1
@@ -89,6 +109,17 @@ namespace {
 #ifndef HYMET_CHAIN_HCPF
 #define HYMET_CHAIN_HCPF 0
 #endif
+// Lean head cache: when the window start enters a block beyond the ring, load only its x (the
+// window-start probes) and the block's suffix records (kept with its summary), not every
+// entry's (x, y, f, p); entries are fetched in full only when a y-bounded scan needs them.
+#ifndef HYMET_CHAIN_HLEAN
+#define HYMET_CHAIN_HLEAN 0
+#endif
+// Entries fetched from HBM (head cache, window scans, the winner) without p: only the inner
+// walk reads an entry's predecessor, and it fetches through the ring or HBM (fetch_p)
+#ifndef HYMET_CHAIN_HNOP
+#define HYMET_CHAIN_HNOP 1
+#endif
 #ifndef HYMET_CHAIN_WPE  // waves per SIMD the register allocation targets (0: compiler's choice)
 #define HYMET_CHAIN_WPE 4
 #endif
@@ -96,6 +127,10 @@ constexpr int kRing = HYMET_CHAIN_RING;  // LDS ring of recent anchors, int4 eac
 constexpr int kRingMask = kRing - 1;
 constexpr int kStair = 4;       // staircase entries kept per block summary
 constexpr int kSumInts = kStair + 1;  // int4 words per block summary: staircase + (ymin, ymax, n|trunc, -)
+// HBM summaries add the block's last kSufRec suffix records: the lanes better than every later
+// lane (the argmins of the suffixes [k, 64)), lane 63 first, as ring entries (x, y, f, pw)
+constexpr int kSufRec = HYMET_CHAIN_HLEAN ? 4 : 0;
+constexpr int kGSumInts = kSumInts + kSufRec;
 constexpr int kSumRing = HYMET_CHAIN_SUMRING;  // LDS ring of the last complete block summaries (1.25 KB)
 #ifndef HYMET_CHAIN_INNER
 #define HYMET_CHAIN_INNER 256
@@ -104,9 +139,12 @@ constexpr int kInnerCap = HYMET_CHAIN_INNER;  // LDS inner-window list (ring-deq
 constexpr int kXRing = 256;  // LDS ring of the last 256 anchors' x (1 KB): the window-start probes
 constexpr int kBdq = HYMET_CHAIN_BDQ;  // block-argmin deque, 2 int4 per element (1 KB)
 constexpr int kIdq = HYMET_CHAIN_IDQ;  // inner max-deque (idx, f + span) (0.5 KB)
+constexpr int kBlx = 64;  // LDS ring of the last 64 complete blocks' last x (0.25 KB)
 constexpr size_t kChainLds = kRing * sizeof(int4) + kSumRing * kSumInts * sizeof(int4) + 64 * 2 * sizeof(int4) +
-                             kInnerCap * sizeof(int2) + kXRing * sizeof(int32_t) + kBdq * 2 * sizeof(int4) + kIdq * sizeof(int2);
+                             kInnerCap * sizeof(int2) + kXRing * sizeof(int32_t) + kBdq * 2 * sizeof(int4) + kIdq * sizeof(int2) +
+                             (HYMET_CHAIN_BLX ? kBlx * sizeof(int32_t) : 0);
 constexpr int kNegInf = -(1 << 29);
+constexpr int kSpecGap0 = HYMET_CHAIN_SPEC_GAP0;
 
 // ISA section markers (static instruction counts by section: build with -DHYMET_CHAIN_MARKS -S)
 #ifdef HYMET_CHAIN_MARKS
@@ -167,7 +205,7 @@ struct ChainParams {
     int32_t *f;
     int64_t *p;
     int32_t *t_global;        // overflow path only
-    int4 *sum;                // block summaries of every group (group g at ((g_start[g] >> 6) + g) * kSumInts)
+    int4 *sum;                // block summaries of every group (group g at ((g_start[g] >> 6) + g) * kGSumInts)
     int max_dist, max_dist_inner, bw, max_chn_skip, cap_rmq_size;
     float pen_gap, pen_skip;
     const int32_t *work_end;  // device: the wave kernel takes work items [0, *work_end) (null: n_work)
@@ -429,6 +467,8 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
     int2 *idq = reinterpret_cast<int2 *>(sp);  // (idx, f + span)
     sp += kIdq * sizeof(int2);
     int32_t *xring = reinterpret_cast<int32_t *>(sp);  // x of anchor j at [j & (kXRing - 1)]
+    sp += kXRing * sizeof(int32_t);
+    int32_t *blx = reinterpret_cast<int32_t *>(sp);  // x of block b's last anchor at [b & (kBlx - 1)]
     const double c = 0.5 * (double)P.pen_gap;
     const int32_t n_work = P.work_end ? min(P.n_work, *P.work_end) : P.n_work;
     for (;;) {
@@ -441,9 +481,11 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         const int64_t g0 = P.g_start[g];
         const int32_t n = (int32_t)(P.g_start[g + 1] - g0);
         const bool qfirst = P.g_qfirst[g] != 0;
-        int4 *gsum = P.sum + ((g0 >> 6) + g) * kSumInts;
+        int4 *gsum = P.sum + ((g0 >> 6) + g) * kGSumInts;
         int32_t hb = -1;        // block held by the head cache
         bool hsuf_ok = false;   // hsuf holds the suffix argmins of block hb
+        uint64_t hmask = ~0ull;  // lanes of block hb whose full entry is in hc (x always is)
+        int32_t hlow = 0;        // hsuf is valid for the suffixes [k, 64), k >= hlow
         int32_t i = 0;
         CPROF_DECL
         // anchor jl (local) as seen at iteration i: ring [i - kRing, i), head cache, else HBM
@@ -452,10 +494,30 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             int4 v;
             if (i - jl <= kRing) {
                 v = ring[jl & kRingMask];
-            } else if ((jl >> 6) == hb) {
+            } else if ((jl >> 6) == hb && (hmask >> (jl & 63) & 1)) {
                 v = hc[jl & 63];
             } else {
                 CCOUNT(0);
+                const uint64_t x = P.ax[g0 + jl], y = P.ay[g0 + jl];
+#if HYMET_CHAIN_HNOP
+                v = make_int4((int32_t)x, (int32_t)y, ld_l2(P.f + g0 + jl), (int32_t)((uint32_t)(y >> 32 & 0xff) << 24));
+#else
+                const int64_t pp = ld_l2(P.p + g0 + jl);
+                v = make_int4((int32_t)x, (int32_t)y, ld_l2(P.f + g0 + jl),
+                              (int32_t)((pp < 0 ? 0u : (uint32_t)(pp - g0 + 1)) | (uint32_t)(y >> 32 & 0xff) << 24));
+#endif
+            }
+            e.x = v.x, e.y = v.y, e.f = v.z, e.pw = v.w;
+            return e;
+        };
+        // the same with p (the inner walk): the ring, else HBM -- head-cache entries carry no p
+        auto fetch_p = [&](int32_t jl) -> Ent {
+#if HYMET_CHAIN_HNOP
+            Ent e;
+            int4 v;
+            if (i - jl <= kRing) {
+                v = ring[jl & kRingMask];
+            } else {
                 const uint64_t x = P.ax[g0 + jl], y = P.ay[g0 + jl];
                 const int64_t pp = ld_l2(P.p + g0 + jl);
                 v = make_int4((int32_t)x, (int32_t)y, ld_l2(P.f + g0 + jl),
@@ -463,6 +525,9 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             }
             e.x = v.x, e.y = v.y, e.f = v.z, e.pw = v.w;
             return e;
+#else
+            return fetch(jl);
+#endif
         };
         // x of anchor jl (local) at iteration i, for the window-start probes: the x ring (last
         // kXRing anchors), the head cache, else a plain load of ax
@@ -473,7 +538,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         };
         auto fetch_y = [&](int32_t jl) -> int32_t {
             if (i - jl <= kRing) return ring[jl & kRingMask].y;
-            if ((jl >> 6) == hb) return hc[jl & 63].y;
+            if ((jl >> 6) == hb && (hmask >> (jl & 63) & 1)) return hc[jl & 63].y;
             return (int32_t)P.ay[g0 + jl];
         };
         int32_t i0 = 0, st = 0, st_in = 0;
@@ -504,7 +569,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
 #endif
         auto sum_at = [&](int32_t b, int k) -> int4 {  // word k of block b's summary
             if ((i0 >> 6) - b <= kSumRing) return ssum[(b & (kSumRing - 1)) * kSumInts + k];
-            return ld_l2(gsum + (int64_t)b * kSumInts + k);
+            return ld_l2(gsum + (int64_t)b * kGSumInts + k);
         };
         // best (priority, index) over window entries [st, i0) with ylo < y < yq (quirk: y == yq
         // allowed for the query's anchor 0): per complete block the first staircase entry below
@@ -523,6 +588,15 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     }
                 }
             };
+#if HYMET_CHAIN_HLEAN
+            if (st < (fb << 6) && (st >> 6) == hb && hmask != ~0ull) {  // lean head cache: load it in full
+                const Ent e = fetch((hb << 6) + lane);
+                __builtin_amdgcn_wave_barrier();
+                hc[lane] = make_int4(e.x, e.y, e.f, e.pw);
+                __builtin_amdgcn_wave_barrier();
+                hmask = ~0ull;
+            }
+#endif
             if (st < (fb << 6)) scan(st, min(fb << 6, i0));             // head
             if (fe >= fb && (fe << 6) < i0) scan(max(fe << 6, st), i0);  // tail
             for (int32_t base = fb; base < fe; base += 64) {
@@ -615,6 +689,13 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             const int32_t ynx = down1(e.y);
             if (__ballot(lane == 63 || e.y < ynx) == ~0ull) {
 #if HYMET_CHAIN_CBFAST
+#if HYMET_CHAIN_BMONO
+                // priorities non-increasing along the block (a colinear chain): every lane is
+                // its prefix's best, no scan needed
+                const double plp = __hiloint2double(shr1(__double2hiint(pl), __double2hiint(pl)), shr1(__double2loint(pl), __double2loint(pl)));
+                if (__ballot(!(plp < pl)) == ~0ull) rec = true;
+                else
+#endif
                 rec = scan_min_d(pl) == pl;
                 recm = __ballot(rec);
                 rank = __popcll(lane == 63 ? 0ull : recm >> (lane + 1));
@@ -652,15 +733,47 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 wave_minmax(ymn, ymx);
             }
             const int nrec = __popcll(recm);
-            const int4 meta = make_int4(ymn, ymx, min(nrec, kStair) | (nrec > kStair ? 256 : 0), 0);
+            int32_t mw = 0;
+#if HYMET_CHAIN_HLEAN
+            // suffix records: lane l is one iff it beats every lane > l (ties -> larger index);
+            // priorities non-increasing along the block leave lane 63 alone.  meta.w: lanes of
+            // slots 1..3 (6 bits each), the slot count (bits 18..20) and the lowest lane whose
+            // suffix the kept slots cover (bits 21..26)
+            uint64_t srm = 1ull << 63;
+            if (__ballot(lane == 63 || !(pl < down1d(pl))) != ~0ull) {
+                double sp_ = pl;
+                int32_t sj = jl, sy = e.y;
+                suffix_argmin(sp_, sj, sy);
+                srm = __ballot(sj == jl);
+            }
+            const int sslot = __popcll(lane == 63 ? 0ull : srm >> (lane + 1));  // records above this lane
+            {
+                uint64_t m = srm & ~(1ull << 63);
+                int ns = 1;
+                for (; m && ns < kSufRec; ++ns) {
+                    const int l = 63 - __clzll((long long)m);
+                    m &= ~(1ull << l);
+                    mw |= l << (6 * (ns - 1));
+                }
+                mw |= ns << 18;
+                if (m) mw |= (64 - __clzll((long long)m)) << 21;
+            }
+#endif
+            const int4 meta = make_int4(ymn, ymx, min(nrec, kStair) | (nrec > kStair ? 256 : 0), mw);
             int4 *ls = ssum + (b & (kSumRing - 1)) * kSumInts;
-            int4 *gs = gsum + (int64_t)b * kSumInts;
+            int4 *gs = gsum + (int64_t)b * kGSumInts;
             __builtin_amdgcn_wave_barrier();
             if (rec && rank < kStair) {
                 ls[rank] = pack_st(pl, jl, e.y);
                 gs[rank] = pack_st(pl, jl, e.y);
             }
+#if HYMET_CHAIN_HLEAN
+            if ((srm >> lane & 1) && sslot < kSufRec) gs[kSumInts + sslot] = make_int4(e.x, e.y, e.f, e.pw);
+#endif
             if (lane == 0) ls[kStair] = meta, gs[kStair] = meta;
+#if HYMET_CHAIN_BLX
+            if (lane == 63) blx[b & (kBlx - 1)] = e.x;
+#endif
             __builtin_amdgcn_wave_barrier();
             if (!bok) return;
             const int l0 = __ffsll((unsigned long long)__ballot(rec && rank == 0)) - 1;
@@ -776,9 +889,13 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             cb = ii & ~63;
             nnx = ldx(cb + 128 + lane), nny = ldy(cb + 128 + lane);
         };
-        int32_t spec_next = 0, spec_gap = 2;  // next batch attempt (back-off after short batches)
+        // next batch attempt: back-off after short batches, doubling from kSpecGap0 (1: a lone
+        // off-chain anchor fails its own batch, and the next anchor -- back on the chain, whose
+        // predecessor B is the anchor before the off-chain one -- starts one right away)
+        int32_t spec_next = 0, spec_gap = kSpecGap0;
         for (; i < n;) {
             GCNT(x, 1);
+            CCOUNT(23);
             CPROF(7);
             advance(i);
             const int32_t xi = rl(cx, i & 63);
@@ -794,8 +911,74 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             CPROF(0);
             // ---- 2. outer window start: lane-parallel probe, one block at a time
             AMARK(st_begin);
+#ifdef HYMET_CHAIN_PROF
+            bool hchg = false;  // a head change earlier in this iteration
+#endif
+            // cache st's block in hc when it sits beyond the ring
+            auto head_take = [&]() {
+                if (st < i && (st >> 6) < (i0 >> 6) && i - st > kRing && (st >> 6) != hb) {
+                    const int32_t hb2 = st >> 6;
+#ifdef HYMET_CHAIN_PROF
+                    CCOUNT(20);
+                    if (hchg) CCOUNT(21);
+                    hchg = true;
+#endif
+#if HYMET_CHAIN_HLEAN
+                    // x of every entry and the block's suffix records (lanes 1..4: slots 0..3,
+                    // lane 0: the summary's meta word); the suffix argmins come from the records
+                    const int32_t xl = ldx((hb2 << 6) + lane);
+                    const int4 *gw = gsum + (int64_t)hb2 * kGSumInts + kStair;
+                    const int4 w = ld_l2(gw + min(lane, kSufRec));
+                    const uint32_t mw = (uint32_t)rl(w.w, 0);
+                    {
+                        const int nr = mw >> 18 & 7;
+                        int4 rv = make_int4(rl(w.x, 1), rl(w.y, 1), rl(w.z, 1), rl(w.w, 1));
+                        int32_t rlane = 63;
+                        uint64_t msk = 1ull << 63;
+#pragma unroll
+                        for (int s = 1; s < kSufRec; ++s) {
+                            if (nr > s) {
+                                const int ls = mw >> (6 * (s - 1)) & 63;
+                                msk |= 1ull << ls;
+                                if (ls >= lane) rv = make_int4(rl(w.x, 1 + s), rl(w.y, 1 + s), rl(w.z, 1 + s), rl(w.w, 1 + s)), rlane = ls;
+                            }
+                        }
+                        const double rp = prio(rv.z, rv.x, rv.y, c);
+                        __builtin_amdgcn_wave_barrier();
+                        hc[lane] = rlane == lane ? rv : make_int4(xl, 0, 0, 0);
+                        hsuf[lane] = pack_st(rp, (hb2 << 6) + rlane, rv.y);
+                        __builtin_amdgcn_wave_barrier();
+                        hb = hb2;
+                        hmask = msk;
+                        hlow = mw >> 21 & 63;  // hsuf holds the suffixes from lane hlow on
+                        hsuf_ok = true;
+                        return;
+                    }
+#endif
+                    const Ent e = hc_take(hb2);
+                    __builtin_amdgcn_wave_barrier();
+                    hc[lane] = make_int4(e.x, e.y, e.f, e.pw);
+                    __builtin_amdgcn_wave_barrier();
+                    hb = hb2;
+                    hmask = ~0ull;
+                    hlow = 0;
+                    hsuf_ok = false;
+                }
+            };
             for (;;) {
                 if (st >= i) break;
+#if HYMET_CHAIN_BLX
+                // complete blocks the window start passes whole (their last anchor does, and x
+                // never decreases) are skipped by that anchor's x, without loading them; only
+                // the block the start stops in is cached
+                while ((st & 63) == 0 && (st >> 6) < (i0 >> 6) && (i0 >> 6) - (st >> 6) <= kBlx) {
+                    const int32_t xl = blx[(st >> 6) & (kBlx - 1)];
+                    if (!((int64_t)(uint32_t)xi > (int64_t)(uint32_t)xl + P.max_dist || i0 - (st | 63) > P.cap_rmq_size)) break;
+                    st += 64;
+                }
+                if (st >= i) break;
+                head_take();
+#endif
                 const int32_t bend = min(i, ((st >> 6) + 1) << 6);
                 const int32_t j = st + lane;
                 bool adv = false;
@@ -804,16 +987,9 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 const int t = ~m ? __ffsll((unsigned long long)~m) - 1 : 64;  // lanes [0, t) advance
                 st += min(t, bend - st);
                 if (st < bend) break;
-                // st entered a new block: cache it if it sits beyond the ring
-                if (st < i && (st >> 6) < (i0 >> 6) && i - st > kRing && (st >> 6) != hb) {
-                    const int32_t hb2 = st >> 6;
-                    const Ent e = hc_take(hb2);
-                    __builtin_amdgcn_wave_barrier();
-                    hc[lane] = make_int4(e.x, e.y, e.f, e.pw);
-                    __builtin_amdgcn_wave_barrier();
-                    hb = hb2;
-                    hsuf_ok = false;
-                }
+#if !HYMET_CHAIN_BLX
+                head_take();
+#endif
             }
             const int32_t fb = (st + 63) >> 6, fe = i0 >> 6;  // complete window blocks [fb, fe)
             while (bt > bh && (bf_j >> 6) < fb) {
@@ -824,7 +1000,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     bf_e = bdq[(bh & (kBdq - 1)) * 2 + 1];
                 }
             }
-            if ((st & 63) && (st >> 6) < fe && ((st >> 6) != hb || !hsuf_ok)) {
+            if ((st & 63) && (st >> 6) < fe && ((st >> 6) != hb || !hsuf_ok || (st & 63) < hlow)) {
                 // partial head block: cache it with its suffix argmins [lane, 64)
                 CCOUNT(5);
                 const int32_t b = st >> 6, j = (b << 6) + lane;
@@ -844,6 +1020,8 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 hsuf[lane] = pack_st(pr, pj, py);
                 __builtin_amdgcn_wave_barrier();
                 hb = b;
+                hmask = ~0ull;
+                hlow = 0;
                 hsuf_ok = true;
             }
             CPROF(1);
@@ -860,6 +1038,26 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     if (t > 1 && !overflow && ni > 0) {
                         // several entries leave: stable compaction of the list keeps j >= st_in + t
                         const int32_t lim = st_in + t;
+#if HYMET_CHAIN_IPOP
+                        // the list holds exactly the entries [st_in, i0), so when its first nl
+                        // entries all leave they are the nl leaving ones (colinear: lowest y and
+                        // index together) and are popped from the front
+                        const int nl = max(0, min(lim, i0) - st_in);
+                        if (nl <= ni) {
+                            const int2 v = L(min(lane, ni - 1));
+                            if (__ballot(lane < nl && v.y >= lim) == 0ull) {
+                                lh = (lh + nl) & (kInnerCap - 1);
+                                ni -= nl;
+                                if (ni > 0) {
+                                    const int2 a = L(0);
+                                    lfy = a.x, lfj = a.y;
+                                }
+                                st_in += t;
+                                if (t < 64) break;
+                                continue;
+                            }
+                        }
+#endif
                         int kept = 0;
                         for (int base = 0; base < ni; base += 64) {
                             const int kk = base + lane;
@@ -989,7 +1187,16 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 GCNT(y, 1);
                 if (b0j != i - 1) CCOUNT(10);
                 if (!walk_ok) CCOUNT(11);
+#if HYMET_CHAIN_B0ANY
+                // the batch's first anchor takes B as its predecessor (B is the best entry of its
+                // krmq range whenever it lies in that range: checked with the others below), so a
+                // batch also starts right after an anchor that chained elsewhere
+                if (b0j >= 0 && walk_ok && Lb >= 2) {
+                    const Ent e0 = b0j == i - 1 ? prev : fetch(b0j);
+#else
                 if (b0j == i - 1 && walk_ok && Lb >= 2) {
+                    const Ent e0 = prev;
+#endif
                     AMARK(batch_begin);
                     // anchors k = i + lane from the chunk registers (cx: [cb, cb+64), nx: next 64)
                     const int off = (i - cb) + lane;
@@ -999,7 +1206,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     const int32_t kx = off < 64 ? kx_lo : kx_hi;
                     const uint64_t kyy = off < 64 ? ky_lo : ky_hi;
                     const int32_t ky = (int32_t)kyy, ksp = (int32_t)(kyy >> 32 & 0xff);
-                    const int32_t px = shr1(kx, prev.x), py = shr1(ky, prev.y), psp = shr1(ksp, prev.sp());
+                    const int32_t px = shr1(kx, e0.x), py = shr1(ky, e0.y), psp = shr1(ksp, e0.sp());
                     int32_t ex = 1, wd = 0;
                     const int32_t s = comput_sc(kx, ky, px, py, psp, P.pen_gap, P.pen_skip, &ex, &wd);
                     // ky <= batch_y: B covers y <= Y, Y = the y of the batch's LAST anchor, which is a
@@ -1010,18 +1217,31 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     // f_k = max(span_k, f_{k-1} + s_k): maps f -> max(f + a, b), composed by scan
                     int a = s, bb = ksp;
                     scan_maxplus(a, bb);
-                    const int32_t fk = max(prev.f + a, bb);
-                    const int32_t fp = shr1(fk, prev.f);
-                    const bool linked = fp + s > ksp;  // sc > max_f = span: predecessor k-1
+                    const int32_t fk = max(e0.f + a, bb);
+                    const int32_t fp = shr1(fk, e0.f);
+                    const bool linked = fp + s > ksp;  // sc > max_f = span: predecessor k-1 (lane 0: B)
                     // priorities of batch entries; the candidate of lane l is entry l-1
                     const double pk = prio(fk, kx, ky, c);
+                    const int vk = inb ? fk + ksp : INT32_MIN;
+#if HYMET_CHAIN_BMONO
+                    // a colinear batch: priorities fall and f + span rises along it, so each
+                    // prefix min / max is the lane's own value and the two scans are skipped
+                    // (lanes past the batch only feed lanes that fail `inb`)
+                    const double pkp = __hiloint2double(shr1(__double2hiint(pk), __double2hiint(pk)), shr1(__double2loint(pk), __double2loint(pk)));
+                    const bool bmono = __ballot(!inb || (!(pkp < pk) && vk >= shr1(vk, vk))) == ~0ull;
+                    double ipm = pk;
+                    int vmx = vk;
+                    if (!bmono) ipm = scan_min_d(inb ? pk : 1e300), vmx = scan_max(vk);
+                    const int vex = shr1(vmx, INT32_MIN);  // max over the entries before k
+#else
                     const double ipm = scan_min_d(inb ? pk : 1e300);
+                    const int vex = shr1(scan_max(vk), INT32_MIN);  // max over the entries before k
+#endif
                     const bool best_here = pk == ipm && !(b0p < pk);  // beats B0 and earlier entries
                     // (cross-lane operations run with every lane active: DPP reads of an
                     // inactive lane return the fallback value)
                     const bool cand_ok = shr1(best_here ? 1 : 0, 1) != 0;
                     // inner walk: max(f_j + span_j) over the inner window must not exceed f_k
-                    const int vex = shr1(scan_max(inb ? fk + ksp : INT32_MIN), INT32_MIN);  // entries before k
                     bool wok = true;
                     if (P.max_dist_inner > 0 && !ex && ky > 0) wok = max(vex, it > ih ? if_v : INT32_MIN) <= fk;
                     // inner-list keys (y, idx) of entries i.. strictly increase (py < ky); they must
@@ -1073,7 +1293,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         spec_next = i + spec_gap;
                         spec_gap = min(spec_gap * 2, 64);
                     } else {
-                        spec_gap = 2;
+                        spec_gap = kSpecGap0;
                     }
                     AMARK(batch_verified);
                     if (acc > 0) {
@@ -1082,7 +1302,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         advance(i + acc);
                         // commit anchors [i, i + acc): f, p, ring; insert entries [i, i + acc - 1)
                         const int32_t k = i + lane;
-                        const int32_t pk_local = linked ? k - 1 : -1;
+                        const int32_t pk_local = linked ? (lane == 0 ? b0j : k - 1) : -1;
                         const int32_t pw = (int32_t)((uint32_t)(pk_local + 1) | (uint32_t)ksp << 24);
                         if (lane < acc) {
 #if !HYMET_CHAIN_LATE_FP
@@ -1253,7 +1473,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                             if (e >= 0) {
                                 const int2 v = L(e);
                                 yj = v.x, jl = v.y;
-                                const Ent ej = fetch(jl);
+                                const Ent ej = fetch_p(jl);
                                 int32_t ex;
                                 sc_l = ej.f + comput_sc(xi, yi, ej.x, ej.y, ej.sp(), P.pen_gap, P.pen_skip, &ex, &w_l);
                                 pj = ej.p();
@@ -1313,7 +1533,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                             first = false;
                             cy_ = by, cj = bjl;
                             if (by < ylo_in) break;
-                            const Ent ej = fetch(bjl);
+                            const Ent ej = fetch_p(bjl);
                             int32_t ex, wl;
                             const int32_t sl = ej.f + comput_sc(xi, yi, ej.x, ej.y, ej.sp(), P.pen_gap, P.pen_skip, &ex, &wl);
                             if (wl <= P.bw) {
@@ -1406,7 +1626,12 @@ constexpr int kBtChunks = HYMET_BT_CHUNKS;
 #ifndef HYMET_BT_PROBE
 #define HYMET_BT_PROBE 4
 #endif
-constexpr int kBtProbe = HYMET_BT_PROBE;  // z probe block: kBtProbe * 64 entries
+constexpr int kBtProbe = HYMET_BT_PROBE;
+// Starts whose predecessor is already used are settled from the probe's prefetched t / f of
+// that predecessor, without a walk (no window load, no mark re-read).
+#ifndef HYMET_BT_TRIV
+#define HYMET_BT_TRIV 1
+#endif  // z probe block: kBtProbe * 64 entries
 
 __device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int64_t uni64(int64_t v) {
@@ -1467,6 +1692,9 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
         int64_t ptop = -1;  // the block covers z positions (ptop - 64 * kBtProbe, ptop]
         int32_t zc[kBtProbe], tv[kBtProbe], zfv[kBtProbe];
         int64_t zpv[kBtProbe];  // f and p of the entries that read unmarked: a walk's start
+#if HYMET_BT_TRIV
+        int32_t tqv[kBtProbe], fqv[kBtProbe];  // t and f of their predecessors (t as read at the probe)
+#endif
         bool stale = false;
         while (k >= z0) {
             if (ptop < 0 || k <= ptop - 64 * kBtProbe) {
@@ -1488,6 +1716,14 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                     zfv[c] = tv[c] == 0 ? P.f[zc[c]] : 0;
                     zpv[c] = tv[c] == 0 ? P.p[zc[c]] : -1;
                 }
+#if HYMET_BT_TRIV
+#pragma unroll
+                for (int c = 0; c < kBtProbe; c++) {
+                    const bool q = tv[c] == 0 && zpv[c] >= 0;
+                    tqv[c] = q ? ld_l2(P.t + zpv[c]) : 0;
+                    fqv[c] = q ? P.f[zpv[c]] : 0;
+                }
+#endif
             } else if (stale) {  // a walk since the probe: re-read the marks (z indices stay valid)
                 stale = false;
 #pragma unroll
@@ -1500,6 +1736,9 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             int hit = -1;
             int32_t zsel = 0, zfsel = 0;
             int64_t zpsel = -1;
+#if HYMET_BT_TRIV
+            int32_t tqsel = 0, fqsel = 0;
+#endif
 #pragma unroll
             for (int c = kBtProbe - 1; c >= 0; c--) {  // the nearest unmarked entry at or below k wins
                 const uint64_t m = __ballot(tv[c] == 0 && 64 * c + lane >= d);
@@ -1509,6 +1748,10 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                     zsel = __builtin_amdgcn_readlane(zc[c], h);
                     zfsel = __builtin_amdgcn_readlane(zfv[c], h);
                     zpsel = rlane64(zpv[c], h);
+#if HYMET_BT_TRIV
+                    tqsel = __builtin_amdgcn_readlane(tqv[c], h);
+                    fqsel = __builtin_amdgcn_readlane(fqv[c], h);
+#endif
                 }
             }
             hit = uni(hit);
@@ -1518,8 +1761,19 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             }
             const int64_t zi = (int64_t)uni(zsel);
             k = ptop - hit - 1;
-            stale = true;
             const int32_t zf = uni(zfsel);
+#if HYMET_BT_TRIV
+            // a start whose predecessor was already used (or that has none) walks one node: its
+            // score z.x - f[p] (or z.x) decides whether it stays used, and a one-anchor path is
+            // never a chain (min_cnt >= 2).  No other mark changes, so the block stays fresh.
+            if (P.min_cnt >= 2 && (zpsel < 0 || uni(tqsel) != 0)) {
+                const int32_t sv = zpsel < 0 ? zf : zf - uni(fqsel);
+                if (sv > 0) P.t[zi] = 1;  // every lane: same value, same address
+                c_walk++;
+                continue;
+            }
+#endif
+            stale = true;
             int64_t *buf = P.chain_ids + wpos;
             buf[0] = zi;  // every lane: same value, same address
             P.t[zi] = 2;  // path nodes are marked as recorded; those past the best end are unmarked after
@@ -1855,7 +2109,7 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
     if (n_work <= 0) return HYMET_OK;
     DevBuf cnt, sum, split;
     const size_t n_sum = (size_t)(n_anchors >> 6) + (size_t)n_groups + 2;
-    HY_HIP(sum.alloc(16 * kSumInts * n_sum, ctx->stream));
+    HY_HIP(sum.alloc(16 * kGSumInts * n_sum, ctx->stream));
     HY_HIP(cnt.alloc(4, ctx->stream));
     HY_HIP(split.alloc(4, ctx->stream));
     if (max_dist < bw) max_dist = bw;

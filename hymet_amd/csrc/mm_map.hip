@@ -542,8 +542,10 @@ __global__ __launch_bounds__(256) void group_count_kernel(const uint64_t *x, int
 
 // also: t[i] = 0 for every anchor (the backtrack's initial marks; the chaining kernels'
 // overflow path stamps iterations as i + 1) and the g_start[G] = n sentinel
+// (g_start and each group's query-first flag -- lchain.c's krmq index-0 quirk -- at its head;
+// t zeroed for the chaining and backtrack kernels)
 __global__ __launch_bounds__(256) void group_write_kernel(const uint64_t *x, int64_t n, const int64_t *qoff, int n_q,
-                                                          const int64_t *tile_off, int64_t *g_start, int32_t *gid,
+                                                          const int64_t *tile_off, int64_t *g_start, uint8_t *qfirst,
                                                           int32_t *t, int64_t G) {
     __shared__ uint32_t qs[kGTile / 32], rc[64];
     bool h[16];
@@ -567,9 +569,12 @@ __global__ __launch_bounds__(256) void group_write_kernel(const uint64_t *x, int
         const uint64_t b = __ballot(h[j]);
         const int64_t g = base + rc[j * 4 + w] + __popcll(b & ((2ull << lane) - 1)) - 1;  // inclusive - 1
         if (i < n) {
-            gid[i] = (int32_t)g;
             t[i] = 0;
-            if (h[j]) g_start[g] = i;
+            if (h[j]) {
+                const int64_t l = i - t0;
+                g_start[g] = i;
+                qfirst[g] = (uint8_t)(qs[l >> 5] >> (l & 31) & 1);
+            }
         }
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) g_start[G] = n;
@@ -581,12 +586,6 @@ __global__ void group_start_kernel(const uint32_t *flag, const int64_t *gpos, in
     const int64_t g = gpos[i] + flag[i] - 1;
     gid[i] = (int32_t)g;
     if (flag[i]) g_start[g] = i;
-}
-
-// groups that start their query's anchor array (lchain.c's krmq index-0 quirk is per query)
-__global__ void group_qfirst_kernel(const int64_t *qoff, int n_q, const int32_t *gid, uint8_t *out) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < n_q && qoff[q] < qoff[q + 1]) out[gid[qoff[q]]] = 1;
 }
 
 // largest group: the first of the size-descending list, or, when sizes tie at the 16-bit
@@ -618,7 +617,7 @@ __global__ void group_size_kernel(const int64_t *g_start, int32_t G, int min_cnt
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g < 8) zlists[g] = 0;
     if (g >= G) return;
-    qfirst[g] = 0;
+    if (qfirst) qfirst[g] = 0;
     const int64_t sz = g_start[g + 1] - g_start[g];
     // descending size in 16 bits (two radix passes): groups above 65535 anchors tie at the
     // front, non-work groups (< min_cnt <= 3 anchors) come after every work group
@@ -1152,10 +1151,13 @@ struct AnchorSet {
 // Chains of an anchor set: compacted anchors (chain by chain, chains ordered by first
 // anchor) + chain scores/counts + per-query chain offsets.
 struct ChainSet {
-    DevBuf bx, by, cu, cboff;  // cboff: offset of each chain's anchors in bx/by
-    DevBuf bchain, cq;         // chain of each compacted anchor; query of each chain
+    DevBuf cu, cboff;          // per chain: score<<32 | count; offset of its anchors in chain order
+    DevBuf ids, cfirst;        // backtrack output (each chain end -> start) and each chain's first slot
+    const uint64_t *ax = nullptr, *ay = nullptr;  // the chained anchor set (alive as long as the chains)
+    DevBuf bx, by, bchain;     // a copy of the chained anchors in chain order (only for re-chain paths)
+    DevBuf cq;                 // query of each chain
     int64_t n_anchor = 0, n_chain = 0;
-    DevBuf d_qc, d_qb;  // n_q + 1 chain / compacted-anchor offsets per query
+    DevBuf d_qc, d_qb;  // n_q + 1 chain / chain-order anchor offsets per query
 };
 
 // A first pass followed by the long join (map.c's rmq rescue): chain_set flags the re-chained
@@ -1230,8 +1232,9 @@ static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n,
 
 // chaining + backtrack + compact_a over an anchor set
 static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, float pen_skip, int bw, AnchorSet &A,
-                     int n_q, ChainSet &C, LeanJoin *lj = nullptr) {
+                     int n_q, ChainSet &C, LeanJoin *lj = nullptr, bool copy = false) {
     const int64_t n = A.n;
+    C.ax = A.ax.as<uint64_t>(), C.ay = A.ay.as<uint64_t>();
     if (n == 0) {
         HY_HIP(C.d_qc.alloc(8 * (size_t)(n_q + 1), ctx->stream));
         HY_HIP(C.d_qb.alloc(8 * (size_t)(n_q + 1), ctx->stream));
@@ -1240,7 +1243,7 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         return HYMET_OK;
     }
     // groups: (query, strand, target) runs, by tiles (count, scan of the tile counts, write)
-    DevBuf tcnt, toff, gid;
+    DevBuf tcnt, toff;
     const int64_t ntile = cdiv(n, kGTile);
     HY_HIP(tcnt.alloc(4 * (size_t)(ntile + 1), ctx->stream));
     HY_HIP(toff.alloc(8 * (size_t)(ntile + 1), ctx->stream));
@@ -1250,25 +1253,24 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
     int64_t G = 0;
     int rc = exclusive_scan_u32_i64(ctx, tcnt.as<uint32_t>(), toff.as<int64_t>(), ntile, &G);
     if (rc) return rc;
-    DevBuf g_start, t;
+    DevBuf g_start, t, qfirst;
     HY_HIP(g_start.alloc(8 * (size_t)(G + 1), ctx->stream));
-    HY_HIP(gid.alloc(4 * (size_t)n, ctx->stream));
+    HY_HIP(qfirst.alloc((size_t)G, ctx->stream));
     HY_HIP(t.alloc(4 * (size_t)n, ctx->stream));
     hipLaunchKernelGGL(group_write_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.ax.as<uint64_t>(), n,
-                       A.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), g_start.as<int64_t>(), gid.as<int32_t>(),
+                       A.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
                        t.as<int32_t>(), G);
     HY_CHECK_LAUNCH("group_write_kernel");
     // work list: groups with >= min_cnt anchors, biggest first
-    DevBuf skey, sidx, swork, skey2, sidx2, qfirst, zlists;
+    DevBuf skey, sidx, swork, skey2, sidx2, zlists;
     HY_HIP(skey.alloc(4 * (size_t)G, ctx->stream));
     HY_HIP(sidx.alloc(4 * (size_t)G, ctx->stream));
     HY_HIP(swork.alloc(4 * (size_t)G, ctx->stream));
     HY_HIP(skey2.alloc(4 * (size_t)G, ctx->stream));
     HY_HIP(sidx2.alloc(4 * (size_t)G, ctx->stream));
-    HY_HIP(qfirst.alloc((size_t)G, ctx->stream));
     HY_HIP(zlists.alloc(32, ctx->stream));
     LAUNCH1(group_size_kernel, std::max<int64_t>(G, 8), g_start.as<int64_t>(), (int32_t)G, opt->min_cnt, skey.as<uint32_t>(),
-            sidx.as<uint32_t>(), swork.as<uint32_t>(), qfirst.as<uint8_t>(), zlists.as<int32_t>());
+            sidx.as<uint32_t>(), swork.as<uint32_t>(), (uint8_t *)nullptr, zlists.as<int32_t>());
     // drop non-work groups: key of those = 0xffffffff (sorted last), count them on the host
     {
         DevBuf wpos;
@@ -1293,7 +1295,6 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         // the chaining kernels write f/p of every anchor of a work group; the rest (groups of
         // fewer than min_cnt anchors) get f = 0, p = -1 here instead of memsets of all n
         LAUNCH1(nonwork_fp_kernel, G, g_start.as<int64_t>(), (int32_t)G, opt->min_cnt, f.as<int32_t>(), p.as<int64_t>());
-        LAUNCH1(group_qfirst_kernel, n_q, A.d_off.as<int64_t>(), n_q, gid.as<int32_t>(), qfirst.as<uint8_t>());
         rc = launch_chain(ctx, A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
                           (const int32_t *)vp,
                           (int32_t)n_work, f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(), opt->max_gap,
@@ -1498,13 +1499,15 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         rc = scan_flags(ctx, ccnt.as<uint32_t>(), NC, C.cboff, &NB);
         if (rc) return rc;
         C.n_anchor = NB;
-        HY_HIP(C.bx.alloc(8 * (size_t)(NB + 1), ctx->stream));
-        HY_HIP(C.by.alloc(8 * (size_t)(NB + 1), ctx->stream));
-        HY_HIP(C.bchain.alloc(4 * (size_t)(NB + 1), ctx->stream));
-        if (NC > 0 && NB > 0)
-            LAUNCH1(chain_copy_kernel, NB, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), C.cboff.as<int64_t>(),
-                    chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, NB, C.bx.as<uint64_t>(),
-                    C.by.as<uint64_t>(), C.bchain.as<int32_t>());
+        if (copy) {  // the re-sort / two-key long-join paths read the chained anchors as a copy
+            HY_HIP(C.bx.alloc(8 * (size_t)(NB + 1), ctx->stream));
+            HY_HIP(C.by.alloc(8 * (size_t)(NB + 1), ctx->stream));
+            HY_HIP(C.bchain.alloc(4 * (size_t)(NB + 1), ctx->stream));
+            if (NC > 0 && NB > 0)
+                LAUNCH1(chain_copy_kernel, NB, C.cu.as<uint64_t>(), cf_s.as<int64_t>(), C.cboff.as<int64_t>(),
+                        chain_ids.as<int64_t>(), A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), NC, NB, C.bx.as<uint64_t>(),
+                        C.by.as<uint64_t>(), C.bchain.as<int32_t>());
+        }
         HY_HIP(C.d_qb.alloc(8 * (size_t)(n_q + 1), ctx->stream));
         LAUNCH1(chain_qb_kernel, n_q + 1, C.d_qc.as<int64_t>(), C.cboff.as<int64_t>(), NC, NB, n_q, C.d_qb.as<int64_t>());
         if (qflag) {  // the re-chained queries' chain anchors: per-query counts, and t handed over
@@ -1519,6 +1522,9 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
             LAUNCH1(chain_qb_kernel, n_q + 1, C.d_qc.as<int64_t>(), boff2.as<int64_t>(), NC, NB2, n_q, lj->qb2.as<int64_t>());
             lj->n2 = NB2;
         }
+        // regions and chain statistics read the chains in place
+        C.ids.swap(chain_ids);
+        C.cfirst.swap(cf_s);
     }
     return HYMET_OK;
 }
@@ -1528,11 +1534,12 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
 
 namespace hymet {
 namespace mm {
-int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const uint64_t *cu, const int64_t *cboff,
+int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *ids, const int64_t *cfirst,
+                   const uint64_t *cu, const int64_t *cboff,
                    const int64_t *qc, const int64_t *qb, const uint64_t *mini_pos, const int64_t *mp_off, const int64_t *qlen,
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
-                   int64_t NB, int64_t NC, int64_t NM, const int32_t *bchain, const uint32_t *cq,
+                   int64_t NB, int64_t NC, int64_t NM, const uint32_t *cq,
                    const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q);
 
 namespace {
@@ -1934,18 +1941,18 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     const bool long_join = opt->bw_long > opt->bw;
     const bool resort = getenv("HYMET_RECHAIN_SORT") != nullptr;  // tests: the re-sort path
     LeanJoin lj{d_qlen.as<int64_t>(), opt->rmq_rescue_size, opt->rmq_rescue_ratio, key_path && !resort};
-    rc = chain_set(ctx, opt, pen_gap, pen_skip, opt->bw, S1, n_q, C1, long_join ? &lj : nullptr);
+    rc = chain_set(ctx, opt, pen_gap, pen_skip, opt->bw, S1, n_q, C1, long_join ? &lj : nullptr, long_join && !lj.mark_only);
     if (rc) return rc;
     tr.mark("chain_set 1");
     ChainSet *CF = &C1;
     ChainSet C2;
+    AnchorSet S2;  // the long join's anchors: its chains (C2) are read in place until the regions
     DevBuf flag;  // queries re-chained by the long join (their first-pass regions are not built)
     if (long_join && C1.n_chain > 0) {
         flag.swap(lj.flag);
         // anchors of flagged queries only: their per-query offsets, built on the device (the
         // total and whether any query is flagged come back through the mailbox)
         const DevBuf &qbuf = lj.mark_only ? lj.qb2 : C1.d_qb;
-        AnchorSet S2;
         DevBuf fcnt;
         HY_HIP(fcnt.alloc(4 * (size_t)(n_q + 1), st));
         ctx->mbox_h[kMbFlag] = 0;
@@ -2044,11 +2051,12 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
         HY_HIP(cov.alloc(8 * (size_t)(NC + 1), st));
         HY_HIP(tmp.alloc(4 * (size_t)(NC + 1), st));
         HY_HIP(nr.alloc(4 * (size_t)n_q, st));
-        return launch_regions(ctx, C.bx.as<uint64_t>(), C.by.as<uint64_t>(), C.cu.as<uint64_t>(), C.cboff.as<int64_t>(),
+        return launch_regions(ctx, C.ax, C.ay, C.ids.as<int64_t>(), C.cfirst.as<int64_t>(), C.cu.as<uint64_t>(),
+                              C.cboff.as<int64_t>(),
                               C.d_qc.as<int64_t>(), C.d_qb.as<int64_t>(), mini_pos.as<uint64_t>(), mp_off.as<int64_t>(),
                               d_qlen.as<int64_t>(), d_hash, rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
                               z.p, rg.as<hymet_mm_reg>(), wv.as<int32_t>(), cov.as<uint64_t>(), tmp.as<int32_t>(),
-                              nr.as<int32_t>(), C.n_anchor, NC, NM, C.bchain.as<int32_t>(), C.cq.as<uint32_t>(),
+                              nr.as<int32_t>(), C.n_anchor, NC, NM, C.cq.as<uint32_t>(),
                               pos_tab.as<int32_t>(), d_qbase.as<int64_t>(), skip_q);
     };
     DevBuf rg1, nr1, rg2, nr2;

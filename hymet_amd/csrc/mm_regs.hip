@@ -66,9 +66,10 @@ __device__ __forceinline__ int64_t upper_idx(const int64_t *off, int64_t n, int6
 }
 
 struct RegParams {
-    const uint64_t *bx, *by;       // chained anchors, chain by chain
+    const uint64_t *ax, *ay;       // the chained anchor set
+    const int64_t *ids, *cfirst;   // backtrack output (chains end -> start) and each chain's first slot in it
     const uint64_t *cu;            // score<<32 | count per chain
-    const int64_t *cboff;          // chain -> offset in bx/by
+    const int64_t *cboff;          // chain -> offset of its anchors in chain order (region `as`)
     const int64_t *qc;             // n_q + 1 chain offsets
     const int64_t *qb;             // n_q + 1 anchor offsets
     const uint64_t *mini_pos;
@@ -93,19 +94,20 @@ struct RegParams {
     const uint32_t *skip_q;        // queries whose regions come from the long join (nullable)
 };
 
-__device__ void set_coor(hymet_mm_reg *r, int32_t qlen, const uint64_t *ax, const uint64_t *ay, int32_t mlen,
+// (x0, y0): the chain's first anchor, (x1, y1): its last
+__device__ void set_coor(hymet_mm_reg *r, int32_t qlen, uint64_t x0, uint64_t y0, uint64_t x1, uint64_t y1, int32_t mlen,
                          int32_t blen) {
-    const int32_t k = r->as, q_span = (int32_t)(ay[k] >> 32 & 0xff);
-    r->rev = (int32_t)(ax[k] >> 63);
-    r->rid = (int32_t)(ax[k] << 1 >> 33);
-    r->rs = (int32_t)ax[k] + 1 > q_span ? (int32_t)ax[k] + 1 - q_span : 0;
-    r->re = (int32_t)ax[k + r->cnt - 1] + 1;
+    const int32_t q_span = (int32_t)(y0 >> 32 & 0xff);
+    r->rev = (int32_t)(x0 >> 63);
+    r->rid = (int32_t)(x0 << 1 >> 33);
+    r->rs = (int32_t)x0 + 1 > q_span ? (int32_t)x0 + 1 - q_span : 0;
+    r->re = (int32_t)x1 + 1;
     if (!r->rev) {
-        r->qs = (int32_t)ay[k] + 1 - q_span;
-        r->qe = (int32_t)ay[k + r->cnt - 1] + 1;
+        r->qs = (int32_t)y0 + 1 - q_span;
+        r->qe = (int32_t)y1 + 1;
     } else {
-        r->qs = qlen - ((int32_t)ay[k + r->cnt - 1] + 1);
-        r->qe = qlen - ((int32_t)ay[k] + 1 - q_span);
+        r->qs = qlen - ((int32_t)y1 + 1);
+        r->qe = qlen - ((int32_t)y0 + 1 - q_span);
     }
     r->mlen = mlen;  // span(first) + sum over consecutive anchors (chain_stats_flat_kernel)
     r->blen = blen;
@@ -123,12 +125,12 @@ __device__ __forceinline__ int64_t chain_of(const int64_t *cboff, int64_t c0, in
 }
 
 struct AnchorStatParams {
-    const uint64_t *bx, *by, *cu;
+    const uint64_t *ax, *ay, *cu;
+    const int64_t *ids, *cfirst;  // backtrack output (chains end -> start), each chain's first slot in it
     const int64_t *cboff, *qb, *qlen, *mp_off;
     const uint64_t *mini_pos;
     int64_t NB, NC;
     int n_q;
-    const int32_t *bchain;   // chain of each anchor (chain_copy_kernel)
     const uint32_t *cq;      // query of each chain
     int32_t *c_mlen, *c_blen, *c_st, *c_last;
     const int32_t *pos_tab;  // query base -> minimizer index (or -1), at qbase[q] + position
@@ -136,69 +138,126 @@ struct AnchorStatParams {
     const uint32_t *skip_q;  // queries whose chains are superseded by the long join (nullable)
 };
 
-// Per-chain anchor statistics, flat over the chained anchors (chains are contiguous runs of
-// the copy): mm_reg_set_coor's mlen/blen sums, and for mm_est_err the walk-order first/last
-// minimizer index and the first anchor whose index does not increase (est_err's loop
-// `for (k=1, j=st+1; j<nm && k<cnt; ++j) if (idx(k) == j) ++k, ++n_match;` matches anchor k
-// iff idx(1..k) strictly increase from st; the first that does not, or has no minimizer,
-// stalls it to the end).  The minimizer index (get_mini_idx) is one load from a dense
-// position -> index table (pos_tab, one int32 per query base, -1 where no seeded minimizer
-// starts; built by mini_table_kernel in hymet_mm_map) instead of a binary search.  Every
-// anchor computes its own mm_reg_set_coor terms and est_err stall candidate -- the
-// minimizer index of itself and of its walk-order predecessor by two pos_tab loads, so no
-// a_idx pass -- then a segmented wave reduction by chain id and one atomic per chain piece
-// in the wave.  c_mlen / c_blen start at 0, c_fv at INT32_MAX (every anchor offers cnt).
-// (One wave per chain spent most of its time on the chain's dependent loads: chains are
-// short and many.)
-__device__ __forceinline__ int32_t mini_idx_at(const AnchorStatParams &P, int64_t q, int qlen, int64_t b) {
-    const uint64_t ax = P.bx[b], ay = P.by[b];
+// Per-chain anchor statistics, flat over the chained anchors in chain order (position b of
+// chain c: b - cboff[c] from its start), read in place from the backtrack output and the
+// anchor set -- no copy of the chained anchors is made (a copy cost 48 B per anchor written
+// and read back).  mm_reg_set_coor's mlen/blen sums, and for mm_est_err the walk-order
+// first/last minimizer index and the first anchor whose index does not increase (est_err's
+// loop `for (k=1, j=st+1; j<nm && k<cnt; ++j) if (idx(k) == j) ++k, ++n_match;` matches
+// anchor k iff idx(1..k) strictly increase from st; the first that does not, or has no
+// minimizer, stalls it to the end).  The minimizer index (get_mini_idx) is one load from a
+// dense position -> index table (pos_tab, one int32 per query base, -1 where no seeded
+// minimizer starts; built by mini_table_kernel in hymet_mm_map).  Each block finds its
+// lanes' chains by a search over the next 256 chain offsets staged in LDS; neighbours in
+// chain order come from the adjacent lanes (a load only at a wave edge); then a segmented
+// wave reduction by chain and one atomic per chain piece in the wave.  c_mlen / c_blen
+// start at 0, c_fv at INT32_MAX (every anchor offers cnt).
+__device__ __forceinline__ int32_t mini_idx_at(const AnchorStatParams &P, int64_t q, int qlen, uint64_t ax, uint64_t ay) {
     int32_t x = (int32_t)ay;
     if (ax >> 63) x = qlen - 1 - (int32_t)ay + (int32_t)(ay >> 32 & 0xff) - 1;
     return (x >= 0 && x < qlen) ? P.pos_tab[P.qbase[q] + x] : -1;
 }
 
 __global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams P, int32_t *c_fv) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ int64_t s_c0;
+    __shared__ int32_t s_st[257];  // block-relative starts of chains c0 .. c0 + 256 (clamped)
+    const int64_t b0 = (int64_t)blockIdx.x * blockDim.x;
+    if (threadIdx.x == 0) {
+        int64_t lo = 0, hi = P.NC - 1;  // last c with cboff[c] <= b0
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) >> 1;
+            if (P.cboff[mid] <= b0) lo = mid;
+            else hi = mid - 1;
+        }
+        s_c0 = lo;
+    }
+    __syncthreads();
+    const int64_t cb0 = s_c0;
+    for (int i = threadIdx.x; i < 257; i += blockDim.x) {
+        const int64_t cc = cb0 + i;
+        s_st[i] = cc < P.NC ? (int32_t)min(P.cboff[cc] - b0, (int64_t)256) : 256;
+    }
+    __syncthreads();
+    const int64_t b = b0 + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const bool in = b < P.NB;
-    const int32_t c = in ? P.bchain[b] : -1;
+    int64_t c = -1;
+    if (in) {
+        int lo = 0, hi = 256;  // last i with s_st[i] <= threadIdx.x (s_st[0] <= 0, nondecreasing)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_st[mid] <= (int)threadIdx.x) lo = mid;
+            else hi = mid - 1;
+        }
+        c = cb0 + lo;
+        if (lo == 256) {  // beyond the staged chains (chains with no anchors in the range)
+            int64_t l2 = c, h2 = P.NC - 1;
+            while (l2 < h2) {
+                const int64_t mid = (l2 + h2 + 1) >> 1;
+                if (P.cboff[mid] <= b) l2 = mid;
+                else h2 = mid - 1;
+            }
+            c = l2;
+        }
+    }
     const int64_t q = in ? (int64_t)P.cq[c] : 0;
     const bool act = in && !(P.skip_q && P.skip_q[q]);
+    int32_t cnt = 0, j = 0;
+    int64_t f0 = 0;  // slot of chain-order position 0 in ids
+    uint64_t x = 0, y = 0;
+    if (act) {
+        cnt = (int32_t)P.cu[c];
+        j = (int32_t)(b - P.cboff[c]);
+        f0 = P.cfirst[c] + cnt - 1;
+        const int64_t a = P.ids[f0 - j];
+        x = P.ax[a], y = P.ay[a];
+    }
+    // chain-order neighbours from the adjacent lanes (same chain), else loaded
+    const int32_t ci = (int32_t)c;
+    const int32_t cprev = __shfl_up(ci, 1, 64), cnext = __shfl_down(ci, 1, 64);
+    uint64_t xp = __shfl_up(x, 1, 64), yp = __shfl_up(y, 1, 64);
+    uint64_t xn = __shfl_down(x, 1, 64), yn = __shfl_down(y, 1, 64);
     int dm = 0, db = 0, fv = INT32_MAX;
     if (act) {
-        const int64_t o = P.cboff[c];
-        const int32_t cnt = (int32_t)P.cu[c], j = (int32_t)(b - o);
-        const int qlen = (int)P.qlen[q];
-        const uint64_t x = P.bx[b], y = P.by[b];
         const bool rev = x >> 63;
+        if (j > 0 && (lane == 0 || cprev != ci)) {
+            const int64_t a = P.ids[f0 - j + 1];
+            xp = P.ax[a], yp = P.ay[a];
+        }
+        if (rev && j + 1 < cnt && (lane == 63 || cnext != ci)) {
+            const int64_t a = P.ids[f0 - j - 1];
+            xn = P.ax[a], yn = P.ay[a];
+        }
+        const int qlen = (int)P.qlen[q];
         const int32_t span = (int32_t)(y >> 32 & 0xff);
         if (j == 0) {
             dm = db = span;
         } else {  // hit.c mm_reg_set_coor
-            const int32_t tl = (int32_t)x - (int32_t)P.bx[b - 1];
-            const int32_t ql = (int32_t)y - (int32_t)P.by[b - 1];
+            const int32_t tl = (int32_t)x - (int32_t)xp;
+            const int32_t ql = (int32_t)y - (int32_t)yp;
             db = tl > ql ? tl : ql;
             dm = tl > span && ql > span ? span : tl < ql ? tl : ql;
         }
         const int32_t kk = rev ? cnt - 1 - j : j;  // est_err walking order
-        const int32_t cur = mini_idx_at(P, q, qlen, b);
+        const int32_t cur = mini_idx_at(P, q, qlen, x, y);
         fv = cnt;
         if (kk >= 1) {
-            const int32_t prev = mini_idx_at(P, q, qlen, rev ? b + 1 : b - 1);
+            const int32_t prev = rev ? mini_idx_at(P, q, qlen, xn, yn) : mini_idx_at(P, q, qlen, xp, yp);
             if (cur < 0 || cur <= prev) fv = kk;
         }
         if (kk == 0) P.c_st[c] = cur;
         if (kk == cnt - 1) P.c_last[c] = cur;
     }
+    const int32_t cr = act ? ci : -1;
     // segmented inclusive reduction over lanes of the same chain (contiguous in the wave)
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const int32_t co = __shfl_up(c, d, 64);
+        const int32_t co = __shfl_up(cr, d, 64);
         const int dmo = __shfl_up(dm, d, 64), dbo = __shfl_up(db, d, 64), fvo = __shfl_up(fv, d, 64);
-        if (lane >= d && co == c) dm += dmo, db += dbo, fv = min(fv, fvo);
+        if (lane >= d && co == cr) dm += dmo, db += dbo, fv = min(fv, fvo);
     }
-    const int32_t cn = __shfl_down(c, 1, 64);
-    if (act && (lane == 63 || cn != c)) {  // last lane of its chain piece in this wave
+    const int32_t cn = __shfl_down(cr, 1, 64);
+    if (act && (lane == 63 || cn != cr)) {  // last lane of its chain piece in this wave
         atomicAdd(P.c_mlen + c, dm);
         atomicAdd(P.c_blen + c, db);
         atomicMin(c_fv + c, fv);
@@ -227,7 +286,6 @@ __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
         return;
     }
     const int64_t b0 = P.qb[q];
-    const uint64_t *ax = P.bx + b0, *ay = P.by + b0;
     U128 *z = P.z + c0;
     hymet_mm_reg *r = P.regs + c0;
     uint32_t hash = P.name_hash[q];
@@ -237,7 +295,8 @@ __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
     for (int i = 0; i < n; ++i) {
         const int64_t k = P.cboff[c0 + i] - b0;
         const uint64_t u = P.cu[c0 + i];
-        const uint32_t h = (uint32_t)hash64((hash64(ax[k]) + hash64(ay[k])) ^ hash);
+        const int64_t a = P.ids[P.cfirst[c0 + i] + (int32_t)u - 1];  // the chain's first anchor
+        const uint32_t h = (uint32_t)hash64((hash64(P.ax[a]) + hash64(P.ay[a])) ^ hash);
         z[i].x = u ^ h;
         z[i].y = (uint64_t)k << 32 | (uint32_t)(int32_t)u;
     }
@@ -262,7 +321,8 @@ __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
         ri->mapq = 0;
         ri->pad = 0;
         const int64_t c = chain_of(P.cboff, c0, c1, b0 + ri->as);
-        set_coor(ri, qlen, ax, ay, P.c_mlen[c], P.c_blen[c]);
+        const int64_t a0 = P.ids[P.cfirst[c] + ri->cnt - 1], a1 = P.ids[P.cfirst[c]];  // first, last anchor
+        set_coor(ri, qlen, P.ax[a0], P.ay[a0], P.ax[a1], P.ay[a1], P.c_mlen[c], P.c_blen[c]);
     }
     // ---- mm_set_parent (mask_level, mask_len; no alignment: no dp_max branch)
     {
@@ -417,11 +477,12 @@ __global__ void chain_stats_init_kernel(int32_t *c_mlen, int32_t *c_blen, int32_
 
 }  // namespace
 
-int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const uint64_t *cu, const int64_t *cboff,
+int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *ids, const int64_t *cfirst,
+                   const uint64_t *cu, const int64_t *cboff,
                    const int64_t *qc, const int64_t *qb, const uint64_t *mini_pos, const int64_t *mp_off, const int64_t *qlen,
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
-                   int64_t NB, int64_t NC, int64_t NM, const int32_t *bchain, const uint32_t *cq,
+                   int64_t NB, int64_t NC, int64_t NM, const uint32_t *cq,
                    const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q) {
     if (n_q <= 0) return HYMET_OK;
     hipStream_t st = ctx->stream;
@@ -431,8 +492,9 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
     int32_t *c_mlen = cst.as<int32_t>(), *c_blen = c_mlen + (NC + 1), *c_st = c_blen + (NC + 1), *c_last = c_st + (NC + 1),
             *c_fv = c_last + (NC + 1);
     {
-        ProfScope _ps(ctx, "mm_chain_stats", (double)NB * (16.0 + 16.0 + 8.0) + (double)NM * 8.0);
-        AnchorStatParams A{bx, by, cu, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, bchain, cq,
+        // chain slot (8) + anchor x, y (16) + two pos_tab reads (8) per chained anchor
+        ProfScope _ps(ctx, "mm_chain_stats", (double)NB * (8.0 + 16.0 + 8.0) + (double)NM * 8.0);
+        AnchorStatParams A{ax, ay, cu, ids, cfirst, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, cq,
                            c_mlen, c_blen, c_st, c_last, pos_tab, qbase, skip_q};
         if (NB > 0) {
             hipLaunchKernelGGL(chain_stats_init_kernel, dim3((unsigned)cdiv(NC + 1, 256)), dim3(256), 0, st, c_mlen, c_blen,
@@ -446,7 +508,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *bx, const uint64_t *by, const
                            sumk.as<unsigned long long>());
         HY_CHECK_LAUNCH("query_sumk_kernel");
     }
-    RegParams P{bx, by, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
+    RegParams P{ax, ay, ids, cfirst, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
                 tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk.as<uint64_t>(), skip_q};
     ProfScope _ps(ctx, "mm_regions", (double)NC * (8.0 + 8.0 + 4.0 * 5) + (double)n_q * 64.0);  // chain + stats reads, reg writes

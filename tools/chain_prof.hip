@@ -53,7 +53,7 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&df, 4 * n));
     CK(hipMalloc(&dt, 4 * n));
     CK(hipMalloc(&qf, 1));
-    CK(hipMalloc(&sum, 16 * kSumInts * ns));
+    CK(hipMalloc(&sum, 16 * kGSumInts * ns));
     CK(hipMemcpy(dx, hx.data(), 8 * n, hipMemcpyHostToDevice));
     CK(hipMemcpy(dy, hy.data(), 8 * n, hipMemcpyHostToDevice));
     // groups = runs of equal x >> 32, work list by size descending, group 0 holds anchor 0
@@ -99,6 +99,11 @@ int main(int argc, char **argv) {
     // waves per CU as the library launches them (launch_chain: 16), HYMET_CHAIN_PROF_WPC overrides
     const char *wpc = getenv("HYMET_CHAIN_PROF_WPC");
     const int nblk = std::min(nwork, prop.multiProcessorCount * (wpc ? atoi(wpc) : 16));
+    {
+        int per_cu = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_groups_kernel<0>, 64, kChainLds);
+        printf("occupancy: %d waves per CU at %zu B of LDS per wave\n", per_cu, (size_t)kChainLds);
+    }
     int max_dist = 10000 < bw ? bw : 10000;
     for (int rep = 0; rep < 2; rep++) {
         unsigned long long z[32] = {0};
@@ -167,6 +172,15 @@ int main(int argc, char **argv) {
                            ba[c] / na[c], bn[c] / na[c], bx[c] / na[c], tc[c] / std::max(1.0, it[c]));
         }
 #endif
+        {  // f / p digest: variants must agree bit for bit
+            std::vector<int32_t> hf(n);
+            std::vector<int64_t> hp(n);
+            CK(hipMemcpy(hf.data(), df, 4 * n, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(hp.data(), dp, 8 * n, hipMemcpyDeviceToHost));
+            uint64_t h = 1469598103934665603ull;
+            for (int64_t i = 0; i < n; i++) h = (h ^ (uint64_t)(uint32_t)hf[i]) * 1099511628211ull, h = (h ^ (uint64_t)hp[i]) * 1099511628211ull;
+            printf("fp digest %016llx\n", (unsigned long long)h);
+        }
         const char *names[8] = {"i0-advance", "st+head", "st_in", "rmq", "walk", "winner+cert", "st_in-probe", "loop/batch"};
         double tot = 0;
         for (int k = 0; k < 8; k++) tot += (double)z[k];
@@ -180,6 +194,8 @@ int main(int argc, char **argv) {
         const char *cn2[12] = {"batch attempts", "pre: cert", "pre: b0 != prev", "pre: walk", "fail: x same", "fail: y range",
                                "fail: gap/width", "fail: cand", "fail: walk", "fail: list", "accepted", "st_in pop prefix"};
         for (int k = 0; k < 12; k++) printf("  %-20s %8.4f per anchor\n", cn2[k], (double)z[16 + k] / n);
+        const char *cn3[4] = {"head changes", "head chg repeated", "(unused)", "loop iterations"};
+        for (int k = 0; k < 4; k++) printf("  %-20s %8.4f per anchor\n", cn3[k], (double)z[28 + k] / n);
     }
     return 0;
 }
