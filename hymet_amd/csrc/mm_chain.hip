@@ -82,7 +82,7 @@ namespace {
 #endif
 // Window-start blocks passed whole are skipped by their last x (an LDS ring) instead of loaded.
 #ifndef HYMET_CHAIN_BLX
-#define HYMET_CHAIN_BLX 1
+#define HYMET_CHAIN_BLX 0
 #endif
 // A batch starts at any anchor whose window best B lies in its range (not only after B = i-1).
 #ifndef HYMET_CHAIN_B0ANY
@@ -1142,6 +1142,11 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             // in the krmq range, its score passes bw, and the inner walk cannot improve max_f.
             // The verified prefix is committed in bulk; the first failing anchor runs below.
             // Attempts back off after short batches (non-colinear stretches).
+#ifdef HYMET_CHAIN_PROF
+            if (i0 != i) CCOUNT(9);                            // no attempt: same x as the previous anchor
+            else if (i == 0 || st >= i0) CCOUNT(19);           // no attempt: empty window
+            else if (i < spec_next) CCOUNT(22);                // no attempt: back-off
+#endif
             if (i0 == i && i > 0 && st < i0 && i >= spec_next) {
                 const bool walk_ok = P.max_dist_inner <= 0 || (iok && !overflow);
                 int Lb = min(64, n - i);

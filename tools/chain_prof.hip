@@ -190,11 +190,12 @@ int main(int argc, char **argv) {
             if (z[k]) printf("  %-12s %8.0f cyc/anchor  %5.1f%%\n", names[k], (double)z[k] / n, 100.0 * z[k] / tot);
         const char *cn[8] = {"global fetch", "list ins general", "list erase general", "rmq full path", "walk",
                              "head suffix", "cert y-fail", "batches"};
+        printf("  %-20s %8.4f per anchor\n", "no try: same x", (double)z[8 + 9] / n);
         for (int k = 0; k < 8; k++) printf("  %-20s %8.4f per anchor\n", cn[k], (double)z[8 + k] / n);
         const char *cn2[12] = {"batch attempts", "pre: cert", "pre: b0 != prev", "pre: walk", "fail: x same", "fail: y range",
-                               "fail: gap/width", "fail: cand", "fail: walk", "fail: list", "accepted", "st_in pop prefix"};
+                               "fail: gap/width", "fail: cand", "fail: walk", "fail: list", "accepted", "no try: empty window"};
         for (int k = 0; k < 12; k++) printf("  %-20s %8.4f per anchor\n", cn2[k], (double)z[16 + k] / n);
-        const char *cn3[4] = {"head changes", "head chg repeated", "(unused)", "loop iterations"};
+        const char *cn3[4] = {"head changes", "head chg repeated", "no try: back-off", "loop iterations"};
         for (int k = 0; k < 4; k++) printf("  %-20s %8.4f per anchor\n", cn3[k], (double)z[28 + k] / n);
     }
     return 0;
