@@ -45,12 +45,19 @@ struct Seg {
     int32_t q;  // query
 };
 
-// segment classes: thread (<= 8), wave (<= 64), blocks of 256 / 512 / 1024 / 2048 / 4096, large
-enum { kThread = 0, kWave, kB256, kB512, kB1K, kB2K, kB4K, kLarge, kClasses };
+// segment classes: thread (<= 8), wave (<= 64), blocks of 256 / 512 / 1024 / 2048 / 4096 and,
+// for (query, strand, target) groups, 8192 / 16384 (a 1024-thread block sorting 16384 words in
+// 136 KB of LDS), large
+enum { kThread = 0, kWave, kB256, kB512, kB1K, kB2K, kB4K, kB8K, kB16K, kLarge, kClasses };
 
+// queries: up to kTile sorted whole, larger ones tiled
 __device__ __forceinline__ int seg_class(int64_t n) {
     return n <= 8 ? kThread : n <= 64 ? kWave : n <= 256 ? kB256 : n <= 512 ? kB512 : n <= 1024 ? kB1K : n <= 2048 ? kB2K
          : n <= kTile ? kB4K : kLarge;
+}
+// groups of a tiled query: whole up to 16384 (the device radix sort only above)
+__device__ __forceinline__ int seg_class_group(int64_t n) {
+    return n <= kTile ? seg_class(n) : n <= 8192 ? kB8K : n <= 16384 ? kB16K : kLarge;
 }
 
 // the anchor set written for sorted position i: x, y (groups are read from x and the query
@@ -168,47 +175,42 @@ __global__ __launch_bounds__(256) void tile_hist_kernel(const uint64_t *__restri
     for (int b = threadIdx.x; b < nbins; b += 256) row[b] = h[b];
 }
 
-// one block per large query: H[t][b] <- offset (within the query) of tile t's bin-b run;
-// every non-empty bin appended to the group list
-__global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const int64_t *tpos, int nbins,
-                                                         uint32_t *__restrict__ H, Seg *groups, int32_t *n_groups,
-                                                         int64_t *mail) {
-    __shared__ uint32_t part[256];
-    __shared__ uint32_t carry;
+// one wave per large query: H[t][b] <- offset (within the query) of tile t's bin-b run (bins
+// in order, tiles in order inside a bin); every non-empty bin appended to the group list.
+// Bins are taken 64 at a time (coalesced rows), their totals scanned with one wave scan and
+// a carry -- no block barriers (a 256-thread block with an LDS scan per 256 bins spent its
+// time in barriers: most large queries hold one or two tiles).
+__global__ __launch_bounds__(64) void query_scan_kernel(const Seg *large, const int64_t *tpos, int nbins,
+                                                        uint32_t *__restrict__ H, Seg *groups, int32_t *n_groups,
+                                                        int64_t *mail) {
     const Seg S = large[blockIdx.x];
+    const int lane = threadIdx.x;
     const int64_t t0 = tpos[S.q], t1 = t0 + (S.n + kPart - 1) / kPart;
-    if (threadIdx.x == 0) carry = 0;
-    for (int r = 0; r < nbins; r += 256) {  // bins r + tid, in bin order across rows
-        const int b = r + threadIdx.x;
-        uint32_t run = 0;
-        if (b < nbins)
-            for (int64_t t = t0; t < t1; t += 8) {  // 8 loads in flight
-                uint32_t v[8];
-#pragma unroll
-                for (int j = 0; j < 8; j++) v[j] = t + j < t1 ? H[(t + j) * nbins + b] : 0u;
-#pragma unroll
-                for (int j = 0; j < 8; j++)
-                    if (t + j < t1) {
-                        H[(t + j) * nbins + b] = run;  // exclusive within the bin, across tiles
-                        run += v[j];
-                    }
-            }
-        part[threadIdx.x] = run;
-        __syncthreads();
-        for (int d = 1; d < 256; d <<= 1) {  // inclusive scan over the row's bins
-            const uint32_t o = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-            __syncthreads();
-            part[threadIdx.x] += o;
-            __syncthreads();
+    uint32_t carry = 0;
+    for (int r = 0; r < nbins; r += 64) {
+        const int b = r + lane;
+        uint32_t tot = 0;
+        if (b < nbins) {
+#pragma unroll 4
+            for (int64_t t = t0; t < t1; t++) tot += H[t * nbins + b];
         }
-        const uint32_t base = carry + part[threadIdx.x] - run;
-        if (b < nbins && run > 0)
-            for (int64_t t = t0; t < t1; t++) H[t * nbins + b] += base;
-        const int slot = wave_append(n_groups, b < nbins && run > 0);
-        if (slot >= 0) groups[slot] = Seg{S.s + base, (int32_t)run, S.q};
-        __syncthreads();
-        if (threadIdx.x == 255) carry += part[255];
-        __syncthreads();
+        uint32_t inc = tot;  // inclusive scan over the 64 bins
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= d) inc += o;
+        }
+        const uint32_t base = carry + inc - tot;
+        if (b < nbins && tot > 0) {  // (empty bins' entries are never read)
+            uint32_t run = base;
+            for (int64_t t = t0; t < t1; t++) {
+                const uint32_t v = H[t * nbins + b];
+                H[t * nbins + b] = run;
+                run += v;
+            }
+        }
+        const int slot = wave_append(n_groups, b < nbins && tot > 0);
+        if (slot >= 0) groups[slot] = Seg{S.s + base, (int32_t)tot, S.q};
+        carry += (uint32_t)__shfl((int)inc, 63, 64);
     }
     publish_counters(n_groups, 1, mail);
 }
@@ -218,8 +220,8 @@ __global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const
 // straight to its run position scattered 12-byte writes over as many cache lines; instead each
 // round of kSub anchors is ranked by bin in LDS (wave-aggregated atomics), its bin counts are
 // scanned, the round is laid out bin by bin in LDS, and written run by run (consecutive lanes,
-// consecutive addresses).  56 KB of LDS per block.
-constexpr int kSub = 2048;
+// consecutive addresses).
+constexpr int kSub = 3072;  // 68 KB of LDS per block: two blocks per CU
 
 __global__ __launch_bounds__(256) void tile_scatter_kernel(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
                                                            const int64_t *__restrict__ tile_a0, const int32_t *__restrict__ tile_q,
@@ -306,7 +308,7 @@ __global__ __launch_bounds__(256) void group_class_kernel(const Seg *groups, int
         const int64_t g = (int64_t)blockIdx.x * 1024 + j * 256 + threadIdx.x;
         sg[j] = g < G ? groups[g] : Seg{0, 0, 0};
         if (sg[j].n == 1) out.put(sg[j].s, key[sg[j].s], val[sg[j].s]);
-        cls[j] = sg[j].n > 1 ? seg_class(sg[j].n) : -1;
+        cls[j] = sg[j].n > 1 ? seg_class_group(sg[j].n) : -1;
     }
     block_append<4>(sg, cls, lists, cap, cnt);
     publish_counters(cnt, kClasses, mail);
@@ -543,6 +545,8 @@ int sort_segments(hymet_ctx *ctx, const Seg *lists, int64_t cap, const int32_t *
     HY_SEG_LAUNCH(kB1K, (block_seg_sort_kernel<64, 16>), 64)
     HY_SEG_LAUNCH(kB2K, (block_seg_sort_kernel<128, 16>), 128)
     HY_SEG_LAUNCH(kB4K, (block_seg_sort_kernel<256, 16>), 256)
+    HY_SEG_LAUNCH(kB8K, (block_seg_sort_kernel<512, 16>), 512)
+    HY_SEG_LAUNCH(kB16K, (block_seg_sort_kernel<1024, 16>), 1024)
 #undef HY_SEG_LAUNCH
     return HYMET_OK;
 }
@@ -598,7 +602,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     HY_ARG(gcap < INT32_MAX, "grouped_anchor_sort: too many groups in one batch");
     DevBuf groups;
     HY_HIP(groups.alloc(sizeof(Seg) * (size_t)(gcap + 1), st));
-    hipLaunchKernelGGL(query_scan_kernel, dim3((unsigned)nl), dim3(256), 0, st, large, tpos.as<int64_t>(), nbins,
+    hipLaunchKernelGGL(query_scan_kernel, dim3((unsigned)nl), dim3(64), 0, st, large, tpos.as<int64_t>(), nbins,
                        H.as<uint32_t>(), groups.as<Seg>(), ctx->dctr + kCtrGroups, mb_dev(ctx, kMbGroups));
     HY_CHECK_LAUNCH("query_scan_kernel");
     hipLaunchKernelGGL(tile_scatter_kernel, dim3((unsigned)NT), dim3(256), 0, st, key, val, ta0.as<int64_t>(), tq.as<int32_t>(),
