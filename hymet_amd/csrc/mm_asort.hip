@@ -175,42 +175,47 @@ __global__ __launch_bounds__(256) void tile_hist_kernel(const uint64_t *__restri
     for (int b = threadIdx.x; b < nbins; b += 256) row[b] = h[b];
 }
 
-// one wave per large query: H[t][b] <- offset (within the query) of tile t's bin-b run (bins
-// in order, tiles in order inside a bin); every non-empty bin appended to the group list.
-// Bins are taken 64 at a time (coalesced rows), their totals scanned with one wave scan and
-// a carry -- no block barriers (a 256-thread block with an LDS scan per 256 bins spent its
-// time in barriers: most large queries hold one or two tiles).
-__global__ __launch_bounds__(64) void query_scan_kernel(const Seg *large, const int64_t *tpos, int nbins,
-                                                        uint32_t *__restrict__ H, Seg *groups, int32_t *n_groups,
-                                                        int64_t *mail) {
+// one block per large query: H[t][b] <- offset (within the query) of tile t's bin-b run;
+// every non-empty bin appended to the group list
+__global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const int64_t *tpos, int nbins,
+                                                         uint32_t *__restrict__ H, Seg *groups, int32_t *n_groups,
+                                                         int64_t *mail) {
+    __shared__ uint32_t part[256];
+    __shared__ uint32_t carry;
     const Seg S = large[blockIdx.x];
-    const int lane = threadIdx.x;
     const int64_t t0 = tpos[S.q], t1 = t0 + (S.n + kPart - 1) / kPart;
-    uint32_t carry = 0;
-    for (int r = 0; r < nbins; r += 64) {
-        const int b = r + lane;
-        uint32_t tot = 0;
-        if (b < nbins) {
-#pragma unroll 4
-            for (int64_t t = t0; t < t1; t++) tot += H[t * nbins + b];
-        }
-        uint32_t inc = tot;  // inclusive scan over the 64 bins
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
-            if (lane >= d) inc += o;
-        }
-        const uint32_t base = carry + inc - tot;
-        if (b < nbins && tot > 0) {  // (empty bins' entries are never read)
-            uint32_t run = base;
-            for (int64_t t = t0; t < t1; t++) {
-                const uint32_t v = H[t * nbins + b];
-                H[t * nbins + b] = run;
-                run += v;
+    if (threadIdx.x == 0) carry = 0;
+    for (int r = 0; r < nbins; r += 256) {  // bins r + tid, in bin order across rows
+        const int b = r + threadIdx.x;
+        uint32_t run = 0;
+        if (b < nbins)
+            for (int64_t t = t0; t < t1; t += 8) {  // 8 loads in flight
+                uint32_t v[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) v[j] = t + j < t1 ? H[(t + j) * nbins + b] : 0u;
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (t + j < t1) {
+                        H[(t + j) * nbins + b] = run;  // exclusive within the bin, across tiles
+                        run += v[j];
+                    }
             }
+        part[threadIdx.x] = run;
+        __syncthreads();
+        for (int d = 1; d < 256; d <<= 1) {  // inclusive scan over the row's bins
+            const uint32_t o = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+            __syncthreads();
+            part[threadIdx.x] += o;
+            __syncthreads();
         }
-        const int slot = wave_append(n_groups, b < nbins && tot > 0);
-        if (slot >= 0) groups[slot] = Seg{S.s + base, (int32_t)tot, S.q};
-        carry += (uint32_t)__shfl((int)inc, 63, 64);
+        const uint32_t base = carry + part[threadIdx.x] - run;
+        if (b < nbins && run > 0)
+            for (int64_t t = t0; t < t1; t++) H[t * nbins + b] += base;
+        const int slot = wave_append(n_groups, b < nbins && run > 0);
+        if (slot >= 0) groups[slot] = Seg{S.s + base, (int32_t)run, S.q};
+        __syncthreads();
+        if (threadIdx.x == 255) carry += part[255];
+        __syncthreads();
     }
     publish_counters(n_groups, 1, mail);
 }
@@ -602,7 +607,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     HY_ARG(gcap < INT32_MAX, "grouped_anchor_sort: too many groups in one batch");
     DevBuf groups;
     HY_HIP(groups.alloc(sizeof(Seg) * (size_t)(gcap + 1), st));
-    hipLaunchKernelGGL(query_scan_kernel, dim3((unsigned)nl), dim3(64), 0, st, large, tpos.as<int64_t>(), nbins,
+    hipLaunchKernelGGL(query_scan_kernel, dim3((unsigned)nl), dim3(256), 0, st, large, tpos.as<int64_t>(), nbins,
                        H.as<uint32_t>(), groups.as<Seg>(), ctx->dctr + kCtrGroups, mb_dev(ctx, kMbGroups));
     HY_CHECK_LAUNCH("query_scan_kernel");
     hipLaunchKernelGGL(tile_scatter_kernel, dim3((unsigned)NT), dim3(256), 0, st, key, val, ta0.as<int64_t>(), tq.as<int32_t>(),
