@@ -1695,13 +1695,17 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
         // each walk was 2.6x slower: walks mark the upcoming candidates, so most re-reads
         // failed one round trip at a time.)
         int64_t ptop = -1;  // the block covers z positions (ptop - 64 * kBtProbe, ptop]
+        // z entries (f >= min_sc) not yet marked: every mark is counted as it is kept, so the
+        // probes stop once none is left (after a group's main chain the remaining z entries
+        // are all marked, and reading them back cost a few dependent round trips per block)
+        int64_t zrem = z1 - z0;
         int32_t zc[kBtProbe], tv[kBtProbe], zfv[kBtProbe];
         int64_t zpv[kBtProbe];  // f and p of the entries that read unmarked: a walk's start
 #if HYMET_BT_TRIV
         int32_t tqv[kBtProbe], fqv[kBtProbe];  // t and f of their predecessors (t as read at the probe)
 #endif
         bool stale = false;
-        while (k >= z0) {
+        while (k >= z0 && zrem > 0) {
             if (ptop < 0 || k <= ptop - 64 * kBtProbe) {
                 c_probe++;
                 ptop = k;
@@ -1773,7 +1777,7 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             // never a chain (min_cnt >= 2).  No other mark changes, so the block stays fresh.
             if (P.min_cnt >= 2 && (zpsel < 0 || uni(tqsel) != 0)) {
                 const int32_t sv = zpsel < 0 ? zf : zf - uni(fqsel);
-                if (sv > 0) P.t[zi] = 1;  // every lane: same value, same address
+                if (sv > 0) P.t[zi] = 1, zrem--;  // every lane: same value, same address
                 c_walk++;
                 continue;
             }
@@ -1783,6 +1787,7 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             buf[0] = zi;  // every lane: same value, same address
             P.t[zi] = 2;  // path nodes are marked as recorded; those past the best end are unmarked after
             int64_t len = 1, nv = 0;  // recorded path nodes; chain = path[0, nv)
+            int64_t zc_len = 1, zc_nv = 0;  // z entries among path[0, len) and path[0, nv) (the start is one)
             int32_t max_s = 0;
             int64_t nxt = uni64(zpsel);
             int64_t whi = -1;  // window: chunk c, lane l holds anchor whi - 64c - l
@@ -1801,7 +1806,7 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             for (;;) {
                 c_step++;
                 if (nxt < 0) {  // the path reached the start of its chain
-                    if (zf > max_s) max_s = zf, nv = len;
+                    if (zf > max_s) max_s = zf, nv = len, zc_nv = zc_len;
                     break;
                 }
                 if (nxt > whi || nxt <= whi - 64 * kBtChunks) {
@@ -1845,9 +1850,11 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                 }
                 const uint64_t lim = ulim < 0 ? 0ull : ulim >= 63 ? ~0ull : (2ull << ulim) - 1;
                 const uint64_t mu = mupd & lim;
+                const uint64_t mz = __ballot(lane >= o && lane <= last && wf >= P.min_sc);  // recorded z entries
                 if (mu) {
                     const int u = 63 - __clzll((long long)mu);
                     nv = len + (u - o);
+                    zc_nv = zc_len + __popcll(mz & ((1ull << u) - 1));  // path[0, nv) ends at lane u - 1
                     max_s = __builtin_amdgcn_readlane(incl, u);  // = s_u: it beat every earlier value
                 }
                 if (lane >= o && lane <= last) {
@@ -1855,6 +1862,7 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                     P.t[j] = 2;  // the walk never re-reads a node it has passed (p[i] < i)
                 }
                 len += last - o + 1;
+                zc_len += __popcll(mz);
                 if (done) break;
                 nxt = rlane64(wp, R);  // predecessor of the run's last node
             }
@@ -1867,6 +1875,7 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             // issued them).
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             for (int64_t a = nv + lane; a < len; a += 64) P.t[ld_l2(buf + a)] = 0;
+            zrem -= zc_nv;  // path[0, nv) stays marked (in a chain or used), the rest was cleared
             const int32_t sc = nv == 0 ? 0 : max_s;
             if (sc >= P.min_sc && nv > 0 && nv >= P.min_cnt) {
                 P.chain_u[g0 + nc] = (uint64_t)(uint32_t)sc << 32 | (uint32_t)nv;  // every lane: same value

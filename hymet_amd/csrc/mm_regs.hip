@@ -158,21 +158,20 @@ __device__ __forceinline__ int32_t mini_idx_at(const AnchorStatParams &P, int64_
     return (x >= 0 && x < qlen) ? P.pos_tab[P.qbase[q] + x] : -1;
 }
 
-__global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams P, int32_t *c_fv) {
-    __shared__ int64_t s_c0;
+// the chain holding chain-order position 256 b, for every block b of chain_stats_flat_kernel
+// (one thread per chain writes the block starts inside it: no per-block binary search, whose
+// ~log2(NC) dependent loads held the whole block)
+__global__ void block_chain_kernel(const int64_t *cboff, int64_t NC, int64_t NB, int32_t *blk_c0) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= NC) return;
+    const int64_t s = cboff[c], e = c + 1 < NC ? cboff[c + 1] : NB;
+    for (int64_t b = (s + 255) >> 8; (b << 8) < e; ++b) blk_c0[b] = (int32_t)c;
+}
+
+__global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams P, const int32_t *blk_c0, int32_t *c_fv) {
     __shared__ int32_t s_st[257];  // block-relative starts of chains c0 .. c0 + 256 (clamped)
     const int64_t b0 = (int64_t)blockIdx.x * blockDim.x;
-    if (threadIdx.x == 0) {
-        int64_t lo = 0, hi = P.NC - 1;  // last c with cboff[c] <= b0
-        while (lo < hi) {
-            const int64_t mid = (lo + hi + 1) >> 1;
-            if (P.cboff[mid] <= b0) lo = mid;
-            else hi = mid - 1;
-        }
-        s_c0 = lo;
-    }
-    __syncthreads();
-    const int64_t cb0 = s_c0;
+    const int64_t cb0 = blk_c0[blockIdx.x];  // last c with cboff[c] <= b0
     for (int i = threadIdx.x; i < 257; i += blockDim.x) {
         const int64_t cc = cb0 + i;
         s_st[i] = cc < P.NC ? (int32_t)min(P.cboff[cc] - b0, (int64_t)256) : 256;
@@ -486,7 +485,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
                    const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q) {
     if (n_q <= 0) return HYMET_OK;
     hipStream_t st = ctx->stream;
-    DevBuf cst, sumk;
+    DevBuf cst, sumk, blk;
     HY_HIP(cst.alloc(4 * 5 * (size_t)(NC + 1), st));
     HY_HIP(sumk.alloc(8 * (size_t)n_q, st));
     int32_t *c_mlen = cst.as<int32_t>(), *c_blen = c_mlen + (NC + 1), *c_st = c_blen + (NC + 1), *c_last = c_st + (NC + 1),
@@ -500,7 +499,12 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
             hipLaunchKernelGGL(chain_stats_init_kernel, dim3((unsigned)cdiv(NC + 1, 256)), dim3(256), 0, st, c_mlen, c_blen,
                                c_fv, NC + 1);
             HY_CHECK_LAUNCH("chain_stats_init_kernel");
-            hipLaunchKernelGGL(chain_stats_flat_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A, c_fv);
+            HY_HIP(blk.alloc(4 * (size_t)(cdiv(NB, 256) + 1), st));
+            hipLaunchKernelGGL(block_chain_kernel, dim3((unsigned)cdiv(NC, 256)), dim3(256), 0, st, cboff, NC, NB,
+                               blk.as<int32_t>());
+            HY_CHECK_LAUNCH("block_chain_kernel");
+            hipLaunchKernelGGL(chain_stats_flat_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A,
+                               (const int32_t *)blk.as<int32_t>(), c_fv);
             HY_CHECK_LAUNCH("chain_stats_flat_kernel");
         }
         const int nqb = n_q < ctx->n_cu * 64 ? n_q : ctx->n_cu * 64;
