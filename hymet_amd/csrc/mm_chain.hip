@@ -543,30 +543,34 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         };
         int32_t i0 = 0, st = 0, st_in = 0;
         bool t_used = false;  // the overflow walk stamped t_global
-#if HYMET_CHAIN_HCPF
+        // head-cache prefetch (HYMET_CHAIN_HCPF: 1 both passes, 2 the long join only): when the
+        // head cache takes block b, block b + 1's x, y, f are loaded into registers (p-less, as
+        // every HBM entry fetch), so the next window-start block change does not wait on HBM
+        constexpr bool kHcpf = HYMET_CHAIN_HCPF == 1 || (HYMET_CHAIN_HCPF == 2 && kLongPass);
+        static_assert(!kHcpf || HYMET_CHAIN_HNOP, "the prefetched head entries carry no p");
         int32_t pfb = -1, pf_x = 0, pf_ylo = 0, pf_yhi = 0, pf_f = 0;  // block pfb's entries (lane l: entry l)
-        int64_t pf_p = 0;
-        auto hc_take = [&](int32_t b) -> Ent {  // entry (b << 6) + lane for the head cache, then prefetch b + 1
-            Ent e;
-            if (b == pfb) {
-                e.x = pf_x, e.y = pf_ylo, e.f = pf_f;
-                e.pw = (int32_t)((pf_p < 0 ? 0u : (uint32_t)(pf_p - g0 + 1)) | ((uint32_t)pf_yhi & 0xff) << 24);
+        auto hc_take = [&](int32_t b) -> Ent {  // entry (b << 6) + lane for the head cache
+            if constexpr (!kHcpf) {
+                return fetch((b << 6) + lane);
             } else {
-                e = fetch((b << 6) + lane);
+                Ent e;
+                if (b == pfb) {
+                    e.x = pf_x, e.y = pf_ylo, e.f = pf_f;
+                    e.pw = (int32_t)(((uint32_t)pf_yhi & 0xff) << 24);
+                } else {
+                    e = fetch((b << 6) + lane);
+                }
+                const int32_t jn = ((b + 1) << 6) + lane;
+                if (((b + 1) << 6) + 63 < i0) {
+                    const int32_t *ax32 = reinterpret_cast<const int32_t *>(P.ax + g0 + jn);
+                    const int32_t *ay32 = reinterpret_cast<const int32_t *>(P.ay + g0 + jn);
+                    pf_x = ax32[0], pf_ylo = ay32[0], pf_yhi = ay32[1];
+                    pf_f = ld_l2(P.f + g0 + jn);
+                    pfb = b + 1;
+                }
+                return e;
             }
-            const int32_t jn = ((b + 1) << 6) + lane;
-            if (((b + 1) << 6) + 63 < i0) {
-                const int32_t *ax32 = reinterpret_cast<const int32_t *>(P.ax + g0 + jn);
-                const int32_t *ay32 = reinterpret_cast<const int32_t *>(P.ay + g0 + jn);
-                pf_x = ax32[0], pf_ylo = ay32[0], pf_yhi = ay32[1];
-                pf_f = ld_l2(P.f + g0 + jn), pf_p = ld_l2(P.p + g0 + jn);
-                pfb = b + 1;
-            }
-            return e;
         };
-#else
-        auto hc_take = [&](int32_t b) -> Ent { return fetch((b << 6) + lane); };
-#endif
         auto sum_at = [&](int32_t b, int k) -> int4 {  // word k of block b's summary
             if ((i0 >> 6) - b <= kSumRing) return ssum[(b & (kSumRing - 1)) * kSumInts + k];
             return ld_l2(gsum + (int64_t)b * kGSumInts + k);
