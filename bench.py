@@ -119,14 +119,16 @@ def cpu_info():
 
 
 # ------------------------------------------------------------------ CAMI-medium
-def build_cami(args, comm, gpu):
-    from hymet_amd import ingest, pipeline, screen as scr, synth
-    from hymet_amd.msh import SketchDB, write_msh
-    from hymet_amd.seqio import DevicePool, from_records
+def cami_inputs(args, sketch):
+    """The CAMI-shaped workload of `args` (bench.py's own; tests/golden/make_cami_golden.py
+    builds the same one on the CPU): (workload, FASTA bytes, sketch DBs).  sketch(w) returns
+    the Mash sketch (k=21, s=1000, seed 42) of every candidate genome, by the GPU here and
+    by the oracle in the fixture generator, so both sides screen the same DB bytes."""
+    from hymet_amd import ingest, synth
+    from hymet_amd.msh import SketchDB
     t0 = time.time()
     # the same community and the same contig pool on every rank (strong scaling)
-    w = synth.make_cami(np.random.default_rng(1234), n_taxa=args.taxa, per_taxon=args.per_taxon,
-                        contig_gbp=args.contig_gbp, contig_rng=np.random.default_rng(5000))
+    w = make_workload(args)
     # MEGAHIT-style headers, as CAMI's assemblies carry them
     heads = [f"{n} flag=1 multi={2 + i % 7}.0000 len={len(s)}" for i, (n, s) in enumerate(zip(w.contig_names, w.contigs))]
     fasta = ingest.to_fasta(heads, w.contigs, width=args.fasta_width)
@@ -134,8 +136,7 @@ def build_cami(args, comm, gpu):
         f"FASTA {len(fasta)/1e6:.0f} MB ({time.time()-t0:.1f}s)")
     t0 = time.time()
     db_names = [n + ".fna.gz" for n in w.ref_names]
-    refs_ss = from_records([(n, "", s) for n, s in zip(w.ref_names, w.refs)])
-    sk = scr.sketch_sequences(gpu, DevicePool(gpu, refs_ss, DevicePool.ALPHA_MASH), 21, 42, 1000)
+    sk = sketch(w)
     # sketch DBs of H hashes each (sketch1, and for CAMI-high GTDB/custom-sized sketch2/3):
     # the candidates' own sketches split over the DBs by share, decoy references fill up
     sizes = [int(float(x)) for x in args.db_hashes.split(",")]
@@ -154,9 +155,30 @@ def build_cami(args, comm, gpu):
                                                for i in range(n_dec)]
         dbs.append(SketchDB(names=names, comments=[f"[1 seqs] {n}" for n in names],
                             lengths=np.full(len(names), 4_000_000, np.int64), offsets=off, hashes=hashes))
-    db = dbs[0]
     log(f"sketch DBs: " + ", ".join(f"{x.n_refs} refs / {len(x.hashes)/1e6:.0f}M hashes" for x in dbs) +
         f" ({time.time()-t0:.1f}s)")
+    return w, fasta, dbs
+
+
+def make_workload(args):
+    from hymet_amd import synth
+    return synth.make_cami(np.random.default_rng(1234), n_taxa=args.taxa, per_taxon=args.per_taxon,
+                           contig_gbp=args.contig_gbp, contig_rng=np.random.default_rng(5000))
+
+
+def build_cami(args, comm, gpu):
+    from hymet_amd import pipeline, screen as scr
+    from hymet_amd.msh import write_msh
+    from hymet_amd.seqio import DevicePool, from_records
+    held = {}
+
+    def gpu_sketch(w):
+        held["refs"] = from_records([(n, "", s) for n, s in zip(w.ref_names, w.refs)])
+        return scr.sketch_sequences(gpu, DevicePool(gpu, held["refs"], DevicePool.ALPHA_MASH), 21, 42, 1000)
+
+    w, fasta, dbs = cami_inputs(args, gpu_sketch)
+    refs_ss = held["refs"]
+    db = dbs[0]
     td = tempfile.mkdtemp(prefix="hymet_bench_")
     # the DBs as Mash .msh files (data/sketch{1,2,3}.msh): every step reads them, as every
     # `mash screen` does (scripts/mash.sh:14), so S1 is inside the timed window
@@ -273,7 +295,38 @@ def bench_cami(args, comm, gpu, torch):
     return out
 
 
-def cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier, budget_s=None):
+def host_cpus():
+    """(CPUs this process may run on, the cgroup CPU quota in CPUs or None): the box's
+    nproc counts the whole machine, the scheduler affinity and the cgroup quota what a job
+    actually gets."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
+def cpu_threads_default():
+    """The job's CPU share: the affinity set, capped by the cgroup quota and by the thread
+    count the box assigns a job (OMP_NUM_THREADS; the GPU pool sets 16 per GPU job)."""
+    aff, quota = host_cpus()
+    n = min(aff, int(quota) if quota else aff)
+    try:
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", "0")) or n)
+    except ValueError:
+        pass
+    return max(1, n)
+
+
+def cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier, budget_s=None, must=None, n_random=None):
     """The CPU oracle restatement on a bounded sample of the same workload, on the host's
     cores, CHECKED against the GPU run: worker threads take 8-contig batches of a random
     sample and run the minimap2 asm10 restatement against the same candidate index parts
@@ -282,7 +335,10 @@ def cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier, budget_s=None):
     screened in one oracle run (Mash screens the pooled input once) and classified by the
     classification_cami restatement with the run's global ref_abundance (the per-target
     line counts of the whole PAF, classification_cami.py:181-208).  The sample's PAF lines
-    and TSV rows must equal the GPU's for the same contigs (single GPU)."""
+    and TSV rows must equal the GPU's for the same contigs (single GPU).
+    must: contig indices mapped before the random ones and regardless of the budget (the
+    stratified C5 check: every long contig); n_random: exactly this many random contigs
+    after them, with no time budget."""
     import threading
     from concurrent.futures import ThreadPoolExecutor
     from hymet_amd.ingest import FastaIndex
@@ -301,24 +357,33 @@ def cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier, budget_s=None):
         parts.append(oracle_lib.mm_index_from_arrays(hs, pos, ix.lens[first:first + n], ix.names[first:first + n]))
     opt = oracle_lib.asm10_opt()
     opt.mid_occ = ix.opt.mid_occ
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    aff, quota = host_cpus()
+    threads = max(1, min(args.cpu_threads or cpu_threads_default(), aff))
     log(f"cpu baseline setup {time.time()-t0:.1f}s, {threads} threads")
     d = fasta
 
     def seq(i):
         return d[fx.seq_off[i]:fx.seq_end[i]].replace(b"\n", b"").replace(b"\r", b"")
 
-    order = [int(q) for q in np.random.default_rng(7).permutation(fx.n)]
+    forced = [int(q) for q in (must if must is not None else [])]
+    fset = set(forced)
+    order = forced + [int(q) for q in np.random.default_rng(7).permutation(fx.n) if int(q) not in fset]
+    if n_random is not None:
+        order = order[:len(forced) + n_random]
+        budget_s = float("inf")
     lock = threading.Lock()
     state = {"next": 0, "contigs": 0, "bases": 0, "done": [], "paf": {}}
     t_start = time.perf_counter()
 
     def worker(_):
-        while time.perf_counter() - t_start < budget_s:
+        while True:
             with lock:
                 b0 = state["next"]
-                state["next"] += 8
-            batch = order[b0:b0 + 8]
+                if b0 >= len(forced) and time.perf_counter() - t_start >= budget_s:
+                    return
+                # the forced (long) contigs one at a time, the random ones 8 per batch
+                state["next"] += 1 if b0 < len(forced) else 8
+                batch = order[b0:state["next"]]
             if not batch:
                 return
             seqs = [(names[i], seq(i)) for i in batch]
@@ -366,9 +431,11 @@ def cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier, budget_s=None):
     model, ncpu = cpu_info()
     out = {"value": state["contigs"] / dt, "unit": "contigs/s", "cores": threads, "kind": "port",
            "mbp_per_s": state["bases"] / 1e6 / dt, "cpu_model": model, "nproc": ncpu,
+           "sched_affinity_cpus": aff, "cgroup_cpu_quota": quota,
            "checked": {"contigs": len(done), "paf_identical": paf_ok, "tsv_rows_identical": tsv_ok,
                        "paf_lines": len(paf_lines)},
-           "sample": f"{state['contigs']} random contigs / {state['bases']/1e6:.2f} Mbp on {threads} threads: oracle "
+           "sample": (f"{len(forced)} listed + " if forced else "") +
+                     f"{state['contigs'] - len(forced)} random contigs / {state['bases']/1e6:.2f} Mbp on {threads} threads: oracle "
                      f"minimap2 asm10 vs the same {len(ix.parts)} index parts, one oracle screen run over those contigs "
                      f"(prebuilt table, {db.n_refs} refs), classification_cami restatement with the run's global "
                      f"ref_abundance, {dt:.1f}s"}
@@ -494,7 +561,8 @@ def parse_args(argv=None):
     ap.add_argument("--db-hashes", default=None, help="hashes per sketch DB, comma-separated (C4: 1e8; C5: 1e8,5e7,1e7)")
     ap.add_argument("--cand-max", type=int, default=5000, help="CAND_MAX (run_hymet_cami.sh:26)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="CPU baseline threads (the GPU box's CPU share is 16)")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline threads (default: every CPU the scheduler affinity and cgroup quota give this job)")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU mapping in the checked CPU leg")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend for N > 1 (auto: nccl = RCCL over xGMI)")

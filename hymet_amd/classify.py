@@ -40,6 +40,18 @@ CAMI, LEGACY = 0, 1
 
 
 # ------------------------------------------------------------------ taxonomy maps
+def add_alias(m: Dict[str, str], tok, tax) -> None:
+    """The identifier rule shared by classification_cami.py:84-93 and build_id_map.py:20-24:
+    a stripped, non-empty token maps to its TaxID unless an earlier row claimed it, and so
+    does its versionless form (the part before the first '.')."""
+    tok = (tok or "").strip()
+    if not tok:
+        return
+    m.setdefault(tok, tax)
+    if "." in tok:
+        m.setdefault(tok.split(".", 1)[0], tax)
+
+
 class TaxonomyMap:
     """identifier -> TaxID string.  CAMI variant: classification_cami.py:63-102 (first row
     wins, versionless aliases, GCF/GCA and accession regex hits from every column); legacy:
@@ -60,14 +72,7 @@ class TaxonomyMap:
                             self.m[c] = tax
 
     def _add(self, tok, tax):
-        if not tok:
-            return
-        tok = tok.strip()
-        if not tok:
-            return
-        self.m.setdefault(tok, tax)
-        if "." in tok:
-            self.m.setdefault(tok.split(".", 1)[0], tax)
+        add_alias(self.m, tok, tax)
 
     def _load_cami(self, path):
         with open(path, "r", newline="") as f:

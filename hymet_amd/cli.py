@@ -107,8 +107,11 @@ def cmd_limit(argv: Sequence[str]) -> int:
     if not cands:
         raise SystemExit(f"No candidates found in {a.selected}")
     scores = sel.read_scores([s for s in a.score_files if os.path.exists(s)])
-    # never downloads: without local assembly summaries the species key is the accession
-    smap = sel.species_map(a.assembly_dir) if a.dedupe else {}
+    # never downloads: without local assembly summaries the species key is the accession.
+    # Default directory as limit_candidates.py:259-263 resolves it (repo/data/...).
+    adir = a.assembly_dir or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data",
+                                          "downloaded_genomes", "assembly_summaries")
+    smap = sel.species_map(adir) if a.dedupe else {}
     chosen = sel.limit(cands, scores, a.max, a.dedupe, smap)
     tmp = a.output + ".tmp"
     _write_lines(tmp, chosen)

@@ -106,8 +106,12 @@ __device__ __forceinline__ void block_append(const Seg (&sg)[ITEMS], const int (
     if (threadIdx.x < kClasses) gb[threadIdx.x] = lc[threadIdx.x] ? atomicAdd(&cnt[threadIdx.x], lc[threadIdx.x]) : 0;
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < ITEMS; j++)
-        if (cls[j] >= 0) lists[cls[j] * cap + gb[cls[j]] + slot[j]] = sg[j];
+    for (int j = 0; j < ITEMS; j++) {
+        // the counters persist across calls (cleared by each kernel's last block): a stale
+        // count must never write past a list; the host checks the totals against cap
+        const int64_t at = cls[j] >= 0 ? (int64_t)gb[cls[j]] + slot[j] : cap;
+        if (at < cap) lists[cls[j] * cap + at] = sg[j];
+    }
 }
 
 // queries by size class (large: tiles counted)
@@ -178,8 +182,8 @@ __global__ __launch_bounds__(256) void tile_hist_kernel(const uint64_t *__restri
 // one block per large query: H[t][b] <- offset (within the query) of tile t's bin-b run;
 // every non-empty bin appended to the group list
 __global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const int64_t *tpos, int nbins,
-                                                         uint32_t *__restrict__ H, Seg *groups, int32_t *n_groups,
-                                                         int64_t *mail) {
+                                                         uint32_t *__restrict__ H, Seg *groups, int64_t cap,
+                                                         int32_t *n_groups, int64_t *mail) {
     __shared__ uint32_t part[256];
     __shared__ uint32_t carry;
     const Seg S = large[blockIdx.x];
@@ -212,7 +216,7 @@ __global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const
         if (b < nbins && run > 0)
             for (int64_t t = t0; t < t1; t++) H[t * nbins + b] += base;
         const int slot = wave_append(n_groups, b < nbins && run > 0);
-        if (slot >= 0) groups[slot] = Seg{S.s + base, (int32_t)run, S.q};
+        if (slot >= 0 && slot < cap) groups[slot] = Seg{S.s + base, (int32_t)run, S.q};  // host checks the total
         __syncthreads();
         if (threadIdx.x == 255) carry += part[255];
         __syncthreads();
@@ -579,7 +583,10 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     HY_CHECK_LAUNCH("query_class_kernel");
     HY_HIP(hipStreamSynchronize(st));
     int32_t hq[kClasses] = {};
-    for (int c = 0; c < kClasses; c++) hq[c] = (int32_t)mb_read(ctx, kMbQClass + c);
+    for (int c = 0; c < kClasses; c++) {
+        hq[c] = (int32_t)mb_read(ctx, kMbQClass + c);
+        if (hq[c] < 0 || hq[c] > n_q) return hymet::fail(HYMET_E_INTERNAL, "grouped_anchor_sort: query class count > cap");
+    }
     ProfScope _ps(ctx, "mm_anchor_gsort", 52.0 * (double)n);  // key+y read, scatter write, sort read, x+y write
     // 2 small queries: sorted whole
     int rc = sort_segments(ctx, qlists.as<Seg>(), n_q, hq, key, val, 1 + rb + pb, ybits, out);
@@ -608,7 +615,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     DevBuf groups;
     HY_HIP(groups.alloc(sizeof(Seg) * (size_t)(gcap + 1), st));
     hipLaunchKernelGGL(query_scan_kernel, dim3((unsigned)nl), dim3(256), 0, st, large, tpos.as<int64_t>(), nbins,
-                       H.as<uint32_t>(), groups.as<Seg>(), ctx->dctr + kCtrGroups, mb_dev(ctx, kMbGroups));
+                       H.as<uint32_t>(), groups.as<Seg>(), gcap, ctx->dctr + kCtrGroups, mb_dev(ctx, kMbGroups));
     HY_CHECK_LAUNCH("query_scan_kernel");
     hipLaunchKernelGGL(tile_scatter_kernel, dim3((unsigned)NT), dim3(256), 0, st, key, val, ta0.as<int64_t>(), tq.as<int32_t>(),
                        tn.as<int32_t>(), d_qoff, gb, nbins, H.as<uint32_t>(), okey, oval);
@@ -617,6 +624,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     HY_HIP(hipStreamSynchronize(st));
     const int32_t G = (int32_t)mb_read(ctx, kMbGroups);
     if (G == 0) return HYMET_OK;
+    if (G < 0 || G > gcap) return hymet::fail(HYMET_E_INTERNAL, "grouped_anchor_sort: group count > cap");
     DevBuf glists;
     HY_HIP(glists.alloc(sizeof(Seg) * kClasses * (size_t)G, st));
     hipLaunchKernelGGL(group_class_kernel, dim3((unsigned)cdiv(G, 1024)), dim3(256), 0, st, groups.as<Seg>(), (int64_t)G,
@@ -624,7 +632,10 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     HY_CHECK_LAUNCH("group_class_kernel");
     HY_HIP(hipStreamSynchronize(st));
     int32_t hg[kClasses] = {};
-    for (int c = 0; c < kClasses; c++) hg[c] = (int32_t)mb_read(ctx, kMbGClass + c);
+    for (int c = 0; c < kClasses; c++) {
+        hg[c] = (int32_t)mb_read(ctx, kMbGClass + c);
+        if (hg[c] < 0 || hg[c] > G) return hymet::fail(HYMET_E_INTERNAL, "grouped_anchor_sort: group class count > cap");
+    }
     rc = sort_segments(ctx, glists.as<Seg>(), (int64_t)G, hg, okey, oval, gb, ybits, out);
     if (rc) return rc;
     if (hg[kLarge] > 0) {

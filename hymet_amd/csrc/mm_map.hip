@@ -2,12 +2,15 @@
 // (replaces `minimap2 -x asm10 reference.mmi input/ *.fna`, scripts/minimap2.sh:23;
 // SURVEY.md §3.4, §8a rows A2-A4).  Stage by stage (map.c mm_map_frag):
 //   1 sketch every query (mm_sketch_kernel, rid 0)
-//   2 mm_seed_mz_flt: per-query over-represented minimizers, by a (query, x) sort + runs
+//   2 mm_seed_mz_flt: per-query over-represented minimizers (an LDS bucket screen per query;
+//     a (query, x) radix sort + run count only for the queries it cannot clear)
 //   3 seeds: CSR lookup of every minimizer (two adjacent loads), then one thread per query
 //     replays mm_seed_select / mm_collect_matches (high-occurrence streaks, rep_len,
 //     mini_pos) -- sequential by nature but O(minimizers) and parallel over queries
 //   4 anchors: exclusive scan of seed occurrence counts, one thread per seed writes them
-//   5 sort anchors by (query, strand, target, tpos, qpos) with stable rocPRIM radix passes
+//   5 sort anchors by (query, strand, target, tpos, qpos): the grouped per-query sort of
+//     mm_asort.hip (block sorts in LDS; the library's LSD radix sort only for groups of
+//     more than 16384 anchors)
 //   6 groups (query, strand, target) -> chain_groups_kernel (one wave per group) ->
 //     backtrack_groups_kernel -> chains ordered by first anchor (compact_a)
 //   7 long-join re-chain of the chained anchors with bw_long for the queries that need it

@@ -14,14 +14,14 @@
 // batches, one write launch into fixed per-chunk slots (slot_cap entries, counted on the
 // way) -> scan of the counts -> a compaction copy (the winnowing replay runs once).
 //
-// Index: minimizer (hash = x>>8, y) pairs are sorted by (hash, y) with two stable rocPRIM
-// radix passes and laid out as a CSR over ALL 4^k hash values (k <= 15: 2^30+1 uint32
+// Index: minimizer (hash = x>>8, y) pairs are sorted by (hash, y) with the library's stable
+// LSD radix sort (sort.hpp): y first (32 + bits_for(n_seq) bits), then the hash (2k bits);
+// the sorted pairs are copied into idx->d_hash / idx->d_pos and laid out as a CSR over ALL
+// 4^k hash values (k <= 15: 2^30+1 uint32
 // offsets = 4.3 GB per index part, which MI355X's 288 GB HBM affords), so a seed lookup is
 // two adjacent loads instead of a hash-table probe chain.
 #include "mm_common.hpp"
 
-// the cold index build keeps rocPRIM's onesweep for its one-off sorts of every reference
-// minimizer (hundreds of millions); the warm mapping path uses the library's own sort.hpp
 #include "sort.hpp"
 
 #include <cstdio>

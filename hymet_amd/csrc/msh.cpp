@@ -74,7 +74,22 @@ struct Reader {
             const bool dbl = (p >> 2) & 1;
             const int tseg = (int)(p >> 32);
             const int64_t land = (int64_t)((p >> 3) & ((1ull << 29) - 1));
-            if (!dbl) return resolve(tseg, land, out);
+            if (!dbl) {
+                // single-far: the landing pad is an ordinary struct / list pointer in the
+                // target segment; a far or capability pad there is malformed (and a far pad
+                // could loop), so decode it here without recursing
+                uint64_t pad;
+                if (!word_at(tseg, land, &pad)) return false;
+                if (pad == 0) return true;
+                if ((pad & 3) >= 2) return fail("far pointer landing pad is not a struct or list pointer");
+                int64_t poff = (int64_t)((pad >> 2) & ((1ull << 30) - 1));
+                if (poff & (1ll << 29)) poff -= 1ll << 30;
+                out->seg = tseg;
+                out->word = land + 1 + poff;
+                out->desc = pad;
+                out->null = false;
+                return true;
+            }
             uint64_t pad0, pad1;
             if (!word_at(tseg, land, &pad0) || !word_at(tseg, land + 1, &pad1)) return false;
             if ((pad0 & 3) != 2 || ((pad0 >> 2) & 1)) return fail("bad double-far landing pad");

@@ -17,41 +17,39 @@ from collections import OrderedDict
 from typing import Dict, Iterable, List, Sequence, Tuple
 
 
-def build_id_map(taxonomy_path: str) -> "OrderedDict[str, str]":
-    """tools/build_id_map.py:17-43: GCF and every ';'-separated identifier -> TaxID, first
-    row wins, plus the versionless form of every key that has a '.'.  Header columns GCF /
-    TaxID / Identifiers are located by name (fallback: 0, 1, 2)."""
-    id2tax: "OrderedDict[str, str]" = OrderedDict()
+_ID_ROLES = ("GCF", "TaxID", "Identifiers")
 
-    def emit(k: str, tax: str):
-        if not k:
-            return
-        id2tax.setdefault(k, tax)
-        if "." in k:
-            id2tax.setdefault(k.split(".", 1)[0], tax)
 
+def _taxonomy_rows(taxonomy_path: str):
+    """(TaxID, [identifier tokens]) per usable row of detailed_taxonomy.tsv, with columns
+    found by header name, else by position (tools/build_id_map.py:26-30)."""
     with open(taxonomy_path, "r", encoding="utf-8", errors="ignore", newline="") as f:
-        first = f.readline()
-        if not first:
+        head = f.readline()
+        if not head:
             raise SystemExit("empty taxonomy file")
-        hdr = first.rstrip("\n").split("\t")
-        try:
-            i_gcf, i_tax, i_ids = hdr.index("GCF"), hdr.index("TaxID"), hdr.index("Identifiers")
-        except ValueError:
-            i_gcf, i_tax, i_ids = 0, 1, 2
-        for line in f:
-            if not line.strip():
+        names = head.rstrip("\n").split("\t")
+        col = ({r: names.index(r) for r in _ID_ROLES} if all(r in names for r in _ID_ROLES)
+               else {r: k for k, r in enumerate(_ID_ROLES)})
+        need = max(col["GCF"], col["TaxID"])
+        for raw in f:
+            if not raw.strip():
                 continue
-            row = line.rstrip("\n").split("\t")
-            if len(row) <= max(i_gcf, i_tax):
+            cells = raw.rstrip("\n").split("\t")
+            if len(cells) <= need:
                 continue
-            gcf, tax = row[i_gcf].strip(), row[i_tax].strip()
-            if gcf:
-                emit(gcf, tax)
-            ids = row[i_ids].strip() if len(row) > i_ids else ""
-            if ids:
-                for tok in ids.split(";"):
-                    emit(tok.strip(), tax)
+            extra = cells[col["Identifiers"]] if len(cells) > col["Identifiers"] else ""
+            yield cells[col["TaxID"]].strip(), [cells[col["GCF"]]] + extra.strip().split(";")
+
+
+def build_id_map(taxonomy_path: str) -> "OrderedDict[str, str]":
+    """tools/build_id_map.py:17-43 on the classifier's identifier rule (classify.add_alias):
+    the GCF and every ';'-separated identifier of a row, and their versionless forms, map to
+    the row's TaxID; the first row to name a key keeps it."""
+    from .classify import add_alias
+    id2tax: "OrderedDict[str, str]" = OrderedDict()
+    for tax, tokens in _taxonomy_rows(taxonomy_path):
+        for tok in tokens:
+            add_alias(id2tax, tok, tax)
     return id2tax
 
 

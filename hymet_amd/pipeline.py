@@ -77,6 +77,7 @@ class RunResult:
     n_classified: int                 # rows with a lineage other than Unknown
     n_paf_lines: int                  # this rank's PAF lines
     paf_bytes: Optional[bytes] = None  # this rank's resultados.paf text (with_paf)
+    screen: Optional[list] = None      # per DB, the ScreenResult (shared / median arrays)
 
     @property
     def paf(self) -> Optional[List[str]]:
@@ -285,7 +286,11 @@ class Pipeline:
 
     def _load_dbs(self):
         """S1: each sketch DB file parsed (csrc/msh.cpp), its hashes gathered into pinned
-        memory and uploaded by DMA, and its hash table built in HBM."""
+        memory and uploaded by DMA, and its hash table built in HBM.  The pinned buffers are
+        reused run after run, so the SketchDB.hashes of a path-built Pipeline (and of its
+        RunResult.screen) are valid until the next run.  The previous tables are released
+        before the new ones are built (no second copy of the tables in HBM)."""
+        self.tables, self.dbs = [], []
         t0 = time.perf_counter()
         self.dbs = [read_msh(p, alloc=lambda n, i=i: self._pinned_hashes(i, n).numpy().view(np.uint64)[:n])
                     for i, p in enumerate(self.db_paths)]
@@ -344,6 +349,7 @@ class Pipeline:
 
     def screen_select(self, pool):
         res = scr.screen(self.gpu, pool, self.dbs, self.tables, self.comm)
+        self.last_screen = res
         rows, thr, selections = [], [], []
         for r in res:
             s = sel.sort_gr(sel.sort_unique_k5(r.lines(v_max=0.9)))
@@ -463,7 +469,7 @@ class Pipeline:
         if total_rows < 1:  # fewer than 2 TSV lines: run_hymet_cami.sh:182-206
             tsv = self._fallback(ix, sh)
             n_rows = n_cls = 0
-        return RunResult(selected, rows, thr, tsv, n_rows, n_cls, n_lines, paf_bytes)
+        return RunResult(selected, rows, thr, tsv, n_rows, n_cls, n_lines, paf_bytes, self.last_screen)
 
     def _global_names(self, sh: QueryShard):
         """Rank 0's name pool of the whole input (rows from every rank index into it)."""

@@ -66,7 +66,7 @@ def split_parts(lengths, batch=2e9, mini=50e6):
     return parts
 
 
-def map_paf(ref_names, ref_seqs, queries, part_bases=2e9, mini_batch=50e6, threads=1):
+def map_paf(ref_names, ref_seqs, queries, part_bases=2e9, mini_batch=50e6, threads=1, opt=None):
     """minimap2 -I<part_bases> -d ; minimap2 -x asm10 : PAF lines in minimap2's order.
     threads > 1 maps queries concurrently (the C mapper releases the GIL; its state is
     per call), then emits them in input order like minimap2's ordered output."""
@@ -74,12 +74,13 @@ def map_paf(ref_names, ref_seqs, queries, part_bases=2e9, mini_batch=50e6, threa
     lens = [len(s) for s in ref_seqs]
     parts = split_parts(lens, part_bases, mini_batch)
     out = []
-    opt = None
+    resolved = False
     for p in parts:
         idx = oracle_lib.MmIndex([ref_seqs[i] for i in p], names=[ref_names[i] for i in p])
-        if opt is None:
-            opt = oracle_lib.asm10_opt()
+        if not resolved:
+            opt = opt if opt is not None else oracle_lib.asm10_opt()
             oracle_lib._mm_lib().mmo_opt_update_mid_occ(ctypes.byref(opt), idx.h)
+            resolved = True
 
         def one(q):
             qn, qs = q

@@ -164,3 +164,72 @@ def c2_contigs(seed=1):
             st = int(rng.integers(0, len(synth) - L)) if L < len(synth) else 0
             out.append((qn, synth[st:st + L]))
     return out
+
+
+def expected_secondaries(q_entry):
+    """The fixture's secondary lines of one re-cut query that the re-cut can reproduce: on a
+    shipped target and lying (>= 90 % of their query span) inside the query interval of the
+    primary line the query was re-cut from.  Returns {(target, strand)}."""
+    seqs = seq_map()
+    qn, _, f = q_entry
+    fqs, fqe = int(f[2]), int(f[3])
+    out = set()
+    for p in _fixture_by_query().get(qn, ()):
+        if p[12] != "tp:A:S" or p[5] not in seqs:
+            continue
+        qs, qe = int(p[2]), int(p[3])
+        if max(0, min(qe, fqe) - max(qs, fqs)) >= 0.9 * max(1, qe - qs):
+            out.add((p[5], p[4]))
+    return out
+
+
+@lru_cache(maxsize=1)
+def _fixture_by_query():
+    by = {}
+    for p in fixture_paf():
+        by.setdefault(p[0], []).append(p)
+    return by
+
+
+def secondary_agreement(queries, paf_lines, relaxed_lines=None):
+    """Secondary (tp:A:S) lines against the real minimap2 fixture, per re-cut query, as
+    (target, strand) sets.  recall: the fixture's in-interval secondaries
+    (expected_secondaries) that we also report; precision: our secondaries whose (target,
+    strand) the fixture lists for that query (any line type).  relaxed_lines: the same
+    queries mapped with pri_ratio = 0 and best_n = 1000; a miss that appears there was
+    dropped by mm_select_sub's pri_ratio test (the re-cut query is the primary target's own
+    sequence, so its primary scores higher than the real contig's did) -- `explained`."""
+    by = _fixture_by_query()
+
+    def sets(lines):
+        d = {}
+        for l in lines:
+            p = l.split("\t")
+            if p[12] == "tp:A:S":
+                d.setdefault(p[0], set()).add((p[5], p[4]))
+        return d
+
+    ours = sets(paf_lines)
+    relaxed = sets(relaxed_lines) if relaxed_lines is not None else {}
+    relaxed_all = {}
+    for l in relaxed_lines or ():
+        p = l.split("\t")
+        relaxed_all.setdefault(p[0], set()).add((p[5], p[4]))
+    exp_n = rec = got_n = prec = explained = 0
+    misses, extras = [], []
+    for entry in queries:
+        qn = entry[0]
+        exp = expected_secondaries(entry)
+        got = ours.get(qn, set())
+        listed = {(p[5], p[4]) for p in by.get(qn, ())}
+        exp_n += len(exp)
+        rec += len(exp & got)
+        got_n += len(got)
+        prec += len(got & listed)
+        for e in sorted(exp - got):
+            ok = e in relaxed_all.get(qn, set())
+            explained += ok
+            misses.append((qn, e, "pri_ratio" if ok else "no chain"))
+        extras.extend((qn, e) for e in sorted(got - listed))
+    return {"expected": exp_n, "recalled": rec, "ours": got_n, "ours_listed": prec, "misses_explained": explained,
+            "misses": misses, "extras": extras}

@@ -187,8 +187,33 @@ def old_list():
     return message([s0]), exp
 
 
+def bad_far_loop():
+    """Malformed: the reference list's single-far pointer lands on a far pointer to itself
+    (a cycle a recursive decoder would follow until the stack overflows)."""
+    s0, s1 = Seg(), Seg()
+    r = root_struct(s0, 21, 0, 4, 0, 42)
+    land = s1.alloc(1)
+    s0.w[r + 3 + 1] = far(1, land)
+    s1.w[land] = far(1, land)
+    text(s0, r + 3 + 3, "ACGT")
+    return message([s0, s1])
+
+
+def bad_far_to_far():
+    """Malformed: a single-far landing pad that is a double-far pointer."""
+    s0, s1 = Seg(), Seg()
+    r = root_struct(s0, 21, 0, 4, 0, 42)
+    land = s1.alloc(1)
+    s0.w[r + 3 + 1] = far(1, land)
+    s1.w[land] = far(0, 1, double=True)
+    text(s0, r + 3 + 3, "ACGT")
+    return message([s0, s1])
+
+
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
+    for name, fn in (("bad_far_loop.msh", bad_far_loop), ("bad_far_to_far.msh", bad_far_to_far)):
+        (OUT / name).write_bytes(fn())
     expect = {}
     for name, fn in (("v2_single.msh", v2_single), ("v2_far32.msh", v2_far32), ("old_list.msh", old_list)):
         data, exp = fn()

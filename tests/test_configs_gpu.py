@@ -4,7 +4,8 @@ C4 / C5 in tests/test_configs_large_gpu.py).
 * C1 tiny, main.pl path: 60 contigs cut from three real Zymo chromosomes, legacy
   classifier, no limit step; selected list, PAF and TSV identical to the oracle.
 * C2 Zymo screen: the 1,043 fixture contigs at their exact lengths, re-cut from the real
-  Zymo genomes (tests/_zymo.py), against the 25 real genome sketches + decoys (1e7 hashes).
+  Zymo genomes (tests/_zymo.py), against the 25 real genome sketches + 99,975 decoys (1e8
+  hashes, the sketch1 size of BASELINE.md / SURVEY.md §8(d)).
   Counts, shared, median, set size, screen.tab rows and the mash.sh selection bit-exact vs
   the CPU oracle.
 * C3 CAMI-low: 8 taxa, 147 candidate genomes (bench/results_summary.md:90), 10,000
@@ -88,12 +89,14 @@ def _zymo_db(n_decoys, seed=1):
                [sum(len(s) for _, s in f[2]) for f in files])
 
 
+@pytest.mark.timeout(600)
 def test_config_c2_zymo_screen_real_contigs(gpu):
     """BASELINE.json configs[1] "Zymo mock contigs: MinHash sketch+Jaccard vs sketch1.msh on 1
     MI355X (screen stage only)" (SURVEY.md §8(d) C2): the 1,043 fixture contigs at their
     exact lengths, re-cut from the real genomes at each contig's primary hit
     (tests/_zymo.py; 726 Cryptococcus contigs from a seeded synthetic genome, that FASTA is
-    missing) against the 25 real genome sketches + 9,975 decoys (1e7 hashes)."""
+    missing) against the 25 real genome sketches + 99,975 decoys: H = 1e8 hashes, sketch1's
+    size."""
     from hymet_amd import screen as scr
     from hymet_amd import select as sel
     from hymet_amd.seqio import DevicePool, from_records
@@ -101,8 +104,8 @@ def test_config_c2_zymo_screen_real_contigs(gpu):
     recs = z.c2_contigs()
     assert len(recs) == 1043 and sum(len(s) for _, s in recs) == 53_805_448
     seqs = [s for _, s in recs]
-    db = _zymo_db(9975)
-    assert len(db.hashes) >= 10_000_000
+    db = _zymo_db(99975)
+    assert len(db.hashes) == 100_000_000
     pool = DevicePool(gpu, from_records([(n, "", s) for n, s in recs]), DevicePool.ALPHA_MASH)
     res = scr.screen(gpu, pool, [db])[0]
     sh, md, set_size, nk = oracle_lib.ScreenOracle(db).run(seqs)

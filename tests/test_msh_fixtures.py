@@ -41,6 +41,15 @@ def test_truncated_file_fails_loudly(tmp_path):
         msh.read_msh(tmp_path / "missing.msh")
 
 
+@pytest.mark.parametrize("name", ["bad_far_loop.msh", "bad_far_to_far.msh"])
+def test_far_pointer_landing_pad_must_be_struct_or_list(name):
+    """A single-far pointer's landing pad must be a struct or list pointer: one that is itself
+    far (here: to itself) is rejected with HYMET_E_ARG instead of being followed."""
+    from hymet_amd._lib import HymetError
+    with pytest.raises(HymetError):
+        msh.read_msh(MSH / name)
+
+
 def test_writer_round_trip_native(tmp_path):
     rng = np.random.default_rng(3)
     hl = [np.sort(rng.integers(0, 2 ** 63, int(rng.integers(0, 50))).astype(np.uint64)) for _ in range(300)]

@@ -16,7 +16,17 @@ by the query picked the other strain, which the fixture lists as its secondary) 
 whose first shipped primary is a 64 bp chain (4 minimizers at 3.6 % divergence) that does
 not map on its own.
 
-The GPU path is held to the same bar and must equal this restatement byte for byte
+Secondary lines (tp:A:S; they feed ref_counts, classification_cami.py:206): the fixture
+has 92 (target, strand) secondaries lying inside the re-cut intervals of these queries.
+Measured: 71 of them reported (recall 0.77), and 76 of our 81 secondaries name a (target,
+strand) the fixture lists for that query (precision 0.94).  Every one of the 21 misses is
+reported once mm_select_sub's pri_ratio (0.8) and best_n are relaxed: the re-cut query IS
+the primary target's sequence, so its primary chain scores 1.2-2.5x the real contig's and
+the fixture's secondaries fall under 0.8 x s1.  The 5 extras are repeat copies (IS
+elements shared by E. coli / Shigella / Salmonella strains) on 3 short contigs whose
+re-cut primary likewise scores higher.
+
+The GPU path is held to the same bars and must equal this restatement byte for byte
 (tests/test_zymo_real_gpu.py)."""
 import os
 
@@ -37,6 +47,20 @@ def test_fixture_manifest():
     assert len(c2) == 1043 and sum(len(s) for _, s in c2) == 53_805_448
 
 
+def check_secondaries(s):
+    assert s["expected"] == 92
+    assert s["recalled"] >= 71 and s["misses_explained"] == s["expected"] - s["recalled"]
+    assert s["ours_listed"] >= 76 and s["ours"] - s["ours_listed"] <= 5
+
+
+def relaxed_opt():
+    """asm10 with mm_select_sub's filters off (pri_ratio 0, best_n 1000): the diagnosis run."""
+    from oracle import oracle_lib
+    o = oracle_lib.asm10_opt()
+    o.pri_ratio, o.best_n = 0.0, 1000
+    return o
+
+
 def check_agreement(a):
     assert a["queries"] == 322
     assert a["same_target"] >= 318 and a["same_target"] + a["ties"] >= 321
@@ -53,3 +77,8 @@ def test_oracle_matches_real_minimap2_primaries():
     paf = pipeline_oracle.map_paf([n for n, _ in seqs], [s for _, s in seqs], [(n, s) for n, s, _ in q],
                                   threads=THREADS)
     check_agreement(z.primary_agreement(q, paf))
+    relaxed = pipeline_oracle.map_paf([n for n, _ in seqs], [s for _, s in seqs], [(n, s) for n, s, _ in q],
+                                      threads=THREADS, opt=relaxed_opt())
+    s = z.secondary_agreement(q, paf, relaxed)
+    print({k: v for k, v in s.items() if k not in ("misses", "extras")}, s["misses"], s["extras"])
+    check_secondaries(s)
