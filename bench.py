@@ -160,10 +160,32 @@ def cami_inputs(args, sketch):
     return w, fasta, dbs
 
 
+def zymo_genomes():
+    """One real genome per shipped Zymo species (tests/golden/zymo: the reference's
+    case/truth/zymo_refs genomes, committed as data): the first file of each species, its
+    largest record; the yeast's 16 nuclear chromosomes joined."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _zymo
+    out, seen = [], set()
+    for sp, _f, recs in _zymo.genome_files():
+        if sp in seen:
+            continue
+        seen.add(sp)
+        if sp == "saccharomyces_cerevisiae":
+            out.append((sp, b"".join(s for n, s in recs if n != "NC_001224.1")))  # without the mitochondrion
+        else:
+            out.append((sp, max((s for _, s in recs), key=len)))
+    return out
+
+
 def make_workload(args):
     from hymet_amd import synth
-    return synth.make_cami(np.random.default_rng(1234), n_taxa=args.taxa, per_taxon=args.per_taxon,
-                           contig_gbp=args.contig_gbp, contig_rng=np.random.default_rng(5000))
+    rng = np.random.default_rng(1234)
+    kw = {}
+    if args.workload == "cami-medium-zymo":
+        kw = {"backbones": synth.zymo_backbones(rng, zymo_genomes(), args.taxa), "div": (0.005, 0.02)}
+    return synth.make_cami(rng, n_taxa=args.taxa, per_taxon=args.per_taxon, contig_gbp=args.contig_gbp,
+                           contig_rng=np.random.default_rng(5000), **kw)
 
 
 def build_cami(args, comm, gpu):
@@ -285,6 +307,11 @@ def bench_cami(args, comm, gpu, torch):
         "roofline": roofline_from_prof(prof, workload=args.workload, batch_mbp=args.batch_mbp),
         "path_roofline": path_roofline(prof, args.steps, step, total_bases, total_bases, n_lines, len(ix.parts), comm.world),
     }
+    if comm.world == 1:
+        try:
+            out["config"]["predicted_imbalance"] = shard_balance(gpu, pipe, fasta)
+        except Exception as e:  # informative only
+            out["config"]["predicted_imbalance"] = {"error": repr(e)}
     if comm.rank == 0 and comm.world == 1 and not args.no_cpu:   # the CPU leg runs at N=1 only
         try:
             out["cpu_baseline"] = cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier)
@@ -324,6 +351,30 @@ def cpu_threads_default():
     except ValueError:
         pass
     return max(1, n)
+
+
+def shard_balance(gpu, pipe, fasta, worlds=(2, 4, 8)):
+    """Per-rank mapping work of the N-rank runs predicted from this one-rank run (SURVEY.md
+    §8(e) step 1): each rank maps the contiguous record range FastaIndex.shard(rank, N),
+    balanced by bases; a contig's mapping cost is taken as its bases plus its chained
+    anchors (the cm of its PAF lines, summed: chaining and backtrack work grow with the
+    anchors, not the bases).  Returns max/mean over ranks of both, per N."""
+    import ctypes
+    from hymet_amd.ingest import FastaIndex
+    acc = pipe.acc
+    q, _part, _t = acc.columns()
+    cm = np.zeros(max(len(q), 1), np.int32)
+    gpu.call("hymet_paf_acc_field", acc.h, 9, cm.ctypes.data_as(ctypes.c_void_p))
+    fx = FastaIndex(fasta)
+    anchors = np.bincount(q, weights=cm[:len(q)].astype(np.float64), minlength=fx.n)
+    bases = np.asarray(fx.nbases, np.float64)
+    out = {"model": "contiguous base-balanced shards; cost = chained anchors (sum of cm) per contig"}
+    for n in worlds:
+        cuts = [fx.shard(r, n) for r in range(n)]
+        a = np.array([anchors[r0:r1].sum() for r0, r1 in cuts])
+        b = np.array([bases[r0:r1].sum() for r0, r1 in cuts])
+        out[str(n)] = {"anchors_max_over_mean": float(a.max() / a.mean()), "bases_max_over_mean": float(b.max() / b.mean())}
+    return out
 
 
 def cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier, budget_s=None, must=None, n_random=None):
@@ -549,7 +600,7 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="cami-medium", choices=["cami-medium", "cami-high", "screen"])
+    ap.add_argument("--workload", default="cami-medium", choices=["cami-medium", "cami-medium-zymo", "cami-high", "screen"])
     ap.add_argument("--contig-gbp", type=float, default=1.0)
     ap.add_argument("--taxa", type=int, default=12)
     ap.add_argument("--per-taxon", type=int, default=62)
@@ -587,6 +638,8 @@ def parse_args(argv=None):
         # C4: 60 Mbp batches measured 2327 ms/step vs 2460 (30) and ~2390 (40); scratch 148 GB
         args.batch_mbp = args.batch_mbp or 60.0
         args.workload_name = "CAMI-medium (C4)"
+        if args.workload == "cami-medium-zymo":
+            args.workload_name = "CAMI-medium on Zymo backbones (C4 shape, real sequence composition)"
     return args
 
 

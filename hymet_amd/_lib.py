@@ -35,6 +35,7 @@ _SIGS = {
     "hymet_fasta_compact": (_i32, [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp]),
     "hymet_name_hash": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp]),
     "hymet_sort_pairs_u64": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32]),
+    "hymet_scan_u32": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
     "hymet_msh_open": (_i32, [_c.c_char_p, _c.POINTER(_vp)]),
     "hymet_msh_info_get": (_i32, [_vp, _vp]),
     "hymet_msh_copy": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -63,6 +64,7 @@ _SIGS = {
                                   _c.POINTER(_vp), _c.POINTER(_vp)]),
     "hymet_paf_acc_append": (_i32, [_vp, _vp, _vp, _i64, _i64]),
     "hymet_paf_acc_copy": (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    "hymet_paf_acc_field": (_i32, [_vp, _vp, _i32, _vp]),
     "hymet_mm_map_acc": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
     "hymet_emit_paf": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _c.POINTER(_i64), _vp]),
     "hymet_acc_ref_counts": (_i32, [_vp, _vp, _vp]),

@@ -120,6 +120,12 @@ namespace {
 #ifndef HYMET_CHAIN_HNOP
 #define HYMET_CHAIN_HNOP 1
 #endif
+// Wave-uniform loop state pinned to scalar registers (readfirstlane at the derivation points):
+// branches on it become scalar branches instead of exec-mask bookkeeping (first pass 11.55 ->
+// 11.27 ms, long join 7.27 -> 7.07 ms on the real-anchor dump; VALU -9 % per anchor).
+#ifndef HYMET_CHAIN_UNI
+#define HYMET_CHAIN_UNI 1
+#endif
 #ifndef HYMET_CHAIN_WPE  // waves per SIMD the register allocation targets (0: compiler's choice)
 #define HYMET_CHAIN_WPE 4
 #endif
@@ -432,6 +438,15 @@ struct Ent {
 };
 
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+#if HYMET_CHAIN_UNI
+__device__ __forceinline__ int32_t U(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ double Ud(double v) {
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)), __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+#else
+__device__ __forceinline__ int32_t U(int32_t v) { return v; }
+__device__ __forceinline__ double Ud(double v) { return v; }
+#endif
 __device__ __forceinline__ double rld(double v, int l) {
     return __hiloint2double(rl(__double2hiint(v), l), rl(__double2loint(v), l));
 }
@@ -636,6 +651,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             }
             int32_t dummy = 0;
             wave_argmin(bp, bj, dummy);
+            bp = Ud(bp), bj = U(bj);
         };
         // inner list: ring-deque, logical k at lst[(lh + k) & (kInnerCap - 1)]; ends cached
         int ni = 0, lh = 0;
@@ -898,6 +914,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         // predecessor B is the anchor before the off-chain one -- starts one right away)
         int32_t spec_next = 0, spec_gap = kSpecGap0;
         for (; i < n;) {
+            i = U(i), i0 = U(i0), st = U(st), st_in = U(st_in);
             GCNT(x, 1);
             CCOUNT(23);
             CPROF(7);
@@ -1405,7 +1422,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                                     tp = prio(e.f, e.x, e.y, c), tj = j, ty = e.y;
                                 }
                                 wave_argmin(tp, tj, ty);
-                                t_pr = tp, t_j = tj, t_y = ty;
+                                t_pr = Ud(tp), t_j = U(tj), t_y = U(ty);
                             }
                             i0 = i + nins;
                         }

@@ -104,7 +104,7 @@ int scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, De
 enum : int { kMbScan = 0, kMbGmax = 1, kMbZBig = 2, kMbZBigTotal = 3, kMbFlag = 4, kMbQClass = 8, kMbGroups = 20,
              kMbGClass = 24 };
 // self-clearing device counters (hymet_ctx::dctr): counters at [base, base + n), ticket at base + n
-enum : int { kCtrQClass = 0, kCtrGroups = 16, kCtrGClass = 24 };
+enum : int { kCtrQClass = 0, kCtrGroups = 16, kCtrGClass = 24, kCtrScan = 40, kCtrMaxScan = 41 };
 
 // Called by every thread of every block after the block's last update of cnt[0, n): the last
 // block to arrive stores the totals into the mailbox words mail[0, n) and zeroes the counters

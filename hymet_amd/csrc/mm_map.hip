@@ -2191,6 +2191,16 @@ int hymet_paf_acc_copy(hymet_ctx *ctx, const hymet_paf_acc *acc, int32_t *h_q, i
     return HYMET_OK;
 }
 
+int hymet_paf_acc_field(hymet_ctx *ctx, const hymet_paf_acc *acc, int field, int32_t *h_out) {
+    HY_ARG(ctx && acc && h_out && field >= 0 && field < (int)(sizeof(hymet_mm_reg) / 4), "hymet_paf_acc_field: bad argument");
+    if (acc->n <= 0) return HYMET_OK;
+    HY_HIP(hipSetDevice(ctx->device));
+    const char *src = static_cast<const char *>(acc->regs.p) + 4 * (size_t)field;
+    HY_HIP(hipMemcpy2DAsync(h_out, 4, src, sizeof(hymet_mm_reg), 4, (size_t)acc->n, hipMemcpyDeviceToHost, ctx->stream));
+    HY_HIP(hipStreamSynchronize(ctx->stream));
+    return HYMET_OK;
+}
+
 int hymet_mm_map_acc(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *opt, const uint32_t *d_2b,
                      const uint32_t *d_mask, const int64_t *h_starts, const int64_t *h_lens, const uint32_t *d_name_hash,
                      int32_t n_q, int32_t q_base, int32_t part_id, int32_t t_base, hymet_paf_acc *acc) {

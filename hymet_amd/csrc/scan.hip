@@ -1,8 +1,13 @@
 // Exclusive prefix sum of uint32 counts into int64 offsets -- the scan behind every
 // count-then-write pass of the library (seed and anchor offsets, group starts, region and
-// text offsets).  Reduce-then-scan over tiles of 4096 counts: per-tile sums, one block
-// scanning the tile sums, then every tile re-read and scanned in LDS with its offset.
-// 16 B of HBM traffic per count (4 + 4 read, 8 written), no per-call state to initialise.
+// text offsets).  Reduce-then-scan over tiles of 4096 counts, in two launches: per-tile sums,
+// whose LAST block to finish (told by a ticket, an agent-scope atomic add) scans the tile
+// sums into tile offsets; then every tile re-read and scanned in LDS with its offset.
+// 16 B of HBM traffic per count (4 + 4 read, 8 written), no per-call state to initialise
+// (the ticket is a self-clearing context counter).  There is no one-block middle launch: a
+// one-block kernel behind a full-grid one waited for a free CU slot while the other mapping
+// stream's persistent chaining grid held every CU (round 3: 1,159 such launches, 231 ms of
+// waiting per two-stream step).
 #include "mm_common.hpp"
 
 namespace hymet {
@@ -47,8 +52,68 @@ __device__ __forceinline__ uint64_t block_excl(uint64_t v, uint64_t *ws, uint64_
     return before + inc - v;
 }
 
+// The hand-off of the tile sums to the last block (MI355X_MICROARCH.md, inter-workgroup
+// visibility, first row of the measured sc1 table): lane 0 of every block stores its sum with
+// an sc1 store, waits for it (vmcnt(0)), then adds to the ticket; the block whose add returns
+// nb - 1 reads every sum with sc1 loads.  No fence, no dependence on dispatch order.
+__device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
+    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(int32_t *p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t ld_sc1(const int32_t *p) {
+    return __hip_atomic_load(const_cast<int32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// lane 0 publishes this block's partial; returns true (block-uniform) in the last block
+template <typename T>
+__device__ __forceinline__ bool publish_part(T *part, T v, uint32_t *ticket) {
+    __shared__ bool last;
+    if (threadIdx.x == 0) {
+        st_sc1(part + blockIdx.x, v);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    return last;
+}
+
+// the last block: exclusive scan of the nb tile sums in place (rounds of 1024), part[nb] =
+// total, *mail = total; the ticket is cleared for the next call
+__device__ void scan_parts_last(uint64_t *part, int64_t nb, int64_t *mail, uint32_t *ticket) {
+    __shared__ uint64_t ws[kScanBlock / 64];
+    uint64_t carry = 0;
+    for (int64_t b0 = 0; b0 < nb; b0 += 4 * kScanBlock) {
+        const int64_t b = b0 + 4 * (int64_t)threadIdx.x;
+        uint64_t v[4], s = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            v[j] = b + j < nb ? ld_sc1(part + b + j) : 0;
+            s += v[j];
+        }
+        uint64_t total;
+        uint64_t run = carry + block_excl<kScanBlock / 64>(s, ws, &total);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (b + j < nb) part[b + j] = run;
+            run += v[j];
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0) {
+        part[nb] = carry;
+        if (mail) *mail = (int64_t)carry;
+        atomicExch(ticket, 0u);
+    }
+}
+
 __global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint32_t *__restrict__ in, int64_t n,
-                                                                 uint64_t *__restrict__ part) {
+                                                                 uint64_t *__restrict__ part, uint32_t *ticket,
+                                                                 int64_t *mail) {
     __shared__ uint64_t ws[kScanBlock / 64];
     const int64_t base = (int64_t)blockIdx.x * kScanTile;
     uint64_t s = 0;
@@ -68,26 +133,7 @@ __global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint32_t 
     }
     uint64_t total;
     (void)block_excl<kScanBlock / 64>(s, ws, &total);
-    if (threadIdx.x == 0) part[blockIdx.x] = total;
-}
-
-// one block of 1024: tile sums -> exclusive tile offsets; part[nb] = grand total (and *mail,
-// a mailbox word, when given)
-__global__ __launch_bounds__(1024) void scan_parts_kernel(uint64_t *part, int64_t nb, int64_t *mail) {
-    __shared__ uint64_t ws[16];
-    uint64_t carry = 0;
-    for (int64_t b0 = 0; b0 < nb; b0 += 1024) {
-        const int64_t b = b0 + threadIdx.x;
-        const uint64_t v = b < nb ? part[b] : 0;
-        uint64_t total;
-        const uint64_t ex = block_excl<16>(v, ws, &total);
-        if (b < nb) part[b] = carry + ex;
-        carry += total;
-    }
-    if (threadIdx.x == 0) {
-        part[nb] = carry;
-        if (mail) *mail = (int64_t)carry;
-    }
+    if (publish_part(part, total, ticket)) scan_parts_last(part, gridDim.x, mail, ticket);
 }
 
 __device__ __forceinline__ int pad16(int e) { return e + (e >> 4); }
@@ -161,7 +207,8 @@ __global__ __launch_bounds__(kScanBlock) void scan_down_kernel(const uint32_t *_
 // uint64 -> uint64 variant (packed counters, e.g. two 32-bit counts per word): thread t of a
 // tile owns 16 consecutive entries
 __global__ __launch_bounds__(kScanBlock) void scan_reduce64_kernel(const uint64_t *__restrict__ in, int64_t n,
-                                                                   uint64_t *__restrict__ part) {
+                                                                   uint64_t *__restrict__ part, uint32_t *ticket,
+                                                                   int64_t *mail) {
     __shared__ uint64_t ws[kScanBlock / 64];
     const int64_t b = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
     uint64_t s = 0;
@@ -169,7 +216,7 @@ __global__ __launch_bounds__(kScanBlock) void scan_reduce64_kernel(const uint64_
     for (int j = 0; j < kScanItems; j++) s += b + j < n ? in[b + j] : 0ull;
     uint64_t total;
     (void)block_excl<kScanBlock / 64>(s, ws, &total);
-    if (threadIdx.x == 0) part[blockIdx.x] = total;
+    if (publish_part(part, total, ticket)) scan_parts_last(part, gridDim.x, mail, ticket);
 }
 
 __global__ __launch_bounds__(kScanBlock) void scan_down64_kernel(const uint64_t *__restrict__ in, int64_t n,
@@ -225,7 +272,7 @@ __device__ __forceinline__ int32_t block_excl_max(int32_t v, int32_t *ws, int32_
 }
 
 __global__ __launch_bounds__(kScanBlock) void max_reduce_kernel(const int32_t *__restrict__ in, int64_t n,
-                                                                int32_t *__restrict__ part) {
+                                                                int32_t *__restrict__ part, uint32_t *ticket) {
     __shared__ int32_t ws[kScanBlock / 64];
     const int64_t b = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
     int32_t m = INT32_MIN;
@@ -234,20 +281,28 @@ __global__ __launch_bounds__(kScanBlock) void max_reduce_kernel(const int32_t *_
         if (b + j < n) m = max(m, in[b + j]);
     int32_t all;
     (void)block_excl_max<kScanBlock / 64>(m, ws, &all);
-    if (threadIdx.x == 0) part[blockIdx.x] = all;
-}
-
-__global__ __launch_bounds__(1024) void max_parts_kernel(int32_t *part, int64_t nb) {
-    __shared__ int32_t ws[16];
+    if (!publish_part(part, all, ticket)) return;
+    // last block: exclusive max-scan of the tile maxima in place (rounds of 1024)
+    const int64_t nb = gridDim.x;
     int32_t carry = INT32_MIN;
-    for (int64_t b0 = 0; b0 < nb; b0 += 1024) {
-        const int64_t b = b0 + threadIdx.x;
-        const int32_t v = b < nb ? part[b] : INT32_MIN;
-        int32_t all;
-        const int32_t ex = block_excl_max<16>(v, ws, &all);
-        if (b < nb) part[b] = max(carry, ex);
-        carry = max(carry, all);
+    for (int64_t b0 = 0; b0 < nb; b0 += 4 * kScanBlock) {
+        const int64_t q = b0 + 4 * (int64_t)threadIdx.x;
+        int32_t v[4], mm = INT32_MIN;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            v[j] = q + j < nb ? ld_sc1(part + q + j) : INT32_MIN;
+            mm = max(mm, v[j]);
+        }
+        int32_t blk;
+        int32_t run = max(carry, block_excl_max<kScanBlock / 64>(mm, ws, &blk));
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (q + j < nb) part[q + j] = run;
+            run = max(run, v[j]);
+        }
+        carry = max(carry, blk);
     }
+    if (threadIdx.x == 0) atomicExch(ticket, 0u);
 }
 
 __global__ __launch_bounds__(kScanBlock) void max_down_kernel(const int32_t *__restrict__ in, int64_t n,
@@ -276,10 +331,9 @@ int inclusive_max_scan_i32(hymet_ctx *ctx, const int32_t *in, int32_t *out, int6
     hipStream_t st = ctx->stream;
     const int64_t nb = cdiv(n, kScanTile);
     HY_HIP(part.alloc(4 * (size_t)(nb + 1), st));
-    hipLaunchKernelGGL(max_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<int32_t>());
+    hipLaunchKernelGGL(max_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<int32_t>(),
+                       reinterpret_cast<uint32_t *>(ctx->dctr + kCtrMaxScan));
     HY_CHECK_LAUNCH("max_reduce_kernel");
-    hipLaunchKernelGGL(max_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<int32_t>(), nb);
-    HY_CHECK_LAUNCH("max_parts_kernel");
     hipLaunchKernelGGL(max_down_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<int32_t>(), out);
     HY_CHECK_LAUNCH("max_down_kernel");
     return HYMET_OK;
@@ -290,10 +344,9 @@ int scan_u64(hymet_ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n, DevBu
     hipStream_t st = ctx->stream;
     const int64_t nb = cdiv(n, kScanTile);
     HY_HIP(part.alloc(8 * (size_t)(nb + 1), st));
-    hipLaunchKernelGGL(scan_reduce64_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>());
+    hipLaunchKernelGGL(scan_reduce64_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(),
+                       reinterpret_cast<uint32_t *>(ctx->dctr + kCtrScan), mail);
     HY_CHECK_LAUNCH("scan_reduce64_kernel");
-    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<uint64_t>(), nb, mail);
-    HY_CHECK_LAUNCH("scan_parts_kernel");
     hipLaunchKernelGGL(scan_down64_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(), out);
     HY_CHECK_LAUNCH("scan_down64_kernel");
     return HYMET_OK;
@@ -304,10 +357,9 @@ int scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, De
     hipStream_t st = ctx->stream;
     const int64_t nb = cdiv(n, kScanTile);
     HY_HIP(part.alloc(8 * (size_t)(nb + 1), st));
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>());
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(),
+                       reinterpret_cast<uint32_t *>(ctx->dctr + kCtrScan), mail);
     HY_CHECK_LAUNCH("scan_reduce_kernel");
-    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<uint64_t>(), nb, mail);
-    HY_CHECK_LAUNCH("scan_parts_kernel");
     hipLaunchKernelGGL(scan_down_kernel<int64_t>, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(), out);
     HY_CHECK_LAUNCH("scan_down_kernel");
     return HYMET_OK;
@@ -318,10 +370,9 @@ int scan_u32(hymet_ctx *ctx, const uint32_t *in, uint32_t *out, int64_t n, DevBu
     hipStream_t st = ctx->stream;
     const int64_t nb = cdiv(n, kScanTile);
     HY_HIP(part.alloc(8 * (size_t)(nb + 1), st));
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>());
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(),
+                       reinterpret_cast<uint32_t *>(ctx->dctr + kCtrScan), mail);
     HY_CHECK_LAUNCH("scan_reduce_kernel");
-    hipLaunchKernelGGL(scan_parts_kernel, dim3(1), dim3(1024), 0, st, part.as<uint64_t>(), nb, mail);
-    HY_CHECK_LAUNCH("scan_parts_kernel");
     hipLaunchKernelGGL(scan_down_kernel<uint32_t>, dim3((unsigned)nb), dim3(kScanBlock), 0, st, in, n, part.as<uint64_t>(), out);
     HY_CHECK_LAUNCH("scan_down_kernel");
     return HYMET_OK;
@@ -343,6 +394,24 @@ int exclusive_scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int
 
 // ---- C ABI: the library's radix sort, for tests and callers that sort packed keys
 #include "sort.hpp"
+
+extern "C" int hymet_scan_u32(hymet_ctx *ctx, const uint32_t *d_in, int64_t *d_out, int64_t n, int mode, int64_t *total) {
+    HY_ARG(ctx && (n == 0 || (d_in && d_out)) && (mode == 0 || mode == 1), "hymet_scan_u32: bad argument");
+    HY_HIP(hipSetDevice(ctx->device));
+    using namespace hymet::mm;
+    if (mode == 1) {
+        DevBuf part;
+        const int rc = inclusive_max_scan_i32(ctx, reinterpret_cast<const int32_t *>(d_in), reinterpret_cast<int32_t *>(d_out), n,
+                                              part);
+        if (rc) return rc;
+        HY_HIP(hipStreamSynchronize(ctx->stream));
+        return HYMET_OK;
+    }
+    int64_t t = 0;
+    const int rc = exclusive_scan_u32_i64(ctx, d_in, d_out, n, &t);
+    if (total) *total = t;
+    return rc;
+}
 
 extern "C" int hymet_sort_pairs_u64(hymet_ctx *ctx, uint64_t *d_keys, uint32_t *d_vals, int64_t n, int begin_bit,
                                     int end_bit) {

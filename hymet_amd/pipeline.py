@@ -67,6 +67,30 @@ class IndexSet:
     dev: Dict[str, object] = field(default_factory=dict)   # target name pool / lengths in HBM
 
 
+class HostText:
+    """Text the device wrote, landed by one DMA in a pinned host buffer of the pipeline (no
+    host-side copy into a fresh bytes object, which cost ~80 ms per GB of PAF mostly in page
+    faults).  The buffers alternate between runs; before a buffer is reused, the text still
+    referenced from an earlier result is copied out (copy-on-reuse), so a result stays valid
+    for as long as it is referenced."""
+
+    def __init__(self, buf, n: int):
+        self._buf, self.n, self._bytes = buf, int(n), None
+
+    def view(self) -> memoryview:
+        if self._bytes is not None:
+            return memoryview(self._bytes)
+        return memoryview(self._buf)[:self.n]
+
+    def bytes(self) -> bytes:
+        if self._bytes is None:
+            self._bytes = bytes(memoryview(self._buf)[:self.n])
+            self._buf = None
+        return self._bytes
+
+    detach = bytes   # called by the pipeline before it reuses the buffer
+
+
 @dataclass
 class RunResult:
     selected: List[str]
@@ -76,8 +100,13 @@ class RunResult:
     n_queries: int                    # TSV rows (queries with >= 1 PAF line)
     n_classified: int                 # rows with a lineage other than Unknown
     n_paf_lines: int                  # this rank's PAF lines
-    paf_bytes: Optional[bytes] = None  # this rank's resultados.paf text (with_paf)
+    paf_text: Optional[object] = None  # this rank's resultados.paf text (with_paf): bytes or HostText
     screen: Optional[list] = None      # per DB, the ScreenResult (shared / median arrays)
+
+    @property
+    def paf_bytes(self) -> Optional[bytes]:
+        t = self.paf_text
+        return t.bytes() if isinstance(t, HostText) else t
 
     @property
     def paf(self) -> Optional[List[str]]:
@@ -273,6 +302,8 @@ class Pipeline:
         self.map_gpus = [gpu.fork() for _ in range(self.cfg.map_streams)] if self.cfg.map_streams > 1 else []
         self.map_accs = [PafAcc(g) for g in self.map_gpus]
         self._bufs: Dict[str, object] = {}
+        self._paf_pin = [None, None]          # pinned host buffers of the PAF text, alternating per run
+        self._paf_holders = [None, None]      # weak refs to the HostText living in each
         self._ran = False   # the constructor's loads serve the first run
 
     def _pinned_hashes(self, i, n):
@@ -429,9 +460,40 @@ class Pipeline:
             break
         return TSV_HEADER + self._to_host("tsv_h", out, nb.value)
 
-    def emit_paf(self, ix: IndexSet, sh: QueryShard) -> bytes:
-        """This rank's resultados.paf text (its queries' lines, part-major)."""
-        return emit_paf_bytes(self.gpu, ix, sh, self.acc, self._bufs)
+    def emit_paf(self, ix: IndexSet, sh: QueryShard) -> HostText:
+        """This rank's resultados.paf text (its queries' lines, part-major), written on the
+        device and landed in pinned host memory by one DMA."""
+        gpu, torch = self.gpu, self.gpu.torch
+        n = self.acc.n
+        if n == 0:
+            return HostText(b"", 0)
+        nb = _c.c_int64()
+        cap = 200 * n
+        while True:
+            out = self._dev_buf("paf", cap)
+            rc = gpu.lib.hymet_emit_paf(gpu.ctx, self.acc.h, ptr(sh.qname), ptr(sh.qname_off), ptr(sh.qlen),
+                                        ptr(ix.dev["tname"]), ptr(ix.dev["tname_off"]), ptr(ix.dev["tlen"]), ptr(out), cap,
+                                        _c.byref(nb), None)
+            if rc == -3:
+                cap = nb.value
+                continue
+            check(rc, "hymet_emit_paf")
+            break
+        m = nb.value
+        slot = self._paf_slot = (getattr(self, "_paf_slot", 1) + 1) % 2
+        holder = self._paf_holders[slot]() if self._paf_holders[slot] is not None else None
+        if holder is not None:
+            holder.detach()                       # an earlier result still holds this buffer's text
+        buf = self._paf_pin[slot]
+        if buf is None or buf.numel() < m:
+            buf = self._paf_pin[slot] = None      # release before allocating the larger one
+            buf = self._paf_pin[slot] = torch.empty(int(m * 1.25) + 4096, dtype=torch.uint8, pin_memory=True)
+        gpu.sync()                                # the text was written on the library's stream
+        buf[:m].copy_(out[:m])                    # one D2H DMA into pinned memory (synchronous)
+        t = HostText(buf.numpy(), m)
+        import weakref
+        self._paf_holders[slot] = weakref.ref(t)
+        return t
 
     def _dev_buf(self, key, nbytes):
         return _dev_buf(self.gpu, self._bufs, key, nbytes)
@@ -452,7 +514,7 @@ class Pipeline:
             raise RuntimeError("candidate list empty after applying limit")  # run_hymet_cami.sh:126
         ix = self.index_for(selected)
         n_lines = self.map_all(ix, sh)
-        paf_bytes = self.emit_paf(ix, sh) if with_paf else None
+        paf_text = self.emit_paf(ix, sh) if with_paf else None
         tsv, n_rows, n_cls = b"", 0, 0
         if self.classifier is not None:
             rws, R = self.classify_rows(ix, sh)
@@ -469,7 +531,7 @@ class Pipeline:
         if total_rows < 1:  # fewer than 2 TSV lines: run_hymet_cami.sh:182-206
             tsv = self._fallback(ix, sh)
             n_rows = n_cls = 0
-        return RunResult(selected, rows, thr, tsv, n_rows, n_cls, n_lines, paf_bytes, self.last_screen)
+        return RunResult(selected, rows, thr, tsv, n_rows, n_cls, n_lines, paf_text, self.last_screen)
 
     def _global_names(self, sh: QueryShard):
         """Rank 0's name pool of the whole input (rows from every rank index into it)."""

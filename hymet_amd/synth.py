@@ -10,6 +10,12 @@ lognormal-length pieces of a sample strain of each taxon, either strand.
         sketches of the 744 candidates + random decoy sketches (H ~ 1e8 like sketch1).
     cami-low (C3): 8 taxa, 147 candidates, ~100 Mbp of contigs.
     tiny (C1): 3 taxa, 60 contigs of 5-50 kbp.
+    cami-medium-zymo: C4's shape on real sequence composition (SURVEY.md §8(d) "Genomes"):
+        the taxon backbones are the shipped Zymo genomes (zymo_backbones), each taken to a
+        new species by 5-15 % substitutions; three more taxa are sister species of three of
+        them (within-genus similarity); candidates are 0.5-2 % strains of the sampled one.
+        Real genomes keep their repeats (rRNA operons, IS elements, tandem and
+        low-complexity stretches), which i.i.d. backbones lack.
 """
 from __future__ import annotations
 
@@ -83,17 +89,46 @@ class Workload:
         return "\n".join(lines) + "\n"
 
 
+_CODE = np.full(256, 255, np.uint8)
+for _k, _c in zip(b"ACGTacgt", (0, 1, 2, 3, 0, 1, 2, 3)):
+    _CODE[_k] = _c
+
+
+def to_codes(rng, seq: bytes) -> np.ndarray:
+    """ASCII -> 2-bit codes; anything but ACGT (N runs, IUPAC codes) becomes a random base."""
+    c = _CODE[np.frombuffer(seq, np.uint8)]
+    bad = c == 255
+    if bad.any():
+        c[bad] = rng.integers(0, 4, int(bad.sum()), dtype=np.uint8)
+    return c
+
+
+def zymo_backbones(rng, genomes, n_taxa, sisters_of=(2, 7, 0), species_div=(0.05, 0.15)):
+    """Species backbones from real genomes: genomes = [(species, bytes)], one per species
+    (the taxa after them are sister species of genomes[sisters_of[k]]).  Every backbone is
+    its genome with U[species_div] substitutions (testdataset/mutationGCF.py:4-18), so taxa
+    drawn from one genome differ from each other by roughly twice that."""
+    src = [g for _, g in genomes] + [genomes[k][1] for k in sisters_of]
+    if len(src) < n_taxa:
+        raise ValueError(f"{n_taxa} taxa need {n_taxa} backbone sources, have {len(src)}")
+    return [mutate_codes(rng, to_codes(rng, src[t]), float(rng.uniform(*species_div))) for t in range(n_taxa)]
+
+
 def make_cami(rng, n_taxa=12, per_taxon=62, genome_mbp=(3.0, 5.0), div=(0.005, 0.04), contig_gbp=1.0,
-              max_contigs=None, name="cami-medium", contig_rng=None) -> Workload:
+              max_contigs=None, name="cami-medium", contig_rng=None, backbones=None) -> Workload:
     """contig_rng: separate generator for the contigs (per-rank samples of one community).
-    per_taxon: candidate genomes per taxon (an int, or one count per taxon)."""
+    per_taxon: candidate genomes per taxon (an int, or one count per taxon).
+    backbones: one 2-bit code array per taxon (zymo_backbones) instead of i.i.d. ones."""
     taxa = [f"Species{chr(65 + t)} synthetica" for t in range(n_taxa)]
     per = list(per_taxon) if hasattr(per_taxon, "__len__") else [int(per_taxon)] * n_taxa
     ref_names, ref_taxon, ref_strain, refs = [], [], [], []
     sample = []
     for t in range(n_taxa):
-        L = int(rng.uniform(*genome_mbp) * 1e6)
-        backbone = random_codes(rng, L)
+        if backbones is not None:
+            backbone = backbones[t]
+        else:
+            L = int(rng.uniform(*genome_mbp) * 1e6)
+            backbone = random_codes(rng, L)
         strain = mutate_codes(rng, backbone, 0.01)          # the organism actually sampled
         sample.append(strain)
         for s in range(per[t]):

@@ -115,6 +115,11 @@ int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n
  * anchor-segment orders and the LCA row order; no rocPRIM on the mapping path). */
 int hymet_sort_pairs_u64(hymet_ctx *ctx, uint64_t *d_keys, uint32_t *d_vals, int64_t n, int begin_bit, int end_bit);
 
+/* The library's exclusive scan of n device uint32 counts into n int64 offsets (the scan
+ * behind every count-then-write pass); *total = the sum (host).  mode 1: the running
+ * maximum instead (inclusive, int32 in and out; total unused). */
+int hymet_scan_u32(hymet_ctx *ctx, const uint32_t *d_in, int64_t *d_out, int64_t n, int mode, int64_t *total);
+
 /* ---- Mash sketch databases (.msh) ----
  * Replaces the .msh load inside `mash screen` (scripts/mash.sh:14; the DB files of
  * run_hymet_cami.sh:52,85-97 and main.pl:44-46): the Cap'n Proto MinHash message is mapped
@@ -234,6 +239,9 @@ int hymet_paf_acc_info(const hymet_paf_acc *acc, int64_t *n_lines, void **d_regs
 int hymet_paf_acc_append(hymet_ctx *ctx, hymet_paf_acc *dst, const hymet_paf_acc *src, int64_t begin, int64_t end);
 /* query, part and target index of every line, copied to host arrays of n_lines (synchronous) */
 int hymet_paf_acc_copy(hymet_ctx *ctx, const hymet_paf_acc *acc, int32_t *h_q, int32_t *h_part, int32_t *h_t);
+/* one int32 field of every line's hymet_mm_reg record (field = word index, e.g. 9 = cnt, the
+ * chain's minimizer count that PAF prints as cm:i), copied to a host array of n_lines */
+int hymet_paf_acc_field(hymet_ctx *ctx, const hymet_paf_acc *acc, int field, int32_t *h_out);
 int hymet_mm_map_acc(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm_opt *opt, const uint32_t *d_2b,
                      const uint32_t *d_mask, const int64_t *h_starts, const int64_t *h_lens, const uint32_t *d_name_hash,
                      int32_t n_q, int32_t q_base, int32_t part_id, int32_t t_base, hymet_paf_acc *acc);

@@ -33,3 +33,27 @@ def test_radix_sort_matches_stable_argsort(gpu, n, begin, end, distinct):
     order = np.argsort(sub, kind="stable")
     np.testing.assert_array_equal(dv.cpu().numpy().view(np.uint32), order.astype(np.uint32))
     np.testing.assert_array_equal(dk.cpu().numpy().view(np.uint64), keys[order])
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4096, 4097, 1_000_000, 4096 * 1024 + 7, 12_000_000])
+def test_scan_exclusive_sum_and_running_max(gpu, n):
+    """The library's two-launch scan (tile sums whose last block scans them, then the tile
+    pass): every tile-count boundary, including more than 1024 tiles (several rounds in the
+    last block), against numpy; then the running-maximum variant."""
+    torch = gpu.torch
+    rng = np.random.default_rng(n)
+    cnt = rng.integers(0, 3000, n, dtype=np.uint32)
+    d_in = torch.from_numpy(cnt.view(np.int32)).to(gpu.dev)
+    d_out = torch.empty(n, dtype=torch.int64, device=gpu.dev)
+    tot = ctypes.c_int64()
+    for _ in range(2):   # twice: the ticket must be clear again after a call
+        gpu.call("hymet_scan_u32", ctypes.c_void_p(d_in.data_ptr()), ctypes.c_void_p(d_out.data_ptr()), n, 0, ctypes.byref(tot))
+        want = np.zeros(n, np.int64)
+        np.cumsum(cnt[:-1], out=want[1:])
+        np.testing.assert_array_equal(d_out.cpu().numpy(), want)
+        assert tot.value == int(cnt.sum(dtype=np.int64))
+    v = rng.integers(-2 ** 31, 2 ** 31 - 1, n, dtype=np.int64).astype(np.int32)
+    d_v = torch.from_numpy(v).to(gpu.dev)
+    d_m = torch.empty(n, dtype=torch.int32, device=gpu.dev)
+    gpu.call("hymet_scan_u32", ctypes.c_void_p(d_v.data_ptr()), ctypes.c_void_p(d_m.data_ptr()), n, 1, None)
+    np.testing.assert_array_equal(d_m.cpu().numpy(), np.maximum.accumulate(v))
