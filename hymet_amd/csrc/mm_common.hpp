@@ -101,10 +101,10 @@ int scan_u32_i64(hymet_ctx *ctx, const uint32_t *in, int64_t *out, int64_t n, De
 // exclusive scan of n uint64 values (asynchronous; part ends with the total at ceil(n / 4096))
 // mailbox words (hymet_ctx::mbox_h) by use; each is read right after the sync that follows
 // the kernel storing it, so uses that never overlap may share a word
-enum : int { kMbScan = 0, kMbGmax = 1, kMbZBig = 2, kMbZBigTotal = 3, kMbFlag = 4, kMbQClass = 8, kMbGroups = 20,
-             kMbGClass = 24 };
+enum : int { kMbScan = 0, kMbGmax = 1, kMbZBig = 2, kMbZBigTotal = 3, kMbFlag = 4, kMbRegBig = 5, kMbRegBig2 = 6, kMbQClass = 8,
+             kMbGroups = 20, kMbGClass = 24 };
 // self-clearing device counters (hymet_ctx::dctr): counters at [base, base + n), ticket at base + n
-enum : int { kCtrQClass = 0, kCtrGroups = 16, kCtrGClass = 24, kCtrScan = 40, kCtrMaxScan = 41 };
+enum : int { kCtrQClass = 0, kCtrGroups = 16, kCtrGClass = 24, kCtrScan = 40, kCtrMaxScan = 41, kCtrRegBig = 42, kCtrRegBig2 = 44 };
 
 // Called by every thread of every block after the block's last update of cnt[0, n): the last
 // block to arrive stores the totals into the mailbox words mail[0, n) and zeroes the counters

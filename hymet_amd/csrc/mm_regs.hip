@@ -13,6 +13,9 @@
 // chain range.  Float/double arithmetic is written in the order of hit.c (-ffp-contract=off).
 #include "mm_common.hpp"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace hymet {
 namespace mm {
 namespace {
@@ -274,9 +277,24 @@ __global__ __launch_bounds__(64) void query_sumk_kernel(const uint64_t *mini_pos
     }
 }
 
-__global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= P.n_q) return;
+// Queries of more than kRegWave chains take regions_wave_kernel (one wave each); the thread
+// kernel leaves them.  Real genomes make such queries common: a contig that carries a
+// repeat (an IS element, an rRNA operon) hits every copy in every strain, hundreds to
+// thousands of chains, and one thread walking them through global memory took ~0.9 s per
+// step on the Zymo-backbone workload.
+constexpr int kRegWave = 48;
+constexpr int kRegLds = 2048;   // the wave kernel holds a query's regions in LDS up to this many
+constexpr int kRegSmall = 256;  // queries of up to this many chains run in the small-LDS instance
+template <int CAP>
+constexpr size_t reg_wave_lds() { return (size_t)CAP * (16 + 16 + 4 * 3 + 8); }
+
+__device__ __forceinline__ bool wave_query(const RegParams &P, int q, int n, int32_t qlen) {
+    return n > kRegWave && qlen != 0 && !(P.skip_q && P.skip_q[q]);
+}
+
+// the per-query steps, sequential: one thread per query (and the wave kernel's fallback for
+// queries of more than kRegLds chains)
+__device__ void regions_seq(const RegParams &P, int q) {
     const int64_t c0 = P.qc[q], c1 = P.qc[q + 1];
     int n = (int)(c1 - c0);
     const int32_t qlen = (int32_t)P.qlen[q];
@@ -468,6 +486,442 @@ __global__ __launch_bounds__(64) void regions_kernel(RegParams P) {
     P.n_regs[q] = n;
 }
 
+__device__ __forceinline__ void list_append(bool pred, int q, int32_t *list, int32_t *cnt) {  // one atomic per wave
+    const uint64_t m = __ballot(pred);
+    if (!m) return;
+    const int lane = threadIdx.x & 63, leader = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(cnt, __popcll(m));
+    base = __shfl(base, leader, 64);
+    if (pred) list[base + __popcll(m & ((1ull << lane) - 1))] = q;
+}
+
+// one thread per query; the queries of many chains are listed for regions_wave_kernel: up to
+// kRegSmall chains (most of them; small LDS, many waves per CU) and beyond
+__global__ __launch_bounds__(64) void regions_kernel(RegParams P, int32_t *big, int32_t *n_big, int32_t *big2,
+                                                     int32_t *n_big2) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = q < P.n_q ? (int)(P.qc[q + 1] - P.qc[q]) : 0;
+    const bool wq = q < P.n_q && wave_query(P, q, n, (int32_t)P.qlen[q]);
+    list_append(wq && n <= kRegSmall, q, big, n_big);
+    list_append(wq && n > kRegSmall, q, big2, n_big2);
+    if (q >= P.n_q || wq) return;
+    regions_seq(P, q);
+}
+
+// ---- one wave per query of many chains: the same steps, lane-parallel where the sequential
+// code's decisions allow it, sequential (but on LDS-resident data) where they do not.
+__device__ __forceinline__ void wsync() { __syncthreads(); }  // one-wave blocks: LDS order + convergence
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return (uint64_t)(uint32_t)hi << 32 | (uint32_t)lo;
+}
+// ascending sort of one value per lane across the wave (bitonic network)
+__device__ __forceinline__ uint64_t wave_sort_u64(uint64_t v) {
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int s = 2; s <= 64; s <<= 1)
+#pragma unroll
+        for (int d = s >> 1; d > 0; d >>= 1) {
+            const uint64_t o = shfl_xor64(v, d);
+            const bool up = (lane & s) == 0, low = (lane & d) == 0;
+            v = (low == up) ? (o < v ? o : v) : (o > v ? o : v);
+        }
+    return v;
+}
+__device__ __forceinline__ int wave_excl_max(int v, int init) {  // max over lanes < l (init before lane 0)
+    const int lane = threadIdx.x;
+    int x = __shfl_up(v, 1, 64);
+    if (lane == 0) x = init;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(x, d, 64);
+        if (lane >= d) x = max(x, o);
+    }
+    return x;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+__device__ __forceinline__ int64_t wave_sum_l(int64_t v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+// descending bitonic sort of m (a power of two) 128-bit keys in LDS
+__device__ void lds_sort_desc(U128 *a, int m) {
+    for (int s = 2; s <= m; s <<= 1)
+        for (int d = s >> 1; d > 0; d >>= 1) {
+            for (int t = threadIdx.x; t < (m >> 1); t += 64) {
+                const int i = (t / d) * 2 * d + (t % d), j = i + d;
+                const U128 x = a[i], y = a[j];
+                if (((i & s) == 0) ? lt128(x, y) : lt128(y, x)) a[i] = y, a[j] = x;
+            }
+            wsync();
+        }
+}
+__device__ void lds_sort_asc_u64(uint64_t *a, int m) {
+    for (int s = 2; s <= m; s <<= 1)
+        for (int d = s >> 1; d > 0; d >>= 1) {
+            for (int t = threadIdx.x; t < (m >> 1); t += 64) {
+                const int i = (t / d) * 2 * d + (t % d), j = i + d;
+                const uint64_t x = a[i], y = a[j];
+                if (((i & s) == 0) ? y < x : x < y) a[i] = y, a[j] = x;
+            }
+            wsync();
+        }
+}
+
+template <int CAP>
+__device__ void regions_wave(const RegParams &P, int q, unsigned char *rsm);
+
+// a persistent grid over the listed queries; the last block clears the list counter
+template <int CAP>
+__global__ __launch_bounds__(64) void regions_wave_kernel(RegParams P, const int32_t *big, int32_t *n_big, int64_t *mail) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
+    const int nb = __builtin_amdgcn_readfirstlane(*n_big);
+    for (int w = blockIdx.x; w < nb; w += gridDim.x) {
+        regions_wave<CAP>(P, __builtin_amdgcn_readfirstlane(big[w]), rsm);
+        wsync();
+    }
+    publish_counters(n_big, 1, mail);
+}
+
+template <int CAP>
+__device__ void regions_wave(const RegParams &P, int q, unsigned char *rsm) {
+    const int lane = threadIdx.x;
+    const int64_t c0 = P.qc[q], c1 = P.qc[q + 1];
+    int n = (int)(c1 - c0);
+    const int32_t qlen = (int32_t)P.qlen[q];
+    if (n > CAP) {
+        if (lane == 0) regions_seq(P, q);
+        return;
+    }
+    // LDS: slot[i] = (qs, qe, score, cnt) of region i (first the sort keys, in place), aux[i] =
+    // (rid | rev << 31, rs, re, -), then per-step arrays
+    U128 *zs = reinterpret_cast<U128 *>(rsm);
+    int4 *slot = reinterpret_cast<int4 *>(rsm);
+    int4 *aux = reinterpret_cast<int4 *>(rsm + 16 * CAP);
+    int32_t *wl = reinterpret_cast<int32_t *>(rsm + 32 * CAP);  // primaries (set_parent), kept list (select_sub)
+    int32_t *psub = wl + CAP, *pns = psub + CAP;                 // per primary: subsc, n_sub (set_parent)
+    uint64_t *covb = reinterpret_cast<uint64_t *>(pns + CAP);    // overlapping intervals (set_parent)
+    const int64_t b0 = P.qb[q];
+    hymet_mm_reg *r = P.regs + c0;
+    uint32_t hash = P.name_hash[q];
+    hash ^= wang32((uint32_t)qlen) + wang32((uint32_t)P.seed);
+    hash = wang32(hash);
+    // ---- mm_gen_regs: keys (score<<32 | cnt) ^ hash, sorted descending (keys are distinct:
+    // y holds the chain's anchor offset), padded to a power of two with (0, 0)
+    int m = 64;
+    while (m < n) m <<= 1;
+    for (int i = lane; i < m; i += 64) {
+        U128 zz{0, 0};
+        if (i < n) {
+            const int64_t k = P.cboff[c0 + i] - b0;
+            const uint64_t u = P.cu[c0 + i];
+            const int64_t a = P.ids[P.cfirst[c0 + i] + (int32_t)u - 1];
+            const uint32_t h = (uint32_t)hash64((hash64(P.ax[a]) + hash64(P.ay[a])) ^ hash);
+            zz.x = u ^ h;
+            zz.y = (uint64_t)k << 32 | (uint32_t)(int32_t)u;
+        }
+        zs[i] = zz;
+    }
+    wsync();
+    lds_sort_desc(zs, m);
+    for (int i = lane; i < n; i += 64) {
+        const U128 zi = zs[i];
+        hymet_mm_reg ri;
+        ri.id = i;
+        ri.parent = -1;
+        ri.score = (int32_t)(zi.x >> 32);
+        ri.hash = (uint32_t)zi.x;
+        ri.cnt = (int32_t)zi.y;
+        ri.as = (int32_t)(zi.y >> 32);
+        ri.div = -1.0f;
+        ri.subsc = 0;
+        ri.n_sub = 0;
+        ri.strand_retained = 0;
+        ri.mapq = 0;
+        ri.pad = 0;
+        const int64_t c = chain_of(P.cboff, c0, c1, b0 + ri.as);
+        const int64_t a0 = P.ids[P.cfirst[c] + ri.cnt - 1], a1 = P.ids[P.cfirst[c]];
+        set_coor(&ri, qlen, P.ax[a0], P.ay[a0], P.ax[a1], P.ay[a1], P.c_mlen[c], P.c_blen[c]);
+        r[i] = ri;
+        slot[i] = make_int4(ri.qs, ri.qe, ri.score, ri.cnt);  // this lane's own sort slot
+        aux[i] = make_int4(ri.rid | ri.rev << 31, ri.rs, ri.re, 0);
+    }
+    wsync();
+    // ---- mm_set_parent: sequential over regions; each region is tested against all primaries
+    // so far lane-parallel (the sequential loop's first match = the lowest matching lane)
+    {
+        int k = 1;
+        if (lane == 0) wl[0] = 0, psub[0] = 0, pns[0] = 0, r[0].parent = 0;
+        wsync();
+        for (int i = 1; i < n; ++i) {
+            const int4 me = slot[i];
+            const int si = me.x, ei = me.y, sci = me.z, cnti = me.w;
+            // overlapping primaries, clipped, gathered in primary order
+            int ncov = 0;
+            for (int jb = 0; jb < k; jb += 64) {
+                const int j = jb + lane;
+                int sj = 0, ej = 0;
+                if (j < k) {
+                    const int4 o = slot[wl[j]];
+                    sj = o.x, ej = o.y;
+                }
+                const bool ov = j < k && !(ej <= si || sj >= ei);
+                const uint64_t mov = __ballot(ov);
+                if (ov) covb[ncov + __popcll(mov & ((1ull << lane) - 1))] = (uint64_t)(uint32_t)max(sj, si) << 32 | (uint32_t)min(ej, ei);
+                ncov += __popcll(mov);
+            }
+            wsync();
+            int jfound = -1;
+            if (ncov > 0) {
+                // uncovered length of [si, ei]: the sorted sweep x = running max of ends
+                int uncov = 0, carry = si;
+                if (ncov == 1) {  // one overlapping primary: its clipped interval is the union
+                    const uint64_t kv = covb[0];
+                    const int s_ = (int)(kv >> 32), e_ = (int)(uint32_t)kv;
+                    uncov = s_ > si ? s_ - si : 0;
+                    carry = max(si, e_);
+                } else if (ncov <= 64) {
+                    const uint64_t kv = wave_sort_u64(lane < ncov ? covb[lane] : ~0ull);
+                    const int s_ = (int)(kv >> 32), e_ = lane < ncov ? (int)(uint32_t)kv : INT32_MIN;
+                    const int x = wave_excl_max(e_, si);
+                    uncov = wave_sum_i(lane < ncov && s_ > x ? s_ - x : 0);
+                    carry = max(si, wave_max_i(e_));
+                } else {
+                    int mm = 64;
+                    while (mm < ncov) mm <<= 1;
+                    for (int t = ncov + lane; t < mm; t += 64) covb[t] = ~0ull;
+                    wsync();
+                    lds_sort_asc_u64(covb, mm);
+                    for (int tb = 0; tb < ncov; tb += 64) {
+                        const int t = tb + lane;
+                        const uint64_t kv = t < ncov ? covb[t] : ~0ull;
+                        const int s_ = (int)(kv >> 32), e_ = t < ncov ? (int)(uint32_t)kv : INT32_MIN;
+                        const int x = wave_excl_max(e_, carry);
+                        uncov += wave_sum_i(t < ncov && s_ > x ? s_ - x : 0);
+                        carry = max(carry, wave_max_i(e_));
+                    }
+                }
+                if (ei > carry) uncov += ei - carry;
+                // the first primary (in order) that region i is a secondary of
+                for (int jb = 0; jb < k && jfound < 0; jb += 64) {
+                    const int j = jb + lane;
+                    bool hit = false;
+                    if (j < k) {
+                        const int4 o = slot[wl[j]];
+                        const int sj = o.x, ej = o.y;
+                        if (!(ej <= si || sj >= ei)) {
+                            const int mn = ej - sj < ei - si ? ej - sj : ei - si;
+                            const int mx = ej - sj > ei - si ? ej - sj : ei - si;
+                            const int ol = si < sj ? (ei < sj ? 0 : ei < ej ? ei - sj : ej - sj)
+                                                   : (ej < si ? 0 : ej < ei ? ej - si : ei - si);
+                            hit = __fsub_rn(__fdiv_rn((float)ol, (float)mn), __fdiv_rn((float)uncov, (float)mx)) > P.mask_level &&
+                                  uncov <= P.mask_len;
+                        }
+                    }
+                    const uint64_t mh = __ballot(hit);
+                    if (mh) jfound = jb + __ffsll((unsigned long long)mh) - 1;
+                }
+            }
+            if (jfound >= 0) {
+                const int p = wl[jfound];
+                if (lane == 0) {
+                    r[i].parent = p;
+                    psub[jfound] = psub[jfound] > sci ? psub[jfound] : sci;
+                    if (cnti >= slot[p].w) ++pns[jfound];
+                }
+            } else {
+                if (lane == 0) wl[k] = i, psub[k] = 0, pns[k] = 0, r[i].parent = i;
+                ++k;
+            }
+            wsync();
+        }
+        for (int j = lane; j < k; j += 64) {
+            r[wl[j]].subsc = psub[j];
+            r[wl[j]].n_sub = pns[j];
+        }
+    }
+    __threadfence_block();
+    wsync();
+    // ---- mm_select_sub (check_strand = 1) + mm_sync_regs.  The sequential loop compacts in
+    // place and reads r[p] afterwards, so a parent position already overwritten by a kept
+    // region holds THAT region: position p holds the p-th kept region once more than p are
+    // kept.  Decisions run in order (lane by lane inside each 64-region chunk), on the
+    // original records held in LDS; the compaction is applied afterwards.
+    int nk = 0;
+    {
+        const int min_diff = P.k * 2;
+        const int min_strand_sc = (int)(P.max_gap * 0.8);
+        int n_2nd = 0;
+        int32_t *kept = wl;                 // kept[o] = original index of output position o
+        uint64_t *sflag = covb;             // strand_retained, one bit per original index
+        for (int t = lane; t < (n + 63) / 64; t += 64) sflag[t] = 0;
+        wsync();
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + lane;
+            const int pl = i < n ? r[i].parent : 0;
+            uint64_t keepm = 0, strm = 0;
+            const int cnt_chunk = min(64, n - base);
+            for (int l = 0; l < cnt_chunk; ++l) {
+                const int ii = base + l, p = __builtin_amdgcn_readlane(pl, l);
+                bool keep = false, str = false;
+                if (p == ii) {
+                    keep = true;
+                } else {
+                    const int src = nk > p ? kept[p] : p;  // what position p holds by now
+                    const int4 mi = slot[ii], xi = aux[ii], mp = slot[src], xp = aux[src];
+                    if (((float)mi.z >= __fmul_rn((float)mp.z, P.pri_ratio) || mi.z + min_diff >= mp.z) && n_2nd < P.best_n) {
+                        if (!(mi.x == mp.x && mi.y == mp.y && (xi.x & 0x7fffffff) == (xp.x & 0x7fffffff) && xi.y == xp.y &&
+                              xi.z == xp.z))
+                            keep = true, ++n_2nd;
+                    } else if (n_2nd < P.best_n && mi.z > min_strand_sc && ((uint32_t)xi.x >> 31) != ((uint32_t)xp.x >> 31)) {
+                        keep = str = true, ++n_2nd;
+                    }
+                }
+                if (keep) {
+                    if (lane == 0) kept[nk] = ii;
+                    keepm |= 1ull << l;
+                    ++nk;
+                }
+                if (str) strm |= 1ull << l;
+                wsync();
+            }
+            if (lane == 0) sflag[base >> 6] = strm;
+            wsync();
+        }
+        // compaction (output chunks in order: every source index is >= its output position)
+        if (nk != n) {
+            for (int ob = 0; ob < nk; ob += 64) {
+                const int o = ob + lane;
+                hymet_mm_reg v;
+                if (o < nk) {
+                    const int src = kept[o];
+                    v = r[src];
+                    if (sflag[src >> 6] >> (src & 63) & 1) v.strand_retained = 1;
+                }
+                __threadfence_block();
+                wsync();
+                if (o < nk) r[o] = v;
+                __threadfence_block();
+                wsync();
+            }
+            // mm_sync_regs: ids are the original indices; new index of original j = its position
+            int32_t *pos_of = psub;  // n entries
+            for (int j = lane; j < n; j += 64) pos_of[j] = -1;
+            wsync();
+            for (int o = lane; o < nk; o += 64) pos_of[kept[o]] = o;
+            wsync();
+            for (int o = lane; o < nk; o += 64) {
+                const int par = r[o].parent;
+                r[o].id = o;
+                r[o].parent = par >= 0 && pos_of[par] >= 0 ? pos_of[par] : -1;
+            }
+        } else {
+            for (int o = lane; o < n; o += 64)
+                if (sflag[o >> 6] >> (o & 63) & 1) r[o].strand_retained = 1;
+        }
+        n = nk;
+    }
+    __threadfence_block();
+    wsync();
+    // ---- mm_est_err (per region)
+    {
+        const int64_t m0 = P.mp_off[q];
+        const int32_t nm = (int32_t)(P.mp_off[q + 1] - m0);
+        if (nm > 0) {
+            const uint64_t sum_k = P.q_sumk[q];
+            const float avg_k = __fdiv_rn((float)sum_k, (float)nm);
+            for (int i = lane; i < n; i += 64) {
+                hymet_mm_reg *ri = &r[i];
+                float div = -1.0f;
+                if (ri->cnt != 0) {
+                    const int64_t c = chain_of(P.cboff, c0, c1, b0 + ri->as);
+                    const int32_t st = P.c_st[c];
+                    if (st >= 0) {
+                        const int32_t fv = P.c_fv[c] < ri->cnt ? P.c_fv[c] : ri->cnt;
+                        const int32_t n_match = fv;
+                        const int32_t en = fv == ri->cnt ? P.c_last[c] : nm - 1;
+                        const int32_t l_ref = (int32_t)P.ref_len[ri->rid];
+                        int32_t n_tot = en - st + 1;
+                        if ((float)ri->qs > avg_k && (float)ri->rs > avg_k) ++n_tot;
+                        if ((float)(qlen - ri->qe) > avg_k && (float)(l_ref - ri->re) > avg_k) ++n_tot;
+                        div = n_match >= n_tot ? 0.0f : (float)(1.0 - pow((double)n_match / n_tot, 1.0 / (double)avg_k));
+                    }
+                }
+                ri->div = div;
+            }
+        }
+    }
+    __threadfence_block();
+    wsync();
+    // ---- mm_filter_strand_retained: exact in parallel up to the first dropped region (no
+    // position has moved before it); from there the sequential loop (drops are rare)
+    {
+        int first_drop = n;
+        for (int base = 0; base < n && first_drop == n; base += 64) {
+            const int i = base + lane;
+            bool drop = false;
+            if (i < n && r[i].strand_retained) {
+                const int p = r[i].parent;
+                drop = !(r[i].div < __fmul_rn(r[p].div, 5.0f) || r[i].div < 0.01f);
+            }
+            const uint64_t md = __ballot(drop);
+            if (md) first_drop = base + __ffsll((unsigned long long)md) - 1;
+        }
+        if (first_drop < n) {
+            if (lane == 0) {
+                int i, k = first_drop;
+                for (i = first_drop + 1; i < n; ++i) {
+                    const int p = r[i].parent;
+                    if (!r[i].strand_retained || r[i].div < __fmul_rn(r[p].div, 5.0f) || r[i].div < 0.01f) r[k++] = r[i];
+                }
+                psub[0] = k;
+            }
+            __threadfence_block();
+            wsync();
+            n = psub[0];
+        }
+    }
+    __threadfence_block();
+    wsync();
+    // ---- mm_set_mapq (no alignment)
+    {
+        const float q_coef = 40.0f;
+        int64_t sum_sc = 0;
+        for (int i = lane; i < n; i += 64)
+            if (r[i].parent == r[i].id) sum_sc += r[i].score;
+        sum_sc = wave_sum_l(sum_sc);
+        const float uniq_ratio = __fdiv_rn((float)sum_sc, (float)(sum_sc + P.rep_len[q]));
+        for (int i = lane; i < n; i += 64) {
+            hymet_mm_reg *ri = &r[i];
+            if (ri->parent == ri->id) {
+                const float pen_s1 = __fmul_rn(ri->score > 100 ? 1.0f : __fmul_rn(0.01f, (float)ri->score), uniq_ratio);
+                float pen_cm = ri->cnt > 10 ? 1.0f : __fmul_rn(0.1f, (float)ri->cnt);
+                pen_cm = pen_s1 < pen_cm ? pen_s1 : pen_cm;
+                const int subsc = ri->subsc > P.min_chain_score ? ri->subsc : P.min_chain_score;
+                const float x = __fdiv_rn((float)subsc, (float)ri->score);
+                int mapq = (int)__fmul_rn(__fmul_rn(__fmul_rn(pen_cm, q_coef), __fsub_rn(1.0f, x)), logf((float)ri->score));
+                mapq -= (int)__fadd_rn(__fmul_rn(4.343f, logf((float)(ri->n_sub + 1))), .499f);
+                mapq = mapq > 0 ? mapq : 0;
+                ri->mapq = mapq < 60 ? mapq : 60;
+            } else
+                ri->mapq = 0;
+        }
+    }
+    if (lane == 0) P.n_regs[q] = n;
+}
+
 // per-chain stats accumulators: mlen = blen = 0, first-anchor minimum = 0x7f7f7f7f
 __global__ void chain_stats_init_kernel(int32_t *c_mlen, int32_t *c_blen, int32_t *c_fv, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -516,8 +970,44 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
                 tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk.as<uint64_t>(), skip_q};
     ProfScope _ps(ctx, "mm_regions", (double)NC * (8.0 + 8.0 + 4.0 * 5) + (double)n_q * 64.0);  // chain + stats reads, reg writes
-    hipLaunchKernelGGL(regions_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P);
+    static const bool reg_stats = getenv("HYMET_REG_STATS") != nullptr;  // diagnostic: chains per query
+    if (reg_stats) {
+        std::vector<int64_t> hq(n_q + 1);
+        HY_HIP(hipMemcpyAsync(hq.data(), qc, 8 * (size_t)(n_q + 1), hipMemcpyDeviceToHost, st));
+        HY_HIP(hipStreamSynchronize(st));
+        int64_t h[8] = {0}, mx = 0, tot = 0, big_tot = 0;
+        for (int q = 0; q < n_q; q++) {
+            const int64_t c = hq[q + 1] - hq[q];
+            const int b = c <= 48 ? 0 : c <= 256 ? 1 : c <= 1024 ? 2 : c <= 2048 ? 3 : c <= 8192 ? 4 : 5;
+            h[b]++, mx = c > mx ? c : mx, tot += c;
+            if (c > 2048) big_tot += c;
+        }
+        fprintf(stderr, "[regions] n_q %d chains %lld max %lld | <=48 %lld <=256 %lld <=1k %lld <=2k %lld <=8k %lld >8k %lld (chains in >2k: %lld)\n",
+                n_q, (long long)tot, (long long)mx, (long long)h[0], (long long)h[1], (long long)h[2], (long long)h[3],
+                (long long)h[4], (long long)h[5], (long long)big_tot);
+    }
+    DevBuf big, big2;
+    HY_HIP(big.alloc(4 * (size_t)n_q, st));
+    HY_HIP(big2.alloc(4 * (size_t)n_q, st));
+    // self-clearing list counters (each wave kernel's last block clears its own)
+    int32_t *n_big = ctx->dctr + kCtrRegBig, *n_big2 = ctx->dctr + kCtrRegBig2;
+    hipLaunchKernelGGL(regions_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P, big.as<int32_t>(), n_big,
+                       big2.as<int32_t>(), n_big2);
     HY_CHECK_LAUNCH("regions_kernel");
+    // the listed queries of many chains, one wave each, their regions held in LDS: up to
+    // kRegSmall chains with 13 KB of LDS (many waves per CU), the rest with 104 KB (one)
+    static bool lds_ok = false;
+    if (!lds_ok) {
+        HY_HIP(hipFuncSetAttribute((const void *)regions_wave_kernel<kRegLds>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)reg_wave_lds<kRegLds>()));
+        lds_ok = true;
+    }
+    hipLaunchKernelGGL(regions_wave_kernel<kRegSmall>, dim3((unsigned)std::min<int64_t>(n_q, 12 * (int64_t)ctx->n_cu)), dim3(64),
+                       reg_wave_lds<kRegSmall>(), st, P, (const int32_t *)big.as<int32_t>(), n_big, mb_dev(ctx, kMbRegBig));
+    HY_CHECK_LAUNCH("regions_wave_kernel<small>");
+    hipLaunchKernelGGL(regions_wave_kernel<kRegLds>, dim3((unsigned)std::min<int64_t>(n_q, (int64_t)ctx->n_cu)), dim3(64),
+                       reg_wave_lds<kRegLds>(), st, P, (const int32_t *)big2.as<int32_t>(), n_big2, mb_dev(ctx, kMbRegBig2));
+    HY_CHECK_LAUNCH("regions_wave_kernel<large>");
     return HYMET_OK;
 }
 
