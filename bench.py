@@ -46,6 +46,28 @@ SCOPE_KERNEL = {"mm_chain": "chain_groups_kernel<0>", "mm_chain_long": "chain_gr
                 "screen_count": "screen_count_kernel<21>", "mm_anchors": "write_anchor_keys_kernel",
                 "mm_backtrack": "backtrack_groups_kernel"}
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # tools/pmc_summary.py output
+ISSUE_FILE = os.path.join(ROOT, "profiles", "pmc_issue.json")   # tools/sq_summary.py output (SQ counters)
+
+
+def pmc_issue(scope, workload=None, batch_mbp=None):
+    """Instruction-issue roofline of the scope's kernel from the committed SQ counter passes
+    (tools/chain_pmc2.sh, tools/sq_summary.py): the kernel is latency/issue-bound, so beside
+    its HBM fraction the line reports how busy the CU's scalar unit (1 SALU/cycle) and SIMDs
+    (a wave64 VALU op per 2 cycles) are, measured on this workload's real anchors, or None."""
+    try:
+        with open(ISSUE_FILE) as fh:
+            tab = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    w = tab.get(workload or "", {})
+    if batch_mbp is not None and w.get("batch_mbp") != batch_mbp:
+        return None
+    k = w.get("kernels", {}).get(SCOPE_KERNEL.get(scope, ""))
+    if not k:
+        return None
+    return {"bound": "issue", "salu_issue_frac": k["salu_issue_frac"], "valu_issue_frac": k["valu_issue_frac"],
+            "per_64_anchors": {"salu": k["per_64_anchors"]["SQ_INSTS_SALU"], "valu": k["per_64_anchors"]["SQ_INSTS_VALU"]},
+            "model": k["model"], "source": k["source"]}
 
 
 def pmc_traffic(scope, workload=None, batch_mbp=None):
@@ -75,7 +97,8 @@ def roofline_from_prof(prof, prefer=None, workload=None, batch_mbp=None):
     ms, n, b = cand[name]
     achieved = b / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc_traffic(name, workload, batch_mbp), "kernel": name, "kernel_symbol": SCOPE_KERNEL.get(name),
+            "traffic": pmc_traffic(name, workload, batch_mbp), "issue": pmc_issue(name, workload, batch_mbp),
+            "kernel": name, "kernel_symbol": SCOPE_KERNEL.get(name),
             "kernel_avg_ms": ms / max(n, 1), "launches": n, "alg_bytes_per_launch": b / max(n, 1)}
 
 
@@ -231,7 +254,8 @@ def bench_cami(args, comm, gpu, torch):
     tsv_path = os.path.join(td, "classified_sequences.tsv")
     comm.barrier()
     t0 = time.time()
-    res = pipe.run(fasta)                   # cold: builds the candidate index (cached afterwards)
+    # cold: builds the candidate index (cached afterwards) and the pinned PAF text buffers
+    res = pipe.run(fasta, with_paf=True)
     gpu.sync()
     cold = time.time() - t0
     ix = pipe.index_for(res.selected)

@@ -2009,10 +2009,14 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
 // bounds, the chunk loads, f/p stores), which made groups of 3-16 anchors more than half of
 // the kernel's wave time on C4 anchors.  Here 64 such groups run side by side, each lane
 // replaying mg_lchain_rmq (lchain.c; oracle/mm_oracle.c chain_group) on its group with the
-// group in registers: the window trees become bit masks and brute-force scans over <= 16
+// group in registers: the window trees become bit masks and brute-force scans over <= 24
 // entries, the inner walk a scan of the (y, idx) order.  Same decisions, same f/p.
+// 24 anchors (225 VGPRs, two waves per SIMD) measured fastest on the real-anchor dumps: C4
+// first pass 11.35 -> 10.7 ms, Zymo-backbone 20.3 -> 19.5 ms (16: 146 VGPRs but the wave
+// kernel single-steps the 17-24-anchor groups at ~2.3 us per anchor; 32: 262 VGPRs, one
+// wave per SIMD, 11.3 / 23.5 ms).
 #ifndef HYMET_CHAIN_SMALL
-#define HYMET_CHAIN_SMALL 16
+#define HYMET_CHAIN_SMALL 24
 #endif
 constexpr int kSmall = HYMET_CHAIN_SMALL;  // <= 32 (window sets are 32-bit masks)
 

@@ -95,6 +95,7 @@ struct RegParams {
     const int32_t *c_mlen, *c_blen, *c_st, *c_last, *c_fv;
     const uint64_t *q_sumk;
     const uint32_t *skip_q;        // queries whose regions come from the long join (nullable)
+    int wave_min;                  // queries of more chains than this take regions_wave_kernel
 };
 
 // (x0, y0): the chain's first anchor, (x1, y1): its last
@@ -283,13 +284,11 @@ __global__ __launch_bounds__(64) void query_sumk_kernel(const uint64_t *mini_pos
 // thousands of chains, and one thread walking them through global memory took ~0.9 s per
 // step on the Zymo-backbone workload.
 constexpr int kRegWave = 48;
-constexpr int kRegLds = 2048;   // the wave kernel holds a query's regions in LDS up to this many
-constexpr int kRegSmall = 256;  // queries of up to this many chains run in the small-LDS instance
-template <int CAP>
-constexpr size_t reg_wave_lds() { return (size_t)CAP * (16 + 16 + 4 * 3 + 8); }
+constexpr int kRegSmall = 256;  // the wave kernel holds a query's regions in LDS up to this many
+constexpr int kRegEntryBytes = 16 + 16 + 4 * 3 + 8;  // slot, aux, wl, psub, pns, covb per entry
 
 __device__ __forceinline__ bool wave_query(const RegParams &P, int q, int n, int32_t qlen) {
-    return n > kRegWave && qlen != 0 && !(P.skip_q && P.skip_q[q]);
+    return n > P.wave_min && qlen != 0 && !(P.skip_q && P.skip_q[q]);
 }
 
 // the per-query steps, sequential: one thread per query (and the wave kernel's fallback for
@@ -496,15 +495,12 @@ __device__ __forceinline__ void list_append(bool pred, int q, int32_t *list, int
     if (pred) list[base + __popcll(m & ((1ull << lane) - 1))] = q;
 }
 
-// one thread per query; the queries of many chains are listed for regions_wave_kernel: up to
-// kRegSmall chains (most of them; small LDS, many waves per CU) and beyond
-__global__ __launch_bounds__(64) void regions_kernel(RegParams P, int32_t *big, int32_t *n_big, int32_t *big2,
-                                                     int32_t *n_big2) {
+// one thread per query; the queries of many chains are listed for regions_wave_kernel
+__global__ __launch_bounds__(64) void regions_kernel(RegParams P, int32_t *big, int32_t *n_big) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = q < P.n_q ? (int)(P.qc[q + 1] - P.qc[q]) : 0;
     const bool wq = q < P.n_q && wave_query(P, q, n, (int32_t)P.qlen[q]);
-    list_append(wq && n <= kRegSmall, q, big, n_big);
-    list_append(wq && n > kRegSmall, q, big2, n_big2);
+    list_append(wq, q, big, n_big);
     if (q >= P.n_q || wq) return;
     regions_seq(P, q);
 }
@@ -580,31 +576,37 @@ __device__ void lds_sort_asc_u64(uint64_t *a, int m) {
         }
 }
 
-template <int CAP>
-__device__ void regions_wave(const RegParams &P, int q, unsigned char *rsm);
+// the per-query work of one wave on a scratch area of cap entries (LDS, or global memory for
+// the queries beyond the LDS capacity; a separate large-LDS launch could not be placed while
+// the other mapping stream's chaining grid held the CUs' LDS)
+__device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned char *rsm, int cap);
 
 // a persistent grid over the listed queries; the last block clears the list counter
-template <int CAP>
-__global__ __launch_bounds__(64) void regions_wave_kernel(RegParams P, const int32_t *big, int32_t *n_big, int64_t *mail) {
+__global__ __launch_bounds__(64) void regions_wave_kernel(RegParams P, const int32_t *big, int32_t *n_big, int64_t *mail,
+                                                          unsigned char *gscratch) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
     const int nb = __builtin_amdgcn_readfirstlane(*n_big);
     for (int w = blockIdx.x; w < nb; w += gridDim.x) {
-        regions_wave<CAP>(P, __builtin_amdgcn_readfirstlane(big[w]), rsm);
+        const int q = __builtin_amdgcn_readfirstlane(big[w]);
+        const int n = (int)(P.qc[q + 1] - P.qc[q]);
+        if (n <= kRegSmall) {
+            regions_wave(P, q, rsm, kRegSmall);
+        } else {
+            int m = 64;
+            while (m < n) m <<= 1;  // < 2n: the query's share of gscratch (104 B per chain) holds it
+            regions_wave(P, q, gscratch + (size_t)P.qc[q] * 2 * kRegEntryBytes, m);
+        }
+        __threadfence_block();
         wsync();
     }
     publish_counters(n_big, 1, mail);
 }
 
-template <int CAP>
-__device__ void regions_wave(const RegParams &P, int q, unsigned char *rsm) {
+__device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned char *rsm, const int CAP) {
     const int lane = threadIdx.x;
     const int64_t c0 = P.qc[q], c1 = P.qc[q + 1];
     int n = (int)(c1 - c0);
     const int32_t qlen = (int32_t)P.qlen[q];
-    if (n > CAP) {
-        if (lane == 0) regions_seq(P, q);
-        return;
-    }
     // LDS: slot[i] = (qs, qe, score, cnt) of region i (first the sort keys, in place), aux[i] =
     // (rid | rev << 31, rs, re, -), then per-step arrays
     U128 *zs = reinterpret_cast<U128 *>(rsm);
@@ -968,7 +970,9 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
     }
     RegParams P{ax, ay, ids, cfirst, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
-                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk.as<uint64_t>(), skip_q};
+                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk.as<uint64_t>(), skip_q, kRegWave};
+    static const int wave_min_env = getenv("HYMET_REG_WAVE") ? atoi(getenv("HYMET_REG_WAVE")) : -1;  // tests / A-B
+    if (wave_min_env >= 0) P.wave_min = wave_min_env;
     ProfScope _ps(ctx, "mm_regions", (double)NC * (8.0 + 8.0 + 4.0 * 5) + (double)n_q * 64.0);  // chain + stats reads, reg writes
     static const bool reg_stats = getenv("HYMET_REG_STATS") != nullptr;  // diagnostic: chains per query
     if (reg_stats) {
@@ -986,28 +990,18 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
                 n_q, (long long)tot, (long long)mx, (long long)h[0], (long long)h[1], (long long)h[2], (long long)h[3],
                 (long long)h[4], (long long)h[5], (long long)big_tot);
     }
-    DevBuf big, big2;
+    DevBuf big, gscr;
     HY_HIP(big.alloc(4 * (size_t)n_q, st));
-    HY_HIP(big2.alloc(4 * (size_t)n_q, st));
-    // self-clearing list counters (each wave kernel's last block clears its own)
-    int32_t *n_big = ctx->dctr + kCtrRegBig, *n_big2 = ctx->dctr + kCtrRegBig2;
-    hipLaunchKernelGGL(regions_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P, big.as<int32_t>(), n_big,
-                       big2.as<int32_t>(), n_big2);
+    HY_HIP(gscr.alloc(2 * (size_t)kRegEntryBytes * (size_t)(NC + 1), st));
+    int32_t *n_big = ctx->dctr + kCtrRegBig;  // self-clearing (regions_wave_kernel's last block)
+    hipLaunchKernelGGL(regions_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P, big.as<int32_t>(), n_big);
     HY_CHECK_LAUNCH("regions_kernel");
-    // the listed queries of many chains, one wave each, their regions held in LDS: up to
-    // kRegSmall chains with 13 KB of LDS (many waves per CU), the rest with 104 KB (one)
-    static bool lds_ok = false;
-    if (!lds_ok) {
-        HY_HIP(hipFuncSetAttribute((const void *)regions_wave_kernel<kRegLds>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)reg_wave_lds<kRegLds>()));
-        lds_ok = true;
-    }
-    hipLaunchKernelGGL(regions_wave_kernel<kRegSmall>, dim3((unsigned)std::min<int64_t>(n_q, 12 * (int64_t)ctx->n_cu)), dim3(64),
-                       reg_wave_lds<kRegSmall>(), st, P, (const int32_t *)big.as<int32_t>(), n_big, mb_dev(ctx, kMbRegBig));
-    HY_CHECK_LAUNCH("regions_wave_kernel<small>");
-    hipLaunchKernelGGL(regions_wave_kernel<kRegLds>, dim3((unsigned)std::min<int64_t>(n_q, (int64_t)ctx->n_cu)), dim3(64),
-                       reg_wave_lds<kRegLds>(), st, P, (const int32_t *)big2.as<int32_t>(), n_big2, mb_dev(ctx, kMbRegBig2));
-    HY_CHECK_LAUNCH("regions_wave_kernel<large>");
+    // the listed queries of many chains, one wave each: regions in 13 KB of LDS (up to
+    // kRegSmall chains), beyond that in a global scratch area
+    hipLaunchKernelGGL(regions_wave_kernel, dim3((unsigned)std::min<int64_t>(n_q, 12 * (int64_t)ctx->n_cu)), dim3(64),
+                       (size_t)kRegSmall * kRegEntryBytes, st, P, (const int32_t *)big.as<int32_t>(), n_big,
+                       mb_dev(ctx, kMbRegBig), gscr.as<unsigned char>());
+    HY_CHECK_LAUNCH("regions_wave_kernel");
     return HYMET_OK;
 }
 

@@ -486,8 +486,17 @@ class Pipeline:
             holder.detach()                       # an earlier result still holds this buffer's text
         buf = self._paf_pin[slot]
         if buf is None or buf.numel() < m:
-            buf = self._paf_pin[slot] = None      # release before allocating the larger one
-            buf = self._paf_pin[slot] = torch.empty(int(m * 1.25) + 4096, dtype=torch.uint8, pin_memory=True)
+            # both slots at once (pinning ~1.5 GB costs ~0.4 s): the first run with the PAF
+            # text pays for both, not the first two
+            for s_ in (slot, 1 - slot):
+                b_ = self._paf_pin[s_]
+                if b_ is None or b_.numel() < m:
+                    h_ = self._paf_holders[s_]() if self._paf_holders[s_] is not None else None
+                    if h_ is not None:
+                        h_.detach()
+                    self._paf_pin[s_] = None      # release before allocating the larger one
+                    self._paf_pin[s_] = torch.empty(int(m * 1.25) + 4096, dtype=torch.uint8, pin_memory=True)
+            buf = self._paf_pin[slot]
         gpu.sync()                                # the text was written on the library's stream
         buf[:m].copy_(out[:m])                    # one D2H DMA into pinned memory (synchronous)
         t = HostText(buf.numpy(), m)
