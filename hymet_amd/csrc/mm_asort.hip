@@ -193,12 +193,12 @@ __global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const
         const int b = r + threadIdx.x;
         uint32_t run = 0;
         if (b < nbins)
-            for (int64_t t = t0; t < t1; t += 8) {  // 8 loads in flight
-                uint32_t v[8];
+            for (int64_t t = t0; t < t1; t += 32) {  // 32 loads in flight: this serial walk down
+                uint32_t v[32];                      // a long query's tiles is the launch's tail
 #pragma unroll
-                for (int j = 0; j < 8; j++) v[j] = t + j < t1 ? H[(t + j) * nbins + b] : 0u;
+                for (int j = 0; j < 32; j++) v[j] = t + j < t1 ? H[(t + j) * nbins + b] : 0u;
 #pragma unroll
-                for (int j = 0; j < 8; j++)
+                for (int j = 0; j < 32; j++)
                     if (t + j < t1) {
                         H[(t + j) * nbins + b] = run;  // exclusive within the bin, across tiles
                         run += v[j];
@@ -214,7 +214,14 @@ __global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const
         }
         const uint32_t base = carry + part[threadIdx.x] - run;
         if (b < nbins && run > 0)
-            for (int64_t t = t0; t < t1; t++) H[t * nbins + b] += base;
+            for (int64_t t = t0; t < t1; t += 32) {
+                uint32_t v[32];
+#pragma unroll
+                for (int j = 0; j < 32; j++) v[j] = t + j < t1 ? H[(t + j) * nbins + b] : 0u;
+#pragma unroll
+                for (int j = 0; j < 32; j++)
+                    if (t + j < t1) H[(t + j) * nbins + b] = v[j] + base;
+            }
         const int slot = wave_append(n_groups, b < nbins && run > 0);
         if (slot >= 0 && slot < cap) groups[slot] = Seg{S.s + base, (int32_t)run, S.q};  // host checks the total
         __syncthreads();

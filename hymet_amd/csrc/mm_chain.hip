@@ -1646,9 +1646,15 @@ constexpr int64_t kBtLong = 128;
 // step) -- most walks are short (an off-path anchor walks into a marked chain after a step
 // or two), so the kernel is throughput-bound, not bound by its longest walk.
 #ifndef HYMET_BT_CHUNKS
-#define HYMET_BT_CHUNKS 1
+#define HYMET_BT_CHUNKS 4
 #endif
 constexpr int kBtChunks = HYMET_BT_CHUNKS;
+// ... so a walk starts with one chunk per window and widens to kBtChunks once it has
+// reloaded kBtWiden times (a long walk down a group's main chain: ~15 reloads per group on
+// C4, one dependent round trip each)
+#ifndef HYMET_BT_WIDEN
+#define HYMET_BT_WIDEN 2
+#endif
 #ifndef HYMET_BT_PROBE
 #define HYMET_BT_PROBE 4
 #endif
@@ -1814,6 +1820,7 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             int64_t whi = -1;  // window: chunk c, lane l holds anchor whi - 64c - l
             int64_t wpc[kBtChunks];
             int32_t wfc[kBtChunks], wtc[kBtChunks];
+            int nch = 1, nrel = 0;  // chunks the window covers now; reloads so far in this walk
 #pragma unroll
             for (int c = 0; c < kBtChunks; c++) wpc[c] = -1, wfc[c] = 0, wtc[c] = 1;
             c_walk++;
@@ -1830,16 +1837,19 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                     if (zf > max_s) max_s = zf, nv = len, zc_nv = zc_len;
                     break;
                 }
-                if (nxt > whi || nxt <= whi - 64 * kBtChunks) {
+                if (nxt > whi || nxt <= whi - 64 * nch) {
                     c_reload++;
                     whi = nxt;
+                    if (++nrel > HYMET_BT_WIDEN) nch = kBtChunks;
 #pragma unroll
                     for (int c = 0; c < kBtChunks; c++) {
-                        const int64_t jj = nxt - 64 * c - lane;
-                        const bool ok = jj >= g0;
-                        wpc[c] = ok ? P.p[jj] : -1;
-                        wfc[c] = ok ? P.f[jj] : 0;
-                        wtc[c] = ok ? ld_l2(P.t + jj) : 1;
+                        if (c < nch) {  // uniform
+                            const int64_t jj = nxt - 64 * c - lane;
+                            const bool ok = jj >= g0;
+                            wpc[c] = ok ? P.p[jj] : -1;
+                            wfc[c] = ok ? P.f[jj] : 0;
+                            wtc[c] = ok ? ld_l2(P.t + jj) : 1;
+                        }
                     }
                 }
                 const int d = (int)(whi - nxt);
