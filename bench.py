@@ -325,6 +325,8 @@ def bench_cami(args, comm, gpu, torch):
         "paf_lines": n_lines,
         "kernel_ms_per_step_rank0": kern_ms,
         "stage_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
+        # algorithmic GB/s of each stage (its ProfScope byte model / its kernel time)
+        "stage_alg_gbps": {k: v[2] / v[0] / 1e6 for k, v in prof.items() if v[0] > 0 and v[2] > 0},
         # host wall time of the per-step input loads (inside ms_per_step): S1 .msh parse and
         # HBM table build, C1-C2 taxonomy + hierarchy load
         "input_load_ms_per_step": {k.replace("_s", "_ms"): v * 1e3 / args.steps for k, v in loads.items()},

@@ -237,17 +237,24 @@ __global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const
 // round of kSub anchors is ranked by bin in LDS (wave-aggregated atomics), its bin counts are
 // scanned, the round is laid out bin by bin in LDS, and written run by run (consecutive lanes,
 // consecutive addresses).
-constexpr int kSub = 3072;  // 68 KB of LDS per block: two blocks per CU
+// LDS per block: 12 B per round anchor + 8 B per bin (sized to the part's bins at launch:
+// 1024 bins and 2048 anchors = 32 KB, five blocks per CU; measured on C4: 3072 anchors in a
+// static 68 KB was 323 ms/step of mm_anchor_gsort, 44 KB dynamic 300, 2048 anchors 288)
+#ifndef HYMET_SCATTER_SUB
+#define HYMET_SCATTER_SUB 2048
+#endif
+constexpr int kSub = HYMET_SCATTER_SUB;
 
 __global__ __launch_bounds__(256) void tile_scatter_kernel(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
                                                            const int64_t *__restrict__ tile_a0, const int32_t *__restrict__ tile_q,
                                                            const int32_t *__restrict__ tile_n, const int64_t *__restrict__ qoff,
                                                            int pb, int nbins, const uint32_t *__restrict__ H,
                                                            uint64_t *__restrict__ okey, uint32_t *__restrict__ oval) {
-    __shared__ uint32_t c[kMaxBins];       // run position of every bin for the next round
-    __shared__ uint32_t lo[kMaxBins];      // round: bin counts, then their exclusive offsets
-    __shared__ uint64_t sk[kSub];
-    __shared__ uint32_t sv[kSub];
+    extern __shared__ uint64_t smem[];
+    uint64_t *sk = smem;                                   // [kSub]
+    uint32_t *sv = reinterpret_cast<uint32_t *>(sk + kSub);  // [kSub]
+    uint32_t *c = sv + kSub;                               // [nbins] run position of every bin for the next round
+    uint32_t *lo = c + nbins;                              // [nbins] round: bin counts, then their exclusive offsets
     __shared__ uint32_t wsum[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t a0 = tile_a0[blockIdx.x];
@@ -624,7 +631,8 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     hipLaunchKernelGGL(query_scan_kernel, dim3((unsigned)nl), dim3(256), 0, st, large, tpos.as<int64_t>(), nbins,
                        H.as<uint32_t>(), groups.as<Seg>(), gcap, ctx->dctr + kCtrGroups, mb_dev(ctx, kMbGroups));
     HY_CHECK_LAUNCH("query_scan_kernel");
-    hipLaunchKernelGGL(tile_scatter_kernel, dim3((unsigned)NT), dim3(256), 0, st, key, val, ta0.as<int64_t>(), tq.as<int32_t>(),
+    HY_ARG(nbins >= 1 && nbins <= kMaxBins, "grouped_anchor_sort: bin count out of range");
+    hipLaunchKernelGGL(tile_scatter_kernel, dim3((unsigned)NT), dim3(256), (size_t)kSub * 12 + (size_t)nbins * 8, st, key, val, ta0.as<int64_t>(), tq.as<int32_t>(),
                        tn.as<int32_t>(), d_qoff, gb, nbins, H.as<uint32_t>(), okey, oval);
     HY_CHECK_LAUNCH("tile_scatter_kernel");
     // 4 groups of the large queries, sorted in place by (rpos, y)

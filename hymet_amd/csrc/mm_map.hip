@@ -646,6 +646,10 @@ __global__ void group_size_kernel(const int64_t *g_start, int32_t G, int min_cnt
 constexpr int kZs = 2048;
 constexpr int kZRuns = 16;
 constexpr int kZLane = 16;
+#ifndef HYMET_Z_DEPTH
+#define HYMET_Z_DEPTH 8
+#endif
+constexpr int kZDepth = HYMET_Z_DEPTH;  // f chunks in flight per wave (zorder_wave_kernel)
 
 struct ZParams {
     const int32_t *f;
@@ -697,34 +701,43 @@ __global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
         int m = 0, K = 0;  // z entries so far, descents so far (wave-uniform)
         uint64_t last = 0;
         const uint64_t below = (1ull << lane) - 1;
-        int32_t fnx = lane < n ? P.f[g0 + lane] : 0;  // next chunk's f, loaded one chunk ahead
-        for (int64_t base = 0; base < n; base += 64) {
-            const int64_t i = base + lane;
-            const bool ok = i < n;
-            const int32_t fv = fnx;
-            fnx = i + 64 < n ? P.f[g0 + i + 64] : 0;
-            const bool z = ok && fv >= P.min_sc;
-            const uint64_t bal = __ballot(z);
-            if (bal == 0) continue;
-            const uint64_t key = (uint64_t)(uint32_t)fv << 32 | (uint32_t)(g0 + i);
-            const uint64_t lower = bal & below;
-            const int pos = m + __popcll(lower);
-            const int prev = lower ? 63 - __clzll((long long)lower) : lane;
-            uint64_t pk = shfl64(key, prev);
-            if (!lower) pk = last;
-            const bool desc = z && pos > 0 && key < pk;
-            const uint64_t dbal = __ballot(desc);
-            if (z) {
-                P.zkey[g0 + pos] = key;
-                P.z_idx[g0 + pos] = (int32_t)(g0 + i);
+        // kZDepth chunks of f loaded together: a group of tens of thousands of anchors is one
+        // wave's serial walk, the launch's tail (one chunk ahead: a round trip per 64 anchors)
+        for (int64_t base0 = 0; base0 < n; base0 += 64 * kZDepth) {
+            int32_t fc[kZDepth];
+#pragma unroll
+            for (int d = 0; d < kZDepth; d++) {
+                const int64_t i = base0 + 64 * d + lane;
+                fc[d] = i < n ? P.f[g0 + i] : 0;
             }
-            if (desc) {
-                const int r = K + 1 + __popcll(dbal & below);
-                if (r < kZRuns) rs[r] = pos;
+#pragma unroll
+            for (int d = 0; d < kZDepth; d++) {
+                const int64_t i = base0 + 64 * d + lane;
+                const bool ok = i < n;
+                const int32_t fv = fc[d];
+                const bool z = ok && fv >= P.min_sc;
+                const uint64_t bal = __ballot(z);
+                if (bal == 0) continue;
+                const uint64_t key = (uint64_t)(uint32_t)fv << 32 | (uint32_t)(g0 + i);
+                const uint64_t lower = bal & below;
+                const int pos = m + __popcll(lower);
+                const int prev = lower ? 63 - __clzll((long long)lower) : lane;
+                uint64_t pk = shfl64(key, prev);
+                if (!lower) pk = last;
+                const bool desc = z && pos > 0 && key < pk;
+                const uint64_t dbal = __ballot(desc);
+                if (z) {
+                    P.zkey[g0 + pos] = key;
+                    P.z_idx[g0 + pos] = (int32_t)(g0 + i);
+                }
+                if (desc) {
+                    const int r = K + 1 + __popcll(dbal & below);
+                    if (r < kZRuns) rs[r] = pos;
+                }
+                K += __popcll(dbal);
+                m += __popcll(bal);
+                last = shfl64(key, 63 - __clzll((long long)bal));
             }
-            K += __popcll(dbal);
-            m += __popcll(bal);
-            last = shfl64(key, 63 - __clzll((long long)bal));
         }
         const int runs = m > 0 ? K + 1 : 0;
         if (lane == 0) {
@@ -1543,7 +1556,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
                    int64_t NB, int64_t NC, int64_t NM, const uint32_t *cq,
-                   const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q);
+                   const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q, uint64_t *sumk, bool sumk_done);
 
 namespace {
 // dense query position -> index among the query's seeded minimizers (mini_pos order), for
@@ -2045,6 +2058,9 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     tr.mark("long join");
     // -------------------------------------------------------------- 8 regions
     // region records stay in HBM: per chain set, records at the set's chain offsets + counts
+    DevBuf sumk;  // per query: sum of its minimizer spans (avg_k), computed by the first call
+    HY_HIP(sumk.alloc(8 * (size_t)(n_q + 1), st));
+    bool sumk_done = false;
     auto run_regions = [&](ChainSet &C, DevBuf &rg, DevBuf &nr, const uint32_t *skip_q) -> int {
         const int64_t NC = C.n_chain;
         DevBuf z, wv, cov, tmp;
@@ -2060,7 +2076,8 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                               d_qlen.as<int64_t>(), d_hash, rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
                               z.p, rg.as<hymet_mm_reg>(), wv.as<int32_t>(), cov.as<uint64_t>(), tmp.as<int32_t>(),
                               nr.as<int32_t>(), C.n_anchor, NC, NM, C.cq.as<uint32_t>(),
-                              pos_tab.as<int32_t>(), d_qbase.as<int64_t>(), skip_q);
+                              pos_tab.as<int32_t>(), d_qbase.as<int64_t>(), skip_q, sumk.as<uint64_t>(),
+                              std::exchange(sumk_done, true));
     };
     DevBuf rg1, nr1, rg2, nr2;
     rc = run_regions(C1, rg1, nr1, CF ? nullptr : flag.as<uint32_t>());

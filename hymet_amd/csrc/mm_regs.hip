@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams 
     }
     const int64_t q = in ? (int64_t)P.cq[c] : 0;
     const bool act = in && !(P.skip_q && P.skip_q[q]);
-    int32_t cnt = 0, j = 0;
+    int32_t cnt = 0, j = 0, qlen = 0, cur = -1;
     int64_t f0 = 0;  // slot of chain-order position 0 in ids
     uint64_t x = 0, y = 0;
     if (act) {
@@ -214,24 +214,28 @@ __global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams 
         f0 = P.cfirst[c] + cnt - 1;
         const int64_t a = P.ids[f0 - j];
         x = P.ax[a], y = P.ay[a];
+        qlen = (int)P.qlen[q];
+        cur = mini_idx_at(P, q, qlen, x, y);
     }
-    // chain-order neighbours from the adjacent lanes (same chain), else loaded
+    // chain-order neighbours (anchor and minimizer index) from the adjacent lanes (same
+    // chain), else loaded
     const int32_t ci = (int32_t)c;
     const int32_t cprev = __shfl_up(ci, 1, 64), cnext = __shfl_down(ci, 1, 64);
     uint64_t xp = __shfl_up(x, 1, 64), yp = __shfl_up(y, 1, 64);
     uint64_t xn = __shfl_down(x, 1, 64), yn = __shfl_down(y, 1, 64);
+    const int32_t cur_p = __shfl_up(cur, 1, 64), cur_n = __shfl_down(cur, 1, 64);
     int dm = 0, db = 0, fv = INT32_MAX;
     if (act) {
         const bool rev = x >> 63;
-        if (j > 0 && (lane == 0 || cprev != ci)) {
+        const bool own_p = lane > 0 && cprev == ci, own_n = lane < 63 && cnext == ci;
+        if (j > 0 && !own_p) {
             const int64_t a = P.ids[f0 - j + 1];
             xp = P.ax[a], yp = P.ay[a];
         }
-        if (rev && j + 1 < cnt && (lane == 63 || cnext != ci)) {
+        if (rev && j + 1 < cnt && !own_n) {
             const int64_t a = P.ids[f0 - j - 1];
             xn = P.ax[a], yn = P.ay[a];
         }
-        const int qlen = (int)P.qlen[q];
         const int32_t span = (int32_t)(y >> 32 & 0xff);
         if (j == 0) {
             dm = db = span;
@@ -242,10 +246,10 @@ __global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams 
             dm = tl > span && ql > span ? span : tl < ql ? tl : ql;
         }
         const int32_t kk = rev ? cnt - 1 - j : j;  // est_err walking order
-        const int32_t cur = mini_idx_at(P, q, qlen, x, y);
         fv = cnt;
         if (kk >= 1) {
-            const int32_t prev = rev ? mini_idx_at(P, q, qlen, xn, yn) : mini_idx_at(P, q, qlen, xp, yp);
+            const int32_t prev = rev ? (own_n ? cur_n : mini_idx_at(P, q, qlen, xn, yn))
+                                     : (own_p ? cur_p : mini_idx_at(P, q, qlen, xp, yp));
             if (cur < 0 || cur <= prev) fv = kk;
         }
         if (kk == 0) P.c_st[c] = cur;
@@ -272,7 +276,14 @@ __global__ __launch_bounds__(64) void query_sumk_kernel(const uint64_t *mini_pos
                                                         unsigned long long *sumk) {
     for (int q = blockIdx.x; q < n_q; q += gridDim.x) {
         unsigned long long sk = 0;
-        for (int64_t m = mp_off[q] + threadIdx.x; m < mp_off[q + 1]; m += 64) sk += mini_pos[m] >> 32 & 0xff;
+        const int64_t m1 = mp_off[q + 1];
+        for (int64_t m = mp_off[q] + threadIdx.x; m < m1; m += 256) {  // 4 loads in flight per lane
+            uint64_t v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = m + 64 * j < m1 ? mini_pos[m + 64 * j] : 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) sk += v[j] >> 32 & 0xff;
+        }
         for (int o = 32; o > 0; o >>= 1) sk += __shfl_xor(sk, o, 64);
         if (threadIdx.x == 0) sumk[q] = sk;
     }
@@ -938,17 +949,16 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
                    int64_t NB, int64_t NC, int64_t NM, const uint32_t *cq,
-                   const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q) {
+                   const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q, uint64_t *sumk, bool sumk_done) {
     if (n_q <= 0) return HYMET_OK;
     hipStream_t st = ctx->stream;
-    DevBuf cst, sumk, blk;
+    DevBuf cst, blk;
     HY_HIP(cst.alloc(4 * 5 * (size_t)(NC + 1), st));
-    HY_HIP(sumk.alloc(8 * (size_t)n_q, st));
     int32_t *c_mlen = cst.as<int32_t>(), *c_blen = c_mlen + (NC + 1), *c_st = c_blen + (NC + 1), *c_last = c_st + (NC + 1),
             *c_fv = c_last + (NC + 1);
     {
-        // chain slot (8) + anchor x, y (16) + two pos_tab reads (8) per chained anchor
-        ProfScope _ps(ctx, "mm_chain_stats", (double)NB * (8.0 + 16.0 + 8.0) + (double)NM * 8.0);
+        // chain slot (8) + anchor x, y (16) + its pos_tab read (4) per chained anchor
+        ProfScope _ps(ctx, "mm_chain_stats", (double)NB * (8.0 + 16.0 + 4.0) + (double)NM * 8.0);
         AnchorStatParams A{ax, ay, cu, ids, cfirst, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, cq,
                            c_mlen, c_blen, c_st, c_last, pos_tab, qbase, skip_q};
         if (NB > 0) {
@@ -963,14 +973,16 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
                                (const int32_t *)blk.as<int32_t>(), c_fv);
             HY_CHECK_LAUNCH("chain_stats_flat_kernel");
         }
-        const int nqb = n_q < ctx->n_cu * 64 ? n_q : ctx->n_cu * 64;
-        hipLaunchKernelGGL(query_sumk_kernel, dim3((unsigned)nqb), dim3(64), 0, st, mini_pos, mp_off, n_q,
-                           sumk.as<unsigned long long>());
-        HY_CHECK_LAUNCH("query_sumk_kernel");
+        if (!sumk_done) {  // per query, shared by the batch's two chain sets
+            const int nqb = n_q < ctx->n_cu * 64 ? n_q : ctx->n_cu * 64;
+            hipLaunchKernelGGL(query_sumk_kernel, dim3((unsigned)nqb), dim3(64), 0, st, mini_pos, mp_off, n_q,
+                               (unsigned long long *)sumk);
+            HY_CHECK_LAUNCH("query_sumk_kernel");
+        }
     }
     RegParams P{ax, ay, ids, cfirst, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
-                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk.as<uint64_t>(), skip_q, kRegWave};
+                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk, skip_q, kRegWave};
     static const int wave_min_env = getenv("HYMET_REG_WAVE") ? atoi(getenv("HYMET_REG_WAVE")) : -1;  // tests / A-B
     if (wave_min_env >= 0) P.wave_min = wave_min_env;
     ProfScope _ps(ctx, "mm_regions", (double)NC * (8.0 + 8.0 + 4.0 * 5) + (double)n_q * 64.0);  // chain + stats reads, reg writes
@@ -986,8 +998,8 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
             h[b]++, mx = c > mx ? c : mx, tot += c;
             if (c > 2048) big_tot += c;
         }
-        fprintf(stderr, "[regions] n_q %d chains %lld max %lld | <=48 %lld <=256 %lld <=1k %lld <=2k %lld <=8k %lld >8k %lld (chains in >2k: %lld)\n",
-                n_q, (long long)tot, (long long)mx, (long long)h[0], (long long)h[1], (long long)h[2], (long long)h[3],
+        fprintf(stderr, "[regions] n_q %d anchors %lld chains %lld max %lld | <=48 %lld <=256 %lld <=1k %lld <=2k %lld <=8k %lld >8k %lld (chains in >2k: %lld)\n",
+                n_q, (long long)NB, (long long)tot, (long long)mx, (long long)h[0], (long long)h[1], (long long)h[2], (long long)h[3],
                 (long long)h[4], (long long)h[5], (long long)big_tot);
     }
     DevBuf big, gscr;
