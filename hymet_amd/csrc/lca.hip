@@ -185,11 +185,11 @@ __global__ void acc_first_kernel(const int32_t *q, const int32_t *part, int64_t 
 
 __global__ void acc_keys_kernel(const int32_t *first_part, int32_t n_q, uint64_t *key, int32_t *n_rows) {
     const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n_q) return;
-    const int32_t p = first_part[q];
+    const int32_t p = q < n_q ? first_part[q] : kNoPart;
     const bool none = p == kNoPart || p == 0x7f7f7f7f;
-    key[q] = none ? ~0ull : ((uint64_t)(uint32_t)p << 32 | (uint32_t)q);
-    if (!none) atomicAdd(n_rows, 1);
+    if (q < n_q) key[q] = none ? ~0ull : ((uint64_t)(uint32_t)p << 32 | (uint32_t)q);
+    const uint64_t m = __ballot(!none);  // one atomic per wave on the shared counter
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(n_rows, __popcll(m));
 }
 
 __global__ void acc_rows_kernel(const uint64_t *key, int32_t n_rows, const uint32_t *cnt, int32_t *row_q, int32_t *row_part,

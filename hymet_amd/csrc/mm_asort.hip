@@ -169,10 +169,17 @@ __global__ __launch_bounds__(256) void tile_hist_kernel(const uint64_t *__restri
     const int n = tile_n[blockIdx.x];
     for (int b = threadIdx.x; b < nbins; b += 256) h[b] = 0;
     __syncthreads();
-    for (int e0 = 0; e0 < n; e0 += 256) {  // every lane runs the loop (wave-level ballots inside)
-        const int e = e0 + threadIdx.x;
-        const bool act = e < n;
-        (void)lds_rank(h, act ? (int)((key[a0 + e] >> pb) & (nbins - 1)) : 0, act);
+    // every lane runs the loop (wave-level ballots inside); eight rows of keys loaded at a time,
+    // at clamped positions (straight-line loads: the waits are counted, not vmcnt(0) per row)
+    for (int e0 = 0; e0 < n; e0 += 256 * 8) {
+        uint64_t kv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) kv[u] = key[a0 + min(e0 + 256 * u + (int)threadIdx.x, n - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const bool act = e0 + 256 * u + (int)threadIdx.x < n;
+            (void)lds_rank(h, act ? (int)((kv[u] >> pb) & (nbins - 1)) : 0, act);
+        }
     }
     __syncthreads();
     uint32_t *row = H + (int64_t)blockIdx.x * nbins;
@@ -180,23 +187,27 @@ __global__ __launch_bounds__(256) void tile_hist_kernel(const uint64_t *__restri
 }
 
 // one block per large query: H[t][b] <- offset (within the query) of tile t's bin-b run;
-// every non-empty bin appended to the group list
-__global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const int64_t *tpos, int nbins,
-                                                         uint32_t *__restrict__ H, Seg *groups, int64_t cap,
-                                                         int32_t *n_groups, int64_t *mail) {
-    __shared__ uint32_t part[256];
-    __shared__ uint32_t carry;
+// every non-empty bin appended to the group list.  A thread per bin (rows of 1024 bins) walks
+// the bin down the query's tiles: a long contig has hundreds of tiles, and its block is the
+// launch's tail (256 threads walking four rows of bins one after the other took 1.3 ms per
+// launch on C4)
+__global__ __launch_bounds__(1024) void query_scan_kernel(const Seg *large, const int64_t *tpos, int nbins,
+                                                          uint32_t *__restrict__ H, Seg *groups, int64_t cap,
+                                                          int32_t *n_groups, int64_t *mail) {
+    __shared__ uint32_t wsum[16], wgrp[16];
+    __shared__ int32_t gbase;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const Seg S = large[blockIdx.x];
     const int64_t t0 = tpos[S.q], t1 = t0 + (S.n + kPart - 1) / kPart;
-    if (threadIdx.x == 0) carry = 0;
-    for (int r = 0; r < nbins; r += 256) {  // bins r + tid, in bin order across rows
-        const int b = r + threadIdx.x;
+    uint32_t carry = 0;  // anchors in the bins of earlier rows (block-uniform)
+    for (int r = 0; r < nbins; r += 1024) {  // bins r + tid, in bin order across rows
+        const int b = r + tid;
         uint32_t run = 0;
         if (b < nbins)
-            for (int64_t t = t0; t < t1; t += 32) {  // 32 loads in flight: this serial walk down
-                uint32_t v[32];                      // a long query's tiles is the launch's tail
+            for (int64_t t = t0; t < t1; t += 32) {  // 32 loads in flight (clamped rows: straight-line)
+                uint32_t v[32];
 #pragma unroll
-                for (int j = 0; j < 32; j++) v[j] = t + j < t1 ? H[(t + j) * nbins + b] : 0u;
+                for (int j = 0; j < 32; j++) v[j] = H[min(t + j, t1 - 1) * nbins + b];
 #pragma unroll
                 for (int j = 0; j < 32; j++)
                     if (t + j < t1) {
@@ -204,29 +215,51 @@ __global__ __launch_bounds__(256) void query_scan_kernel(const Seg *large, const
                         run += v[j];
                     }
             }
-        part[threadIdx.x] = run;
-        __syncthreads();
-        for (int d = 1; d < 256; d <<= 1) {  // inclusive scan over the row's bins
-            const uint32_t o = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
-            __syncthreads();
-            part[threadIdx.x] += o;
-            __syncthreads();
+        uint32_t inc = run;  // inclusive scan over the row's bins: waves, then the wave sums
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= d) inc += o;
         }
-        const uint32_t base = carry + part[threadIdx.x] - run;
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        uint32_t wex = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t x = wsum[k];
+            wex += k < w ? x : 0u;
+            tot += x;
+        }
+        const uint32_t base = carry + wex + inc - run;
+        carry += tot;
         if (b < nbins && run > 0)
             for (int64_t t = t0; t < t1; t += 32) {
                 uint32_t v[32];
 #pragma unroll
-                for (int j = 0; j < 32; j++) v[j] = t + j < t1 ? H[(t + j) * nbins + b] : 0u;
+                for (int j = 0; j < 32; j++) v[j] = H[min(t + j, t1 - 1) * nbins + b];
 #pragma unroll
                 for (int j = 0; j < 32; j++)
                     if (t + j < t1) H[(t + j) * nbins + b] = v[j] + base;
             }
-        const int slot = wave_append(n_groups, b < nbins && run > 0);
-        if (slot >= 0 && slot < cap) groups[slot] = Seg{S.s + base, (int32_t)run, S.q};  // host checks the total
+        // the row's non-empty bins appended with one global atomic per block (one per wave
+        // serialised ~40k returning atomics per launch on the single counter)
+        const bool ne = b < nbins && run > 0;
+        const uint64_t nm = __ballot(ne);
+        if (lane == 0) wgrp[w] = (uint32_t)__popcll(nm);
         __syncthreads();
-        if (threadIdx.x == 255) carry += part[255];
+        uint32_t gex = 0, gtot = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t x = wgrp[k];
+            gex += k < w ? x : 0u;
+            gtot += x;
+        }
+        if (tid == 0) gbase = gtot ? atomicAdd(n_groups, (int32_t)gtot) : 0;
         __syncthreads();
+        if (ne) {
+            const int64_t slot = (int64_t)gbase + gex + __popcll(nm & ((1ull << lane) - 1));
+            if (slot < cap) groups[slot] = Seg{S.s + base, (int32_t)run, S.q};  // host checks the total
+        }
+        __syncthreads();  // wsum / wgrp / gbase are rewritten by the next row
     }
     publish_counters(n_groups, 1, mail);
 }
@@ -271,11 +304,14 @@ __global__ __launch_bounds__(256) void tile_scatter_kernel(const uint64_t *__res
         uint32_t vv[kSub / 256], rk[kSub / 256];
         int bn[kSub / 256];
 #pragma unroll
+        for (int j = 0; j < kSub / 256; j++) {  // the round's loads first, at clamped positions
+            const int e = min(j * 256 + tid, m - 1);
+            kk[j] = key[a0 + r0 + e];
+            vv[j] = val[a0 + r0 + e];
+        }
+#pragma unroll
         for (int j = 0; j < kSub / 256; j++) {  // every lane runs the loop (wave-level ballots inside)
-            const int e = j * 256 + tid;
-            const bool act = e < m;
-            kk[j] = act ? key[a0 + r0 + e] : 0;
-            vv[j] = act ? val[a0 + r0 + e] : 0;
+            const bool act = j * 256 + tid < m;
             bn[j] = (int)((kk[j] >> pb) & (uint64_t)(nbins - 1));
             rk[j] = lds_rank(lo, bn[j], act);
         }
@@ -437,8 +473,21 @@ __global__ __launch_bounds__(BLOCK) void block_seg_sort_kernel(const Seg *list, 
     const int tid = threadIdx.x;
     const uint64_t lm = (1ull << nbits) - 1, ym = (1ull << ybits) - 1;
     const uint64_t hi_bits = key[S.s] & ~lm;
-    for (int e = tid; e < CAP; e += BLOCK)  // coalesced load, striped
-        sm[lds_ix(e)] = e < S.n ? ((key[S.s + e] & lm) << ybits | val[S.s + e]) : ~0ull;
+    {  // coalesced load, striped: every row's loads issued before any is used (clamped positions)
+        uint64_t kr[ITEMS];
+        uint32_t vr[ITEMS];
+#pragma unroll
+        for (int u = 0; u < ITEMS; u++) {
+            const int e = min(u * BLOCK + tid, S.n - 1);
+            kr[u] = key[S.s + e];
+            vr[u] = val[S.s + e];
+        }
+#pragma unroll
+        for (int u = 0; u < ITEMS; u++) {
+            const int e = u * BLOCK + tid;
+            sm[lds_ix(e)] = e < S.n ? ((kr[u] & lm) << ybits | vr[u]) : ~0ull;
+        }
+    }
     __syncthreads();
     uint64_t k[ITEMS];
 #pragma unroll
@@ -628,7 +677,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     HY_ARG(gcap < INT32_MAX, "grouped_anchor_sort: too many groups in one batch");
     DevBuf groups;
     HY_HIP(groups.alloc(sizeof(Seg) * (size_t)(gcap + 1), st));
-    hipLaunchKernelGGL(query_scan_kernel, dim3((unsigned)nl), dim3(256), 0, st, large, tpos.as<int64_t>(), nbins,
+    hipLaunchKernelGGL(query_scan_kernel, dim3((unsigned)nl), dim3(1024), 0, st, large, tpos.as<int64_t>(), nbins,
                        H.as<uint32_t>(), groups.as<Seg>(), gcap, ctx->dctr + kCtrGroups, mb_dev(ctx, kMbGroups));
     HY_CHECK_LAUNCH("query_scan_kernel");
     HY_ARG(nbins >= 1 && nbins <= kMaxBins, "grouped_anchor_sort: bin count out of range");

@@ -1641,20 +1641,23 @@ constexpr int kBtWin = 8;
 // (C4: threshold 1024 -> 128 took mm_backtrack 623 -> 301 ms per step once the wave kernel
 // stopped issuing agent-scope fences)
 constexpr int64_t kBtLong = 128;
-// The wave kernel's z probes and walk window cover kBtChunks * 64 entries per memory round
-// trip.  Measured on C4: 4 chunks are slower than 1 (mm_backtrack.long 549 -> 814 ms per
-// step) -- most walks are short (an off-path anchor walks into a marked chain after a step
-// or two), so the kernel is throughput-bound, not bound by its longest walk.
+// The wave kernel's work counters (backtrack_long_kernel): kBtStripes of them, kBtCtrPad
+// ints apart, each atomic taking kBtGrab positions of its stripe
+#ifndef HYMET_BT_GRAB
+#define HYMET_BT_GRAB 1
+#endif
+#ifndef HYMET_BT_STRIPES
+#define HYMET_BT_STRIPES 8
+#endif
+constexpr int kBtGrab = HYMET_BT_GRAB, kBtStripes = HYMET_BT_STRIPES, kBtCtrPad = 64;
+// The wave kernel's walk window covers kBtChunks * 64 entries per memory round trip.
+// Measured on C4: 4 chunks are slower than 1 (mm_backtrack.long 549 -> 814 ms per step) --
+// most walks are short (an off-path anchor walks into a marked chain after a step or two);
+// one chunk widening to four after two reloads measured the same as one (round 4).
 #ifndef HYMET_BT_CHUNKS
-#define HYMET_BT_CHUNKS 4
+#define HYMET_BT_CHUNKS 1
 #endif
 constexpr int kBtChunks = HYMET_BT_CHUNKS;
-// ... so a walk starts with one chunk per window and widens to kBtChunks once it has
-// reloaded kBtWiden times (a long walk down a group's main chain: ~15 reloads per group on
-// C4, one dependent round trip each)
-#ifndef HYMET_BT_WIDEN
-#define HYMET_BT_WIDEN 2
-#endif
 #ifndef HYMET_BT_PROBE
 #define HYMET_BT_PROBE 4
 #endif
@@ -1687,7 +1690,7 @@ __global__ void bt_long_count_kernel(const int64_t *g_start, const int32_t *orde
         else hi = mid;
     }
     cnt[0] = lo;
-    cnt[1] = 0;  // the wave kernel's work counter
+    for (int k = 1; k <= kBtStripes; k++) cnt[k * kBtCtrPad] = 0;  // the wave kernel's work counters
 }
 
 __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, const int32_t *list, const int32_t *cnt,
@@ -1700,13 +1703,31 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
     __shared__ int32_t s_w;
     const int lane = threadIdx.x;
     const int32_t n_long = uni(ld_l2(cnt));
+    // The work list is dealt over kBtStripes counters (stripe s: list positions s + kBtStripes t),
+    // each on its own 256-byte line: a returning atomic per group on one counter address
+    // serialised at its L2 channel (~10^5 groups per launch: mm_backtrack.long 232 ms/step).
+    // A wave starts on stripe blockIdx % kBtStripes and moves on when it runs dry.
+    int stripe = (int)(blockIdx.x % kBtStripes), exhausted = 0;
+    int32_t w = 0, w_end = 0;  // stripe tickets [w, w_end) taken by this wave
     for (;;) {
-        if (lane == 0) s_w = atomicAdd(counter, 1);
-        __syncthreads();
-        const int32_t w = uni(s_w);
-        __syncthreads();
-        if (w >= n_long) break;
-        const int32_t g = uni(list[w]);
+        if (w >= w_end) {  // the next kBtGrab positions of this wave's stripe
+            for (;;) {
+                if (lane == 0) s_w = atomicAdd(counter + stripe * kBtCtrPad, kBtGrab);
+                __syncthreads();
+                w = uni(s_w);
+                __syncthreads();
+                w_end = w + kBtGrab;
+                if (stripe + kBtStripes * w < n_long || ++exhausted == kBtStripes) break;
+                stripe = stripe + 1 == kBtStripes ? 0 : stripe + 1;  // this stripe is done: help the next
+            }
+            if (exhausted == kBtStripes) break;
+        }
+        const int32_t wcur = stripe + kBtStripes * w++;
+        if (wcur >= n_long) {
+            w = w_end;  // the rest of this grab is past the list's end
+            continue;
+        }
+        const int32_t g = uni(list[wcur]);
         const int64_t g0 = uni64(P.g_start[g]);
         const int64_t z0 = g0, z1 = g0 + uni(P.z_cnt[g]);
         int64_t wpos = g0;
@@ -1820,7 +1841,6 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
             int64_t whi = -1;  // window: chunk c, lane l holds anchor whi - 64c - l
             int64_t wpc[kBtChunks];
             int32_t wfc[kBtChunks], wtc[kBtChunks];
-            int nch = 1, nrel = 0;  // chunks the window covers now; reloads so far in this walk
 #pragma unroll
             for (int c = 0; c < kBtChunks; c++) wpc[c] = -1, wfc[c] = 0, wtc[c] = 1;
             c_walk++;
@@ -1837,19 +1857,16 @@ __global__ __launch_bounds__(64) void backtrack_long_kernel(BacktrackParams P, c
                     if (zf > max_s) max_s = zf, nv = len, zc_nv = zc_len;
                     break;
                 }
-                if (nxt > whi || nxt <= whi - 64 * nch) {
+                if (nxt > whi || nxt <= whi - 64 * kBtChunks) {
                     c_reload++;
                     whi = nxt;
-                    if (++nrel > HYMET_BT_WIDEN) nch = kBtChunks;
 #pragma unroll
                     for (int c = 0; c < kBtChunks; c++) {
-                        if (c < nch) {  // uniform
-                            const int64_t jj = nxt - 64 * c - lane;
-                            const bool ok = jj >= g0;
-                            wpc[c] = ok ? P.p[jj] : -1;
-                            wfc[c] = ok ? P.f[jj] : 0;
-                            wtc[c] = ok ? ld_l2(P.t + jj) : 1;
-                        }
+                        const int64_t jj = nxt - 64 * c - lane;
+                        const bool ok = jj >= g0;
+                        wpc[c] = ok ? P.p[jj] : -1;
+                        wfc[c] = ok ? P.f[jj] : 0;
+                        wtc[c] = ok ? ld_l2(P.t + jj) : 1;
                     }
                 }
                 const int d = (int)(whi - nxt);
@@ -2195,7 +2212,7 @@ int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, c
     BacktrackParams P{g_start,  f,         p,       t,           z_cnt,    z_idx, n_groups, min_cnt, min_sc, max_drop,
                       long_min, (unsigned long long *)pbuf.p, chain_ids, chain_u, chain_first, n_chains};
     DevBuf cnt;
-    HY_HIP(cnt.alloc(8, ctx->stream));  // [0] long groups, [1] work counter: set by bt_long_count_kernel
+    HY_HIP(cnt.alloc(4 * (size_t)kBtCtrPad * (kBtStripes + 1), ctx->stream));  // [0] long groups, then the stripe counters
     // z index + t probe + walked (p, f) + t mark + chain id write, per anchor
     ProfScope _ps(ctx, "mm_backtrack", 32.0 * (double)n_anchors);
     if (n_work > 0) {
@@ -2210,12 +2227,14 @@ int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, c
     if (n_work > 0) {
         ProfScope _pl(ctx, "mm_backtrack.long");  // the wave-per-group part of mm_backtrack
         // resident waves per CU for the wave kernel (HYMET_BT_WAVES overrides); the occupancy
-        // limit (28) measured 4 % slower than 16 on C4
+        // limit (28) measured 4 % slower than 16 on C4 under the single work counter; with the
+        // striped counters 24 measured 3 % faster one-stream (112 vs 116 ms/step), 16 is kept
+        // to leave the other mapping stream room
         const char *ew = getenv("HYMET_BT_WAVES");
         const int per_cu = ew ? std::max(1, atoi(ew)) : 16;
         const int64_t nb = std::min<int64_t>(n_work, (int64_t)ctx->n_cu * per_cu);
         hipLaunchKernelGGL(backtrack_long_kernel, dim3((unsigned)nb), dim3(64), 0, ctx->stream, P, order,
-                           cnt.as<int32_t>(), cnt.as<int32_t>() + 1);
+                           cnt.as<int32_t>(), cnt.as<int32_t>() + kBtCtrPad);
         HY_CHECK_LAUNCH("backtrack_long_kernel");
     }
     if (prof) {

@@ -503,6 +503,17 @@ __device__ __forceinline__ void group_tile_heads(const uint64_t *x, int64_t n, c
     __shared__ int s_q0;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t t1 = min(t0 + kGTile, n);
+    // the (strand, target) words of the tile's anchors and of their predecessors, loaded before
+    // the query search at clamped positions (straight-line: 32 loads in flight per lane, where
+    // a load inside the head test's short-circuit was one round trip per row)
+    const uint32_t *xh = reinterpret_cast<const uint32_t *>(x) + 1;
+    uint32_t xv[16], xp[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int64_t i = min(t0 + j * 256 + (int64_t)threadIdx.x, n - 1);
+        xv[j] = xh[2 * i];
+        xp[j] = xh[2 * max(i - 1, (int64_t)0)];
+    }
     for (int k = threadIdx.x; k < kGTile / 32; k += 256) qs[k] = 0;
     if (threadIdx.x == 0) {  // first query whose range ends after t0
         int lo = 0, hi = n_q;
@@ -524,7 +535,7 @@ __device__ __forceinline__ void group_tile_heads(const uint64_t *x, int64_t n, c
     for (int j = 0; j < 16; j++) {
         const int64_t i = t0 + j * 256 + threadIdx.x;
         const int64_t l = i - t0;
-        h[j] = i < n && (i == 0 || (qs[l >> 5] >> (l & 31) & 1) || (x[i] >> 32) != (x[i - 1] >> 32));
+        h[j] = i < n && (i == 0 || (qs[l >> 5] >> (l & 31) & 1) || xv[j] != xp[j]);
         const uint64_t b = __ballot(h[j]);
         if (lane == 0) rc[j * 4 + w] = (uint32_t)__popcll(b);
     }
@@ -694,6 +705,25 @@ __global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
     const int lane = threadIdx.x & 63;
     const int32_t split = P.lists[0];
     const int nw = (int)(gridDim.x * (blockDim.x >> 6));
+    // list entries held per wave (lane i: the i-th pending group) and appended 64 at a time:
+    // one returning atomic per listed group on the shared counters serialised (~1 ms per
+    // launch over ~10^5 groups, as in query_scan_kernel before)
+    int32_t pend[3] = {0, 0, 0};  // merge, mid, big
+    int np[3] = {0, 0, 0};
+    unsigned long long big_m = 0;  // z entries of this wave's big groups
+    int32_t *const lst[3] = {P.merge_list, P.mid_list, P.big_list};
+    auto flush = [&](int l) {
+        if (np[l] == 0) return;
+        int base = 0;
+        if (lane == 0) base = atomicAdd(P.lists + (l == 0 ? 3 : l == 1 ? 1 : 2), np[l]);
+        base = __shfl(base, 0, 64);
+        if (lane < np[l]) lst[l][base + lane] = pend[l];
+        np[l] = 0;
+    };
+    auto push = [&](int l, int g) {
+        if (lane == np[l]) pend[l] = g;
+        if (++np[l] == 64) flush(l);
+    };
     for (int w = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); w < split; w += nw) {
         const int g = P.order[w];
         const int64_t g0 = P.g_start[g], n = P.g_start[g + 1] - g0;
@@ -744,20 +774,22 @@ __global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
             rs[0] = 0;
             P.z_cnt[g] = m;
             P.z_runs[g] = runs;
-            if (runs > 1 && runs <= P.max_runs) P.merge_list[atomicAdd(P.lists + 3, 1)] = g;
-            if (runs > P.max_runs) {
-                if (m <= kZs) {
-                    P.mid_list[atomicAdd(P.lists + 1, 1)] = g;
-                } else {
-                    // list rank only: the radix arrays' offsets are a scan of the counts in rank
-                    // order (zbig_count_kernel), since the sorted keys come out rank-major
-                    const int r = atomicAdd(P.lists + 2, 1);
-                    P.big_list[r] = g;
-                    atomicAdd((unsigned long long *)(P.lists + 4), (unsigned long long)m);
-                }
+        }
+        // (wave-uniform conditions)
+        if (runs > 1 && runs <= P.max_runs) push(0, g);
+        if (runs > P.max_runs) {
+            if (m <= kZs) {
+                push(1, g);
+            } else {
+                // list rank only: the radix arrays' offsets are a scan of the counts in rank
+                // order (zbig_count_kernel), since the sorted keys come out rank-major
+                push(2, g);
+                big_m += (unsigned long long)m;
             }
         }
     }
+    flush(0), flush(1), flush(2);
+    if (lane == 0 && big_m) atomicAdd((unsigned long long *)(P.lists + 4), big_m);
 }
 
 // one lane per group of <= kZLane anchors: rank = number of smaller keys

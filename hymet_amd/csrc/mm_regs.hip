@@ -2,7 +2,7 @@
 // mm_gen_regs (score + hash order), mm_reg_set_coor / mm_cal_fuzzy_len, mm_set_parent,
 // mm_select_sub (+ mm_sync_regs), mm_est_err, mm_filter_strand_retained, mm_set_mapq.
 // Everything that walks a chain's anchors is anchor-parallel and runs first:
-//   chain_stats_flat_kernel one thread per chained anchor: mlen/blen terms (mm_reg_set_coor),
+//   chain_stats_flat_kernel four chained anchors per thread: mlen/blen terms (mm_reg_set_coor),
 //                           its minimizer index (mm_est_err's get_mini_idx, by table lookup)
 //                           and the first anchor, in est_err's walking order, whose index does
 //                           not increase -- est_err's sequential two-pointer walk matches
@@ -162,112 +162,151 @@ __device__ __forceinline__ int32_t mini_idx_at(const AnchorStatParams &P, int64_
     return (x >= 0 && x < qlen) ? P.pos_tab[P.qbase[q] + x] : -1;
 }
 
-// the chain holding chain-order position 256 b, for every block b of chain_stats_flat_kernel
-// (one thread per chain writes the block starts inside it: no per-block binary search, whose
-// ~log2(NC) dependent loads held the whole block)
+// chain_stats_flat_kernel: kStatItems chain-order positions per thread (rows of 256 in a
+// block), their loads issued row after row before any is used -- one position per thread
+// left every thread waiting on a chain of ~6 dependent loads (chain, query, chain slot,
+// anchor, minimizer index) with nothing else in flight
+constexpr int kStatItems = 4;
+constexpr int kStatSpan = 256 * kStatItems;  // chain-order positions per block
+
+// the chain holding chain-order position kStatSpan b, for every block b of
+// chain_stats_flat_kernel (one thread per chain writes the block starts inside it: no
+// per-block binary search, whose ~log2(NC) dependent loads held the whole block)
 __global__ void block_chain_kernel(const int64_t *cboff, int64_t NC, int64_t NB, int32_t *blk_c0) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= NC) return;
     const int64_t s = cboff[c], e = c + 1 < NC ? cboff[c + 1] : NB;
-    for (int64_t b = (s + 255) >> 8; (b << 8) < e; ++b) blk_c0[b] = (int32_t)c;
+    for (int64_t b = (s + kStatSpan - 1) / kStatSpan; b * kStatSpan < e; ++b) blk_c0[b] = (int32_t)c;
 }
 
 __global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams P, const int32_t *blk_c0, int32_t *c_fv) {
-    __shared__ int32_t s_st[257];  // block-relative starts of chains c0 .. c0 + 256 (clamped)
-    const int64_t b0 = (int64_t)blockIdx.x * blockDim.x;
+    constexpr int K = kStatItems;
+    __shared__ int32_t s_st[kStatSpan + 1];  // block-relative starts of chains c0 .. c0 + kStatSpan (clamped)
+    const int64_t b0 = (int64_t)blockIdx.x * kStatSpan;
     const int64_t cb0 = blk_c0[blockIdx.x];  // last c with cboff[c] <= b0
-    for (int i = threadIdx.x; i < 257; i += blockDim.x) {
+    for (int i = threadIdx.x; i <= kStatSpan; i += blockDim.x) {
         const int64_t cc = cb0 + i;
-        s_st[i] = cc < P.NC ? (int32_t)min(P.cboff[cc] - b0, (int64_t)256) : 256;
+        s_st[i] = cc < P.NC ? (int32_t)min(P.cboff[cc] - b0, (int64_t)kStatSpan) : kStatSpan;
     }
     __syncthreads();
-    const int64_t b = b0 + threadIdx.x;
     const int lane = threadIdx.x & 63;
-    const bool in = b < P.NB;
-    int64_t c = -1;
-    if (in) {
-        int lo = 0, hi = 256;  // last i with s_st[i] <= threadIdx.x (s_st[0] <= 0, nondecreasing)
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_st[mid] <= (int)threadIdx.x) lo = mid;
-            else hi = mid - 1;
-        }
-        c = cb0 + lo;
-        if (lo == 256) {  // beyond the staged chains (chains with no anchors in the range)
-            int64_t l2 = c, h2 = P.NC - 1;
-            while (l2 < h2) {
-                const int64_t mid = (l2 + h2 + 1) >> 1;
-                if (P.cboff[mid] <= b) l2 = mid;
-                else h2 = mid - 1;
-            }
-            c = l2;
-        }
-    }
-    const int64_t q = in ? (int64_t)P.cq[c] : 0;
-    const bool act = in && !(P.skip_q && P.skip_q[q]);
-    int32_t cnt = 0, j = 0, qlen = 0, cur = -1;
-    int64_t f0 = 0;  // slot of chain-order position 0 in ids
-    uint64_t x = 0, y = 0;
-    if (act) {
-        cnt = (int32_t)P.cu[c];
-        j = (int32_t)(b - P.cboff[c]);
-        f0 = P.cfirst[c] + cnt - 1;
-        const int64_t a = P.ids[f0 - j];
-        x = P.ax[a], y = P.ay[a];
-        qlen = (int)P.qlen[q];
-        cur = mini_idx_at(P, q, qlen, x, y);
-    }
-    // chain-order neighbours (anchor and minimizer index) from the adjacent lanes (same
-    // chain), else loaded
-    const int32_t ci = (int32_t)c;
-    const int32_t cprev = __shfl_up(ci, 1, 64), cnext = __shfl_down(ci, 1, 64);
-    uint64_t xp = __shfl_up(x, 1, 64), yp = __shfl_up(y, 1, 64);
-    uint64_t xn = __shfl_down(x, 1, 64), yn = __shfl_down(y, 1, 64);
-    const int32_t cur_p = __shfl_up(cur, 1, 64), cur_n = __shfl_down(cur, 1, 64);
-    int dm = 0, db = 0, fv = INT32_MAX;
-    if (act) {
-        const bool rev = x >> 63;
-        const bool own_p = lane > 0 && cprev == ci, own_n = lane < 63 && cnext == ci;
-        if (j > 0 && !own_p) {
-            const int64_t a = P.ids[f0 - j + 1];
-            xp = P.ax[a], yp = P.ay[a];
-        }
-        if (rev && j + 1 < cnt && !own_n) {
-            const int64_t a = P.ids[f0 - j - 1];
-            xn = P.ax[a], yn = P.ay[a];
-        }
-        const int32_t span = (int32_t)(y >> 32 & 0xff);
-        if (j == 0) {
-            dm = db = span;
-        } else {  // hit.c mm_reg_set_coor
-            const int32_t tl = (int32_t)x - (int32_t)xp;
-            const int32_t ql = (int32_t)y - (int32_t)yp;
-            db = tl > ql ? tl : ql;
-            dm = tl > span && ql > span ? span : tl < ql ? tl : ql;
-        }
-        const int32_t kk = rev ? cnt - 1 - j : j;  // est_err walking order
-        fv = cnt;
-        if (kk >= 1) {
-            const int32_t prev = rev ? (own_n ? cur_n : mini_idx_at(P, q, qlen, xn, yn))
-                                     : (own_p ? cur_p : mini_idx_at(P, q, qlen, xp, yp));
-            if (cur < 0 || cur <= prev) fv = kk;
-        }
-        if (kk == 0) P.c_st[c] = cur;
-        if (kk == cnt - 1) P.c_last[c] = cur;
-    }
-    const int32_t cr = act ? ci : -1;
-    // segmented inclusive reduction over lanes of the same chain (contiguous in the wave)
+    int64_t c[K], q[K], f0[K];  // chain, query, slot of chain-order position 0 in ids
+    bool act[K];
+    int32_t cnt[K], j[K], qlen[K], cur[K];
+    uint64_t x[K], y[K];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int32_t co = __shfl_up(cr, d, 64);
-        const int dmo = __shfl_up(dm, d, 64), dbo = __shfl_up(db, d, 64), fvo = __shfl_up(fv, d, 64);
-        if (lane >= d && co == cr) dm += dmo, db += dbo, fv = min(fv, fvo);
+    for (int k = 0; k < K; k++) {
+        const int r = 256 * k + (int)threadIdx.x;  // block-relative position
+        const int64_t b = b0 + r;
+        c[k] = -1;
+        if (b < P.NB) {
+            int lo = 0, hi = kStatSpan;  // last i with s_st[i] <= r (s_st[0] <= 0, nondecreasing)
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_st[mid] <= r) lo = mid;
+                else hi = mid - 1;
+            }
+            c[k] = cb0 + lo;
+            if (lo == kStatSpan) {  // beyond the staged chains (chains with no anchors in the range)
+                int64_t l2 = c[k], h2 = P.NC - 1;
+                while (l2 < h2) {
+                    const int64_t mid = (l2 + h2 + 1) >> 1;
+                    if (P.cboff[mid] <= b) l2 = mid;
+                    else h2 = mid - 1;
+                }
+                c[k] = l2;
+            }
+        }
     }
-    const int32_t cn = __shfl_down(cr, 1, 64);
-    if (act && (lane == 63 || cn != cr)) {  // last lane of its chain piece in this wave
-        atomicAdd(P.c_mlen + c, dm);
-        atomicAdd(P.c_blen + c, db);
-        atomicMin(c_fv + c, fv);
+    // (every load below is unconditional, at a valid index for inactive positions -- chain 0,
+    // its first slot -- so the rows' loads stay straight-line code and are all in flight
+    // before the first is used)
+    int64_t qb[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) q[k] = (int64_t)P.cq[c[k] >= 0 ? c[k] : 0];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const int64_t cc = c[k] >= 0 ? c[k] : 0;
+        cnt[k] = (int32_t)P.cu[cc];
+        const int64_t cb = P.cboff[cc];
+        f0[k] = P.cfirst[cc] + cnt[k] - 1;
+        j[k] = (int32_t)(b0 + 256 * k + threadIdx.x - cb);
+        qlen[k] = (int)P.qlen[q[k]];
+        qb[k] = P.qbase[q[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        act[k] = c[k] >= 0;
+        if (P.skip_q) act[k] = act[k] && !P.skip_q[q[k]];
+        if (!act[k]) j[k] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const int64_t a = P.ids[f0[k] - j[k]];
+        x[k] = P.ax[a], y[k] = P.ay[a];
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {  // mini_idx_at, its table read unconditional
+        int32_t xq = (int32_t)y[k];
+        if (x[k] >> 63) xq = qlen[k] - 1 - (int32_t)y[k] + (int32_t)(y[k] >> 32 & 0xff) - 1;
+        const bool inq = xq >= 0 && xq < qlen[k];
+        const int32_t v = P.pos_tab[qb[k] + (inq ? xq : 0)];
+        cur[k] = act[k] && inq ? v : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        // chain-order neighbours (anchor and minimizer index) from the adjacent lanes (same
+        // chain), else loaded
+        const int32_t ci = (int32_t)c[k];
+        const int32_t cprev = __shfl_up(ci, 1, 64), cnext = __shfl_down(ci, 1, 64);
+        uint64_t xp = __shfl_up(x[k], 1, 64), yp = __shfl_up(y[k], 1, 64);
+        uint64_t xn = __shfl_down(x[k], 1, 64), yn = __shfl_down(y[k], 1, 64);
+        const int32_t cur_p = __shfl_up(cur[k], 1, 64), cur_n = __shfl_down(cur[k], 1, 64);
+        int dm = 0, db = 0, fv = INT32_MAX;
+        if (act[k]) {
+            const bool rev = x[k] >> 63;
+            const bool own_p = lane > 0 && cprev == ci, own_n = lane < 63 && cnext == ci;
+            if (j[k] > 0 && !own_p) {
+                const int64_t a = P.ids[f0[k] - j[k] + 1];
+                xp = P.ax[a], yp = P.ay[a];
+            }
+            if (rev && j[k] + 1 < cnt[k] && !own_n) {
+                const int64_t a = P.ids[f0[k] - j[k] - 1];
+                xn = P.ax[a], yn = P.ay[a];
+            }
+            const int32_t span = (int32_t)(y[k] >> 32 & 0xff);
+            if (j[k] == 0) {
+                dm = db = span;
+            } else {  // hit.c mm_reg_set_coor
+                const int32_t tl = (int32_t)x[k] - (int32_t)xp;
+                const int32_t ql = (int32_t)y[k] - (int32_t)yp;
+                db = tl > ql ? tl : ql;
+                dm = tl > span && ql > span ? span : tl < ql ? tl : ql;
+            }
+            const int32_t kk = rev ? cnt[k] - 1 - j[k] : j[k];  // est_err walking order
+            fv = cnt[k];
+            if (kk >= 1) {
+                const int32_t prev = rev ? (own_n ? cur_n : mini_idx_at(P, q[k], qlen[k], xn, yn))
+                                         : (own_p ? cur_p : mini_idx_at(P, q[k], qlen[k], xp, yp));
+                if (cur[k] < 0 || cur[k] <= prev) fv = kk;
+            }
+            if (kk == 0) P.c_st[c[k]] = cur[k];
+            if (kk == cnt[k] - 1) P.c_last[c[k]] = cur[k];
+        }
+        const int32_t cr = act[k] ? ci : -1;
+        // segmented inclusive reduction over lanes of the same chain (contiguous in the wave)
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int32_t co = __shfl_up(cr, d, 64);
+            const int dmo = __shfl_up(dm, d, 64), dbo = __shfl_up(db, d, 64), fvo = __shfl_up(fv, d, 64);
+            if (lane >= d && co == cr) dm += dmo, db += dbo, fv = min(fv, fvo);
+        }
+        const int32_t cn = __shfl_down(cr, 1, 64);
+        if (act[k] && (lane == 63 || cn != cr)) {  // last lane of its chain piece in this wave
+            atomicAdd(P.c_mlen + c[k], dm);
+            atomicAdd(P.c_blen + c[k], db);
+            atomicMin(c_fv + c[k], fv);
+        }
     }
 }
 
@@ -965,11 +1004,11 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
             hipLaunchKernelGGL(chain_stats_init_kernel, dim3((unsigned)cdiv(NC + 1, 256)), dim3(256), 0, st, c_mlen, c_blen,
                                c_fv, NC + 1);
             HY_CHECK_LAUNCH("chain_stats_init_kernel");
-            HY_HIP(blk.alloc(4 * (size_t)(cdiv(NB, 256) + 1), st));
+            HY_HIP(blk.alloc(4 * (size_t)(cdiv(NB, kStatSpan) + 1), st));
             hipLaunchKernelGGL(block_chain_kernel, dim3((unsigned)cdiv(NC, 256)), dim3(256), 0, st, cboff, NC, NB,
                                blk.as<int32_t>());
             HY_CHECK_LAUNCH("block_chain_kernel");
-            hipLaunchKernelGGL(chain_stats_flat_kernel, dim3((unsigned)cdiv(NB, 256)), dim3(256), 0, st, A,
+            hipLaunchKernelGGL(chain_stats_flat_kernel, dim3((unsigned)cdiv(NB, kStatSpan)), dim3(256), 0, st, A,
                                (const int32_t *)blk.as<int32_t>(), c_fv);
             HY_CHECK_LAUNCH("chain_stats_flat_kernel");
         }
