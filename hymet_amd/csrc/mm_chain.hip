@@ -200,6 +200,12 @@ __device__ int4 *g_chain_gcnt;  // per group: loop iterations, batch attempts, b
 #define GCNT(f, v)
 #endif
 
+// the wave kernel's work counters: kChainStripes of them, kChainCtrPad ints (256 B) apart
+#ifndef HYMET_CHAIN_STRIPES
+#define HYMET_CHAIN_STRIPES 8
+#endif
+constexpr int kChainStripes = HYMET_CHAIN_STRIPES, kChainCtrPad = 64;
+
 struct ChainParams {
     const uint64_t *ax;
     const uint64_t *ay;
@@ -486,11 +492,20 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
     int32_t *blx = reinterpret_cast<int32_t *>(sp);  // x of block b's last anchor at [b & (kBlx - 1)]
     const double c = 0.5 * (double)P.pen_gap;
     const int32_t n_work = P.work_end ? min(P.n_work, *P.work_end) : P.n_work;
+    // work list dealt over kChainStripes counters on separate lines (stripe s: positions
+    // s + kChainStripes t), as in backtrack_long_kernel: one returning atomic per group on a
+    // single address serialises at its L2 channel
+    int stripe = (int)(blockIdx.x % kChainStripes), exhausted = 0;
     for (;;) {
         int w = 0;
-        if (lane == 0) w = atomicAdd(P.work_counter, 1);
+        if (lane == 0) w = atomicAdd(P.work_counter + stripe * kChainCtrPad, 1);
         w = __builtin_amdgcn_readfirstlane(w);
-        if (w >= n_work) break;
+        w = stripe + kChainStripes * w;
+        if (w >= n_work) {
+            if (++exhausted == kChainStripes) break;
+            stripe = stripe + 1 == kChainStripes ? 0 : stripe + 1;  // this stripe is done: help the next
+            continue;
+        }
         const int g = P.order[w];
         GTIME_START
         const int64_t g0 = P.g_start[g];
@@ -2052,7 +2067,7 @@ constexpr int kSmall = HYMET_CHAIN_SMALL;  // <= 32 (window sets are 32-bit mask
 __global__ void chain_small_split_kernel(const int64_t *g_start, const int32_t *order, int32_t n_work, int32_t *split,
                                          int32_t *counter) {
     if (threadIdx.x != 0) return;
-    *counter = 0;
+    for (int k = 0; k < kChainStripes; k++) counter[k * kChainCtrPad] = 0;
     int32_t lo = 0, hi = n_work;
     while (lo < hi) {
         const int32_t mid = (lo + hi) >> 1;
@@ -2176,7 +2191,7 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
     DevBuf cnt, sum, split;
     const size_t n_sum = (size_t)(n_anchors >> 6) + (size_t)n_groups + 2;
     HY_HIP(sum.alloc(16 * kGSumInts * n_sum, ctx->stream));
-    HY_HIP(cnt.alloc(4, ctx->stream));
+    HY_HIP(cnt.alloc(4 * (size_t)kChainCtrPad * kChainStripes, ctx->stream));  // the wave kernel's striped work counters
     HY_HIP(split.alloc(4, ctx->stream));
     if (max_dist < bw) max_dist = bw;
     if (max_dist_inner <= 0 || max_dist_inner >= max_dist) max_dist_inner = 0;

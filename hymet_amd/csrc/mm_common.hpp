@@ -38,6 +38,21 @@ __host__ __device__ __forceinline__ uint64_t hash64(uint64_t key) {
 // cache at scope exit.  The cache is per stream and all work of a context runs on its one
 // stream, so a block handed back while kernels that use it are still queued can be reissued
 // at once: the next user is queued behind them.
+// mm_est_err's get_mini_idx as a table lookup: per 64 query bases (each query's range padded
+// to a multiple of 64), a bit per base where a seeded minimizer starts and the query-relative
+// index of the word's first such minimizer; index(x) = base + popcount(bits below x).  16 B per
+// 64 bases (a dense int32 per base was 4 B per base: 240 MB per 60 Mbp batch, a memset and a
+// gather over ~20 cache lines per wave of chain anchors)
+struct MiniWord {
+    uint64_t bits;
+    uint32_t base;
+    uint32_t pad;
+};
+__device__ __forceinline__ int32_t mini_word_idx(const MiniWord &e, int32_t x) {
+    const uint64_t below = (1ull << (x & 63)) - 1;
+    return (e.bits >> (x & 63) & 1) ? (int32_t)(e.base + (uint32_t)__popcll(e.bits & below)) : -1;
+}
+
 struct DevBuf {
     void *p = nullptr;
     size_t n = 0, cls = 0;

@@ -1588,17 +1588,28 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
                    int64_t NB, int64_t NC, int64_t NM, const uint32_t *cq,
-                   const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q, uint64_t *sumk, bool sumk_done);
+                   const MiniWord *mtab, const int64_t *qbase, const uint32_t *skip_q, uint64_t *sumk, bool sumk_done);
 
 namespace {
-// dense query position -> index among the query's seeded minimizers (mini_pos order), for
-// mm_est_err's get_mini_idx (anchor_mini_idx_kernel); positions without one stay -1
-__global__ void mini_table_kernel(const uint64_t *my, const uint32_t *seed_n, const uint32_t *qid, const int64_t *qm_off,
-                                  const int64_t *mp_pos, const int64_t *qbase, int64_t M, int32_t *pos_tab) {
+// query position -> index among the query's seeded minimizers (mini_pos order), for
+// mm_est_err's get_mini_idx (MiniWord): pass 1 sets the start bits, pass 2 writes each word's
+// base (every seeded minimizer of the word writes the same value: its index less the start
+// bits below it)
+__global__ void mini_bits_kernel(const uint64_t *my, const uint32_t *seed_n, const uint32_t *qid, const int64_t *qbase,
+                                 int64_t M, MiniWord *tab) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M || !seed_n[i]) return;
+    const int64_t b = qbase[qid[i]] + ((uint32_t)my[i] >> 1);
+    atomicOr((unsigned long long *)&tab[b >> 6].bits, 1ull << (b & 63));
+}
+__global__ void mini_base_kernel(const uint64_t *my, const uint32_t *seed_n, const uint32_t *qid, const int64_t *qm_off,
+                                 const int64_t *mp_pos, const int64_t *qbase, int64_t M, MiniWord *tab) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= M || !seed_n[i]) return;
     const uint32_t q = qid[i];
-    pos_tab[qbase[q] + ((uint32_t)my[i] >> 1)] = (int32_t)(mp_pos[i] - mp_pos[qm_off[q]]);
+    const int64_t b = qbase[q] + ((uint32_t)my[i] >> 1);
+    const uint64_t bits = tab[b >> 6].bits;
+    tab[b >> 6].base = (uint32_t)(mp_pos[i] - mp_pos[qm_off[q]]) - (uint32_t)__popcll(bits & ((1ull << (b & 63)) - 1));
 }
 
 // re-chain input: the chained anchors of flagged queries (query-major), with sort keys
@@ -1886,21 +1897,25 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
     hipLaunchKernelGGL(sample_off_kernel, dim3((unsigned)cdiv(n_q + 1, 256)), dim3(256), 0, st, mp_pos.as<int64_t>(),
                        qm_off.as<int64_t>(), n_q, NM, mp_off.as<int64_t>());
     HY_CHECK_LAUNCH("sample_off_kernel");
-    // mm_est_err's minimizer lookup table (filled once seed_n is final, below)
+    // mm_est_err's minimizer lookup table (filled once seed_n is final, below): each query's
+    // bases at a 64-aligned offset, 16 B per 64 bases
     DevBuf d_qbase, pos_tab;
     std::vector<int64_t> qbase(n_q + 1, 0);  // lives until the call returns (async H2D source)
     int64_t max_qlen = 1;
     {
         for (int q = 0; q < n_q; q++) {
-            qbase[q + 1] = qbase[q] + h_lens[q];
+            qbase[q + 1] = qbase[q] + ((h_lens[q] + 63) & ~(int64_t)63);
             max_qlen = std::max<int64_t>(max_qlen, h_lens[q]);
         }
         HY_HIP(d_qbase.alloc(8 * (size_t)(n_q + 1), st));
         HY_HIP(hipMemcpyAsync(d_qbase.p, qbase.data(), 8 * (size_t)(n_q + 1), hipMemcpyHostToDevice, st));
-        HY_HIP(pos_tab.alloc(4 * (size_t)(qbase[n_q] + 1), st));
-        HY_HIP(hipMemsetAsync(pos_tab.p, 0xFF, 4 * (size_t)(qbase[n_q] + 1), st));
-        LAUNCH1(mini_table_kernel, M, my.as<uint64_t>(), seed_n.as<uint32_t>(), qid.as<uint32_t>(), qm_off.as<int64_t>(),
-                mp_pos.as<int64_t>(), d_qbase.as<int64_t>(), M, pos_tab.as<int32_t>());
+        const size_t n_words = (size_t)(qbase[n_q] >> 6) + 1;
+        HY_HIP(pos_tab.alloc(sizeof(MiniWord) * n_words, st));
+        HY_HIP(hipMemsetAsync(pos_tab.p, 0, sizeof(MiniWord) * n_words, st));
+        LAUNCH1(mini_bits_kernel, M, my.as<uint64_t>(), seed_n.as<uint32_t>(), qid.as<uint32_t>(), d_qbase.as<int64_t>(), M,
+                pos_tab.as<MiniWord>());
+        LAUNCH1(mini_base_kernel, M, my.as<uint64_t>(), seed_n.as<uint32_t>(), qid.as<uint32_t>(), qm_off.as<int64_t>(),
+                mp_pos.as<int64_t>(), d_qbase.as<int64_t>(), M, pos_tab.as<MiniWord>());
     }
     AnchorSet S1;
     HY_HIP(S1.d_off.alloc(8 * (size_t)(n_q + 1), st));
@@ -2108,7 +2123,7 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                               d_qlen.as<int64_t>(), d_hash, rep_len.as<int32_t>(), idx->d_len, n_q, opt, k,
                               z.p, rg.as<hymet_mm_reg>(), wv.as<int32_t>(), cov.as<uint64_t>(), tmp.as<int32_t>(),
                               nr.as<int32_t>(), C.n_anchor, NC, NM, C.cq.as<uint32_t>(),
-                              pos_tab.as<int32_t>(), d_qbase.as<int64_t>(), skip_q, sumk.as<uint64_t>(),
+                              pos_tab.as<MiniWord>(), d_qbase.as<int64_t>(), skip_q, sumk.as<uint64_t>(),
                               std::exchange(sumk_done, true));
     };
     DevBuf rg1, nr1, rg2, nr2;

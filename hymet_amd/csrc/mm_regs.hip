@@ -137,7 +137,7 @@ struct AnchorStatParams {
     int n_q;
     const uint32_t *cq;      // query of each chain
     int32_t *c_mlen, *c_blen, *c_st, *c_last;
-    const int32_t *pos_tab;  // query base -> minimizer index (or -1), at qbase[q] + position
+    const MiniWord *mtab;    // query base -> minimizer index (or -1): word (qbase[q] + position) >> 6
     const int64_t *qbase;
     const uint32_t *skip_q;  // queries whose chains are superseded by the long join (nullable)
 };
@@ -149,9 +149,9 @@ struct AnchorStatParams {
 // first/last minimizer index and the first anchor whose index does not increase (est_err's
 // loop `for (k=1, j=st+1; j<nm && k<cnt; ++j) if (idx(k) == j) ++k, ++n_match;` matches
 // anchor k iff idx(1..k) strictly increase from st; the first that does not, or has no
-// minimizer, stalls it to the end).  The minimizer index (get_mini_idx) is one load from a
-// dense position -> index table (pos_tab, one int32 per query base, -1 where no seeded
-// minimizer starts; built by mini_table_kernel in hymet_mm_map).  Each block finds its
+// minimizer, stalls it to the end).  The minimizer index (get_mini_idx) is one 16-byte load
+// from a position -> index table (MiniWord: start bits and a base index per 64 query bases,
+// -1 where no seeded minimizer starts; built by mini_bits/base_kernel in hymet_mm_map).  Each block finds its
 // lanes' chains by a search over the next 256 chain offsets staged in LDS; neighbours in
 // chain order come from the adjacent lanes (a load only at a wave edge); then a segmented
 // wave reduction by chain and one atomic per chain piece in the wave.  c_mlen / c_blen
@@ -159,7 +159,7 @@ struct AnchorStatParams {
 __device__ __forceinline__ int32_t mini_idx_at(const AnchorStatParams &P, int64_t q, int qlen, uint64_t ax, uint64_t ay) {
     int32_t x = (int32_t)ay;
     if (ax >> 63) x = qlen - 1 - (int32_t)ay + (int32_t)(ay >> 32 & 0xff) - 1;
-    return (x >= 0 && x < qlen) ? P.pos_tab[P.qbase[q] + x] : -1;
+    return (x >= 0 && x < qlen) ? mini_word_idx(P.mtab[(P.qbase[q] + x) >> 6], x) : -1;
 }
 
 // chain_stats_flat_kernel: kStatItems chain-order positions per thread (rows of 256 in a
@@ -250,7 +250,8 @@ __global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams 
         int32_t xq = (int32_t)y[k];
         if (x[k] >> 63) xq = qlen[k] - 1 - (int32_t)y[k] + (int32_t)(y[k] >> 32 & 0xff) - 1;
         const bool inq = xq >= 0 && xq < qlen[k];
-        const int32_t v = P.pos_tab[qb[k] + (inq ? xq : 0)];
+        const int32_t xc = inq ? xq : 0;
+        const int32_t v = mini_word_idx(P.mtab[(qb[k] + xc) >> 6], xc);
         cur[k] = act[k] && inq ? v : -1;
     }
 #pragma unroll
@@ -988,7 +989,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
                    const uint32_t *name_hash, const int32_t *rep_len, const int64_t *ref_len, int n_q, const hymet_mm_opt *o,
                    int k, void *z, hymet_mm_reg *regs, int32_t *w, uint64_t *cov, int32_t *tmp, int32_t *n_regs,
                    int64_t NB, int64_t NC, int64_t NM, const uint32_t *cq,
-                   const int32_t *pos_tab, const int64_t *qbase, const uint32_t *skip_q, uint64_t *sumk, bool sumk_done) {
+                   const MiniWord *mtab, const int64_t *qbase, const uint32_t *skip_q, uint64_t *sumk, bool sumk_done) {
     if (n_q <= 0) return HYMET_OK;
     hipStream_t st = ctx->stream;
     DevBuf cst, blk;
@@ -996,10 +997,10 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
     int32_t *c_mlen = cst.as<int32_t>(), *c_blen = c_mlen + (NC + 1), *c_st = c_blen + (NC + 1), *c_last = c_st + (NC + 1),
             *c_fv = c_last + (NC + 1);
     {
-        // chain slot (8) + anchor x, y (16) + its pos_tab read (4) per chained anchor
+        // chain slot (8) + anchor x, y (16) + its minimizer-table read (4: 16 B per 64 bases) per chained anchor
         ProfScope _ps(ctx, "mm_chain_stats", (double)NB * (8.0 + 16.0 + 4.0) + (double)NM * 8.0);
         AnchorStatParams A{ax, ay, cu, ids, cfirst, cboff, qb, qlen, mp_off, mini_pos, NB, NC, n_q, cq,
-                           c_mlen, c_blen, c_st, c_last, pos_tab, qbase, skip_q};
+                           c_mlen, c_blen, c_st, c_last, mtab, qbase, skip_q};
         if (NB > 0) {
             hipLaunchKernelGGL(chain_stats_init_kernel, dim3((unsigned)cdiv(NC + 1, 256)), dim3(256), 0, st, c_mlen, c_blen,
                                c_fv, NC + 1);

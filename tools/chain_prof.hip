@@ -49,7 +49,7 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&gs, 16));
     CK(hipMalloc(&dp, 8 * n));
     CK(hipMalloc(&order, 4));
-    CK(hipMalloc(&cnt, 4));
+    CK(hipMalloc(&cnt, 4 * kChainCtrPad * kChainStripes));  // the striped work counters (zeroed by the split kernel)
     CK(hipMalloc(&df, 4 * n));
     CK(hipMalloc(&dt, 4 * n));
     CK(hipMalloc(&qf, 1));
