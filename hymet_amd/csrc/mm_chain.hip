@@ -2204,6 +2204,8 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, kChainLds) != hipSuccess ||
         per_cu <= 0)
         per_cu = 8;
+    static const int waves_env = getenv("HYMET_CHAIN_WAVES") ? atoi(getenv("HYMET_CHAIN_WAVES")) : 0;  // A/B: resident waves per CU
+    if (waves_env > 0 && waves_env < per_cu) per_cu = waves_env;
     const int64_t cap = (int64_t)ctx->n_cu * per_cu;
     if (blocks > cap) blocks = cap;
     ProfScope _ps(ctx, max_dist > 10000 ? "mm_chain_long" : "mm_chain", 28.0 * (double)n_anchors);  // x,y read + f,p write per anchor
@@ -2241,12 +2243,12 @@ int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, c
     HY_CHECK_LAUNCH("backtrack_groups_kernel");
     if (n_work > 0) {
         ProfScope _pl(ctx, "mm_backtrack.long");  // the wave-per-group part of mm_backtrack
-        // resident waves per CU for the wave kernel (HYMET_BT_WAVES overrides); the occupancy
-        // limit (28) measured 4 % slower than 16 on C4 under the single work counter; with the
-        // striped counters 24 measured 3 % faster one-stream (112 vs 116 ms/step), 16 is kept
-        // to leave the other mapping stream room
+        // resident waves per CU for the wave kernel (HYMET_BT_WAVES overrides): 28 measured 4 %
+        // slower than 16 on C4 under the single work counter; with the striped counters 24 (the
+        // register limit) measured faster than 16, one-stream (112 vs 116 ms/step) and
+        // two-stream (1,585 vs 1,594 ms per bench step)
         const char *ew = getenv("HYMET_BT_WAVES");
-        const int per_cu = ew ? std::max(1, atoi(ew)) : 16;
+        const int per_cu = ew ? std::max(1, atoi(ew)) : 24;
         const int64_t nb = std::min<int64_t>(n_work, (int64_t)ctx->n_cu * per_cu);
         hipLaunchKernelGGL(backtrack_long_kernel, dim3((unsigned)nb), dim3(64), 0, ctx->stream, P, order,
                            cnt.as<int32_t>(), cnt.as<int32_t>() + kBtCtrPad);
