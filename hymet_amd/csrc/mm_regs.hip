@@ -194,12 +194,18 @@ __global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams 
     bool act[K];
     int32_t cnt[K], j[K], qlen[K], cur[K];
     uint64_t x[K], y[K];
+    // a block inside one chain (long chains: most blocks) skips the searches and sums its
+    // statistics over the block
+    const bool one_chain = s_st[1] >= kStatSpan;
+    int32_t t_dm = 0, t_db = 0, t_fv = INT32_MAX;
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const int r = 256 * k + (int)threadIdx.x;  // block-relative position
         const int64_t b = b0 + r;
         c[k] = -1;
-        if (b < P.NB) {
+        if (b < P.NB && one_chain) {
+            c[k] = cb0;
+        } else if (b < P.NB) {
             int lo = 0, hi = kStatSpan;  // last i with s_st[i] <= r (s_st[0] <= 0, nondecreasing)
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
@@ -294,6 +300,10 @@ __global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams 
             if (kk == 0) P.c_st[c[k]] = cur[k];
             if (kk == cnt[k] - 1) P.c_last[c[k]] = cur[k];
         }
+        if (one_chain) {  // summed over the block below: one atomic per block and counter
+            t_dm += dm, t_db += db, t_fv = min(t_fv, fv);
+            continue;
+        }
         const int32_t cr = act[k] ? ci : -1;
         // segmented inclusive reduction over lanes of the same chain (contiguous in the wave)
 #pragma unroll
@@ -307,6 +317,25 @@ __global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams 
             atomicAdd(P.c_mlen + c[k], dm);
             atomicAdd(P.c_blen + c[k], db);
             atomicMin(c_fv + c[k], fv);
+        }
+    }
+    if (one_chain) {
+        // device-scope atomics go through the fabric, not an XCD's L2: a long chain's rows
+        // each adding to the same three counters (~10^7 per launch) were the kernel's bound
+        __shared__ int32_t r_dm[4], r_db[4], r_fv[4];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            t_dm += __shfl_xor(t_dm, o, 64);
+            t_db += __shfl_xor(t_db, o, 64);
+            t_fv = min(t_fv, __shfl_xor(t_fv, o, 64));
+        }
+        const int w = threadIdx.x >> 6;
+        if (lane == 0) r_dm[w] = t_dm, r_db[w] = t_db, r_fv[w] = t_fv;
+        __syncthreads();
+        if (threadIdx.x == 0 && act[0]) {  // (a skipped query's chain: no update, as per lane)
+            atomicAdd(P.c_mlen + cb0, r_dm[0] + r_dm[1] + r_dm[2] + r_dm[3]);
+            atomicAdd(P.c_blen + cb0, r_db[0] + r_db[1] + r_db[2] + r_db[3]);
+            atomicMin(c_fv + cb0, min(min(r_fv[0], r_fv[1]), min(r_fv[2], r_fv[3])));
         }
     }
 }
