@@ -1595,12 +1595,24 @@ namespace {
 // mm_est_err's get_mini_idx (MiniWord): pass 1 sets the start bits, pass 2 writes each word's
 // base (every seeded minimizer of the word writes the same value: its index less the start
 // bits below it)
-__global__ void mini_bits_kernel(const uint64_t *my, const uint32_t *seed_n, const uint32_t *qid, const int64_t *qbase,
-                                 int64_t M, MiniWord *tab) {
+__global__ __launch_bounds__(256) void mini_bits_kernel(const uint64_t *my, const uint32_t *seed_n, const uint32_t *qid,
+                                                        const int64_t *qbase, int64_t M, MiniWord *tab) {
+    // consecutive minimizers of a query share words: the bits of a run of lanes on one word
+    // are OR-ed across the run and set by one atomic (device-scope atomics are the costly part)
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= M || !seed_n[i]) return;
-    const int64_t b = qbase[qid[i]] + ((uint32_t)my[i] >> 1);
-    atomicOr((unsigned long long *)&tab[b >> 6].bits, 1ull << (b & 63));
+    const int lane = threadIdx.x & 63;
+    const bool on = i < M && seed_n[i];
+    const int64_t b = on ? qbase[qid[i]] + ((uint32_t)my[i] >> 1) : -64 * (int64_t)(lane + 1);  // distinct dummy words
+    const int64_t w = b >> 6;
+    uint64_t bits = on ? 1ull << (b & 63) : 0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {  // OR over the lanes of the same word (runs are contiguous)
+        const int64_t wo = __shfl_down(w, d, 64);
+        const uint64_t bo = __shfl_down(bits, d, 64);
+        if (lane + d < 64 && wo == w) bits |= bo;
+    }
+    const int64_t wp = __shfl_up(w, 1, 64);
+    if (on && (lane == 0 || wp != w)) atomicOr((unsigned long long *)&tab[w].bits, bits);
 }
 __global__ void mini_base_kernel(const uint64_t *my, const uint32_t *seed_n, const uint32_t *qid, const int64_t *qm_off,
                                  const int64_t *mp_pos, const int64_t *qbase, int64_t M, MiniWord *tab) {
