@@ -198,53 +198,70 @@ __global__ __launch_bounds__(256) void chain_stats_flat_kernel(AnchorStatParams 
     // statistics over the block
     const bool one_chain = s_st[1] >= kStatSpan;
     int32_t t_dm = 0, t_db = 0, t_fv = INT32_MAX;
+    int64_t qb[K];
+    if (one_chain) {
+        // the block's one chain: its values are block-uniform (scalar loads), every position's
+        // anchor one slot further down the chain
+        const int64_t qq = (int64_t)P.cq[cb0];
+        const int32_t cn = (int32_t)P.cu[cb0];
+        const int64_t cbs = P.cboff[cb0], f00 = P.cfirst[cb0] + cn - 1;
+        const int ql = (int)P.qlen[qq];
+        const int64_t qbb = P.qbase[qq];
+        const bool sk = P.skip_q && P.skip_q[qq];
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-        const int r = 256 * k + (int)threadIdx.x;  // block-relative position
-        const int64_t b = b0 + r;
-        c[k] = -1;
-        if (b < P.NB && one_chain) {
-            c[k] = cb0;
-        } else if (b < P.NB) {
-            int lo = 0, hi = kStatSpan;  // last i with s_st[i] <= r (s_st[0] <= 0, nondecreasing)
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (s_st[mid] <= r) lo = mid;
-                else hi = mid - 1;
-            }
-            c[k] = cb0 + lo;
-            if (lo == kStatSpan) {  // beyond the staged chains (chains with no anchors in the range)
-                int64_t l2 = c[k], h2 = P.NC - 1;
-                while (l2 < h2) {
-                    const int64_t mid = (l2 + h2 + 1) >> 1;
-                    if (P.cboff[mid] <= b) l2 = mid;
-                    else h2 = mid - 1;
+        for (int k = 0; k < K; k++) {
+            const int64_t b = b0 + 256 * k + threadIdx.x;
+            c[k] = b < P.NB ? cb0 : -1;
+            q[k] = qq, cnt[k] = cn, f0[k] = f00, qlen[k] = ql, qb[k] = qbb;
+            act[k] = b < P.NB && !sk;
+            j[k] = act[k] ? (int32_t)(b - cbs) : 0;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int r = 256 * k + (int)threadIdx.x;  // block-relative position
+            const int64_t b = b0 + r;
+            c[k] = -1;
+            if (b < P.NB) {
+                int lo = 0, hi = kStatSpan;  // last i with s_st[i] <= r (s_st[0] <= 0, nondecreasing)
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_st[mid] <= r) lo = mid;
+                    else hi = mid - 1;
                 }
-                c[k] = l2;
+                c[k] = cb0 + lo;
+                if (lo == kStatSpan) {  // beyond the staged chains (chains with no anchors in the range)
+                    int64_t l2 = c[k], h2 = P.NC - 1;
+                    while (l2 < h2) {
+                        const int64_t mid = (l2 + h2 + 1) >> 1;
+                        if (P.cboff[mid] <= b) l2 = mid;
+                        else h2 = mid - 1;
+                    }
+                    c[k] = l2;
+                }
             }
         }
-    }
-    // (every load below is unconditional, at a valid index for inactive positions -- chain 0,
-    // its first slot -- so the rows' loads stay straight-line code and are all in flight
-    // before the first is used)
-    int64_t qb[K];
+        // (every load below is unconditional, at a valid index for inactive positions -- chain 0,
+        // its first slot -- so the rows' loads stay straight-line code and are all in flight
+        // before the first is used)
 #pragma unroll
-    for (int k = 0; k < K; k++) q[k] = (int64_t)P.cq[c[k] >= 0 ? c[k] : 0];
+        for (int k = 0; k < K; k++) q[k] = (int64_t)P.cq[c[k] >= 0 ? c[k] : 0];
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-        const int64_t cc = c[k] >= 0 ? c[k] : 0;
-        cnt[k] = (int32_t)P.cu[cc];
-        const int64_t cb = P.cboff[cc];
-        f0[k] = P.cfirst[cc] + cnt[k] - 1;
-        j[k] = (int32_t)(b0 + 256 * k + threadIdx.x - cb);
-        qlen[k] = (int)P.qlen[q[k]];
-        qb[k] = P.qbase[q[k]];
-    }
+        for (int k = 0; k < K; k++) {
+            const int64_t cc = c[k] >= 0 ? c[k] : 0;
+            cnt[k] = (int32_t)P.cu[cc];
+            const int64_t cb = P.cboff[cc];
+            f0[k] = P.cfirst[cc] + cnt[k] - 1;
+            j[k] = (int32_t)(b0 + 256 * k + threadIdx.x - cb);
+            qlen[k] = (int)P.qlen[q[k]];
+            qb[k] = P.qbase[q[k]];
+        }
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-        act[k] = c[k] >= 0;
-        if (P.skip_q) act[k] = act[k] && !P.skip_q[q[k]];
-        if (!act[k]) j[k] = 0;
+        for (int k = 0; k < K; k++) {
+            act[k] = c[k] >= 0;
+            if (P.skip_q) act[k] = act[k] && !P.skip_q[q[k]];
+            if (!act[k]) j[k] = 0;
+        }
     }
 #pragma unroll
     for (int k = 0; k < K; k++) {
