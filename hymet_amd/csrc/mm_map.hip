@@ -756,10 +756,7 @@ __global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
                 if (!lower) pk = last;
                 const bool desc = z && pos > 0 && key < pk;
                 const uint64_t dbal = __ballot(desc);
-                if (z) {
-                    P.zkey[g0 + pos] = key;
-                    P.z_idx[g0 + pos] = (int32_t)(g0 + i);
-                }
+                if (z) P.z_idx[g0 + pos] = (int32_t)(g0 + i);
                 if (desc) {
                     const int r = K + 1 + __popcll(dbal & below);
                     if (r < kZRuns) rs[r] = pos;
@@ -774,6 +771,29 @@ __global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
             rs[0] = 0;
             P.z_cnt[g] = m;
             P.z_runs[g] = runs;
+        }
+        if (runs > 1) {
+            // only the merge / sort paths read the keys: a group of one run (C4's colinear
+            // chains: most of them) writes its order alone, 4 B per z entry instead of 12, and
+            // the others write the keys in a second pass over f
+            int m2 = 0;
+            for (int64_t base0 = 0; base0 < n; base0 += 64 * kZDepth) {
+                int32_t fc[kZDepth];
+#pragma unroll
+                for (int d = 0; d < kZDepth; d++) {
+                    const int64_t i = base0 + 64 * d + lane;
+                    fc[d] = i < n ? P.f[g0 + i] : 0;
+                }
+#pragma unroll
+                for (int d = 0; d < kZDepth; d++) {
+                    const int64_t i = base0 + 64 * d + lane;
+                    const bool z = i < n && fc[d] >= P.min_sc;
+                    const uint64_t bal = __ballot(z);
+                    if (bal == 0) continue;
+                    if (z) P.zkey[g0 + m2 + __popcll(bal & below)] = (uint64_t)(uint32_t)fc[d] << 32 | (uint32_t)(g0 + i);
+                    m2 += __popcll(bal);
+                }
+            }
         }
         // (wave-uniform conditions)
         if (runs > 1 && runs <= P.max_runs) push(0, g);
