@@ -2056,7 +2056,9 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
 // 24 anchors (225 VGPRs, two waves per SIMD) measured fastest on the real-anchor dumps: C4
 // first pass 11.35 -> 10.7 ms, Zymo-backbone 20.3 -> 19.5 ms (16: 146 VGPRs but the wave
 // kernel single-steps the 17-24-anchor groups at ~2.3 us per anchor; 32: 262 VGPRs, one
-// wave per SIMD, 11.3 / 23.5 ms).
+// wave per SIMD, 11.3 / 23.5 ms).  Packing span, predecessor and mark into one register
+// brings 32 anchors to 227 VGPRs (two waves per SIMD), but measured no better in the bench:
+// C4 first pass 374.5 -> 371.7 ms/step, Zymo 976 -> 986 (long join 299 -> 332).
 #ifndef HYMET_CHAIN_SMALL
 #define HYMET_CHAIN_SMALL 24
 #endif
