@@ -321,15 +321,30 @@ class Pipeline:
         reused run after run, so the SketchDB.hashes of a path-built Pipeline (and of its
         RunResult.screen) are valid until the next run.  The previous tables are released
         before the new ones are built (no second copy of the tables in HBM)."""
+        self._read_dbs()
+        self._build_tables()
+
+    def _read_dbs(self):
+        """S1 host part: the .msh files parsed and their hashes gathered into pinned memory
+        (no GPU work: run() does it on a second host thread while the contigs are ingested)."""
         self.tables, self.dbs = [], []
         t0 = time.perf_counter()
         self.dbs = [read_msh(p, alloc=lambda n, i=i: self._pinned_hashes(i, n).numpy().view(np.uint64)[:n])
                     for i, p in enumerate(self.db_paths)]
+        self.timings["msh_read_s"] = time.perf_counter() - t0
+
+    def _build_tables(self):
+        """S1 device part: the pinned hashes uploaded by DMA and the HBM tables built."""
         t1 = time.perf_counter()
         self.tables = [scr.ScreenTable(self.gpu, db, pinned=self._pin[i]) for i, db in enumerate(self.dbs)]
         self.gpu.sync()
-        self.timings["msh_read_s"] = t1 - t0
         self.timings["screen_table_s"] = time.perf_counter() - t1
+
+    def _read_inputs(self):
+        """The host-only input loads of a run (.msh parse, taxonomy tables), for a second thread."""
+        if self.db_paths:
+            self._read_dbs()
+        self._load_classifier()
 
     def _load_classifier(self):
         """C1-C2: detailed_taxonomy.tsv and taxonomy_hierarchy.tsv.  classification_cami.py
@@ -514,10 +529,29 @@ class Pipeline:
     def run(self, queries, with_paf=False) -> RunResult:
         """queries: FASTA bytes, a FastaIndex, a SeqSet, or a QueryShard already resident.
         Rank 0's RunResult.tsv is the whole classified_sequences.tsv."""
+        reader, err = None, []
         if self.cfg.reload_inputs and self._ran:
-            self.load_inputs()
+            # the host-only loads (.msh parse into pinned memory, taxonomy tables) overlap the
+            # contigs' ingest; the tables are built on the GPU once both are done
+            import threading
+
+            def read():
+                try:
+                    self._read_inputs()
+                except BaseException as e:  # noqa: BLE001 -- re-raised on the calling thread
+                    err.append(e)
+            reader = threading.Thread(target=read, name="hymet-inputs")
+            reader.start()
         self._ran = True
-        sh = self.ingest(queries)
+        try:
+            sh = self.ingest(queries)
+        finally:
+            if reader is not None:
+                reader.join()
+        if err:
+            raise err[0]
+        if reader is not None and self.db_paths:
+            self._build_tables()
         selected, rows, thr = self.screen_select(sh.mash)
         if not selected:
             raise RuntimeError("candidate list empty after applying limit")  # run_hymet_cami.sh:126
