@@ -29,6 +29,7 @@ _SIGS = {
     "hymet_scratch_trim": (_i32, [_vp, _c.POINTER(_i64)]),
     "hymet_scratch_cached": (_i32, [_vp, _c.POINTER(_i64)]),
     "hymet_copy_to_host": (_i32, [_vp, _vp, _vp, _i64, _i32]),
+    "hymet_copy_to_device": (_i32, [_vp, _vp, _vp, _i64, _i32]),
     "hymet_pack": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "hymet_fasta_index": (_i32, [_vp, _i64, _i32, _i64, _c.POINTER(_i64), _vp, _vp, _vp, _vp, _vp]),
     "hymet_fasta_names": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),

@@ -275,6 +275,42 @@ int hymet_copy_to_host(hymet_ctx *ctx, void *dst, const void *src, int64_t n, in
     return HYMET_OK;
 }
 
+int hymet_copy_to_device(hymet_ctx *ctx, void *dst, const void *src, int64_t n, int threads) {
+    HY_ARG(ctx && (n == 0 || (dst && src)) && n >= 0, "hymet_copy_to_device: bad argument");
+    if (n == 0) return HYMET_OK;
+    // The mirror of hymet_copy_to_host: host threads copy chunk k into a pinned stage while
+    // chunk k-1 crosses PCIe from the other one (a pageable copy stages on one thread).
+    // Returns once the last chunk has landed (the stages are reused by the next call).
+    constexpr int64_t kChunk = 64ll << 20;
+    threads = std::max(1, std::min(threads, 64));
+    HY_HIP(hipSetDevice(ctx->device));
+    for (int k = 0; k < 2; k++) {
+        if (!ctx->stage[k]) HY_HIP(hipHostMalloc(&ctx->stage[k], kChunk, hipHostMallocDefault));
+        if (!ctx->stage_ev[k]) HY_HIP(hipEventCreateWithFlags(&ctx->stage_ev[k], hipEventDisableTiming));
+    }
+    const int64_t nch = (n + kChunk - 1) / kChunk;
+    bool pending[2] = {false, false};
+    for (int64_t c = 0; c < nch; c++) {
+        const int b = (int)(c & 1);
+        if (pending[b]) HY_HIP(hipEventSynchronize(ctx->stage_ev[b]));  // its previous DMA has read it
+        const int64_t off = c * kChunk, len = std::min(kChunk, n - off);
+        char *to = (char *)ctx->stage[b];
+        const char *from = (const char *)src + off;
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; t++) {
+            const int64_t lo = len * t / threads, hi = len * (t + 1) / threads;
+            if (lo < hi) th.emplace_back([=] { memcpy(to + lo, from + lo, (size_t)(hi - lo)); });
+        }
+        for (auto &x : th) x.join();
+        HY_HIP(hipMemcpyAsync((char *)dst + off, to, (size_t)len, hipMemcpyHostToDevice, ctx->stream));
+        HY_HIP(hipEventRecord(ctx->stage_ev[b], ctx->stream));
+        pending[b] = true;
+    }
+    for (int b = 0; b < 2; b++)
+        if (pending[b]) HY_HIP(hipEventSynchronize(ctx->stage_ev[b]));
+    return HYMET_OK;
+}
+
 int hymet_sync(hymet_ctx *ctx) {
     HY_ARG(ctx != nullptr, "hymet_sync: null ctx");
     HY_HIP(hipStreamSynchronize(ctx->stream));

@@ -20,7 +20,6 @@ from __future__ import annotations
 
 import ctypes
 import os
-import warnings
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -128,14 +127,18 @@ class PackedPool:
 
 
 def _batches(lengths: np.ndarray, max_bases: int):
-    out, b0, acc = [], 0, 0
-    for i, L in enumerate(lengths.tolist()):
-        if acc and acc + int(L) > max_bases:
-            out.append((b0, i))
-            b0, acc = i, 0
-        acc += int(L)
-    if b0 < len(lengths) or not out:
-        out.append((b0, len(lengths)))
+    """Greedy batches of consecutive records, each of at most max_bases unless a record alone
+    exceeds it: a batch closes before the record that would take it past the limit."""
+    n = len(lengths)
+    if n == 0:
+        return [(0, 0)]
+    cs = np.cumsum(np.asarray(lengths, np.int64))
+    out, b0, base = [], 0, 0
+    while b0 < n:
+        i = int(np.searchsorted(cs, base + max_bases, side="right"))  # first record past the limit
+        i = max(i, b0 + 1)
+        out.append((b0, i))
+        base, b0 = int(cs[i - 1]), i
     return out
 
 
@@ -172,10 +175,11 @@ class QueryShard:
             return cls._empty(gpu, r0, batch_bases)
         lo = int(min(fx.name_off[r0], fx.seq_off[r0]))
         hi = int(fx.seq_end[r1 - 1])
-        with warnings.catch_warnings():  # the FASTA bytes are read-only; torch only reads them
-            warnings.simplefilter("ignore")
-            raw_host = torch.frombuffer(memoryview(fx.data)[lo:hi], dtype=torch.uint8)
-        d_raw = raw_host.to(gpu.dev)
+        # one upload through the library's double-buffered pinned staging (a pageable copy
+        # staged the gigabyte on one thread)
+        d_raw = gpu.empty(max(hi - lo, 1), torch.uint8)
+        addr = ctypes.cast(fx._buf, ctypes.c_void_p).value + lo  # the record scan's pointer to the bytes
+        check(gpu.lib.hymet_copy_to_device(gpu.ctx, ptr(d_raw), ctypes.c_void_p(addr), hi - lo, 16), "hymet_copy_to_device")
         d_pool = gpu.empty(max(pool_len, 1) + 16, torch.uint8)
         d_start = gpu.empty(n, torch.int64)
         so = np.ascontiguousarray(fx.seq_off[r0:r1])

@@ -66,6 +66,10 @@ int hymet_scratch_cached(hymet_ctx *ctx, int64_t *bytes);
  * (The PAF / TSV text copy-out: resultados.paf is written by minimap2.sh:23, the TSV by
  * classification_cami.py:333-339.) */
 int hymet_copy_to_host(hymet_ctx *ctx, void *dst, const void *src, int64_t n, int threads);
+/* host -> device copy of n bytes through the same double-buffered pinned staging (threads
+ * copy chunk k while chunk k-1 is in flight); returns when the bytes are in HBM.  Uploads the
+ * FASTA bytes (ingest; classification's input is a host buffer like the reference's file). */
+int hymet_copy_to_device(hymet_ctx *ctx, void *dst, const void *src, int64_t n, int threads);
 
 /* ------------------------------------------------------- sequence packing
  * ASCII bases (device) -> 2-bit codes (16 bases per uint32, base i at bits 2*(i%16)) and an
