@@ -479,6 +479,9 @@ class Pipeline:
         """This rank's resultados.paf text (its queries' lines, part-major), written on the
         device and landed in pinned host memory by one DMA."""
         gpu, torch = self.gpu, self.gpu.torch
+        if getattr(self, "_paf_copy", None) is not None:  # a run that raised after its copy was issued
+            self._paf_copy.synchronize()
+            self._paf_copy = None
         n = self.acc.n
         if n == 0:
             return HostText(b"", 0)
@@ -512,8 +515,19 @@ class Pipeline:
                     self._paf_pin[s_] = None      # release before allocating the larger one
                     self._paf_pin[s_] = torch.empty(int(m * 1.25) + 4096, dtype=torch.uint8, pin_memory=True)
             buf = self._paf_pin[slot]
-        gpu.sync()                                # the text was written on the library's stream
-        buf[:m].copy_(out[:m])                    # one D2H DMA into pinned memory (synchronous)
+        if self.map_gpus:
+            # one D2H DMA into pinned memory on an idle mapping stream, after the text kernels
+            # (an event on this stream), overlapping the classification; run() waits for it
+            side = self.map_gpus[0].stream
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(gpu.device))
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                buf[:m].copy_(out[:m], non_blocking=True)
+            self._paf_copy = side
+        else:
+            gpu.sync()                            # the text was written on the library's stream
+            buf[:m].copy_(out[:m])                # one D2H DMA into pinned memory (synchronous)
         t = HostText(buf.numpy(), m)
         import weakref
         self._paf_holders[slot] = weakref.ref(t)
@@ -574,6 +588,9 @@ class Pipeline:
         if total_rows < 1:  # fewer than 2 TSV lines: run_hymet_cami.sh:182-206
             tsv = self._fallback(ix, sh)
             n_rows = n_cls = 0
+        if getattr(self, "_paf_copy", None) is not None:
+            self._paf_copy.synchronize()          # the PAF text has landed in host memory
+            self._paf_copy = None
         return RunResult(selected, rows, thr, tsv, n_rows, n_cls, n_lines, paf_text, self.last_screen)
 
     def _global_names(self, sh: QueryShard):
