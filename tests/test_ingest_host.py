@@ -58,3 +58,29 @@ def test_fasta_index_threaded_large():
     assert max(per) - min(per) <= 2 * int(fx.nbases.max())
     pool, off = fx.name_pool(5, 9)
     assert pool.tobytes() == b"".join(n.split()[0].encode() for n in names[5:9]) and off[-1] == len(pool)
+
+
+def _greedy_batches(lengths, max_bases):
+    """The batching rule spelled out record by record: a batch closes before the record
+    that would take it past max_bases (a record longer than that sits alone)."""
+    out, b0, acc = [], 0, 0
+    for i, L in enumerate(lengths):
+        if acc and acc + int(L) > max_bases:
+            out.append((b0, i))
+            b0, acc = i, 0
+        acc += int(L)
+    if b0 < len(lengths) or not out:
+        out.append((b0, len(lengths)))
+    return out
+
+
+def test_mapping_batches_match_the_greedy_rule():
+    from hymet_amd.ingest import _batches
+    rng = np.random.default_rng(5)
+    for _ in range(500):
+        n = int(rng.integers(0, 80))
+        lengths = rng.integers(1, 120, size=n)
+        if n and rng.random() < 0.3:  # records longer than a batch
+            lengths[rng.integers(0, n, size=min(n, 3))] = rng.integers(150, 600, size=min(n, 3))
+        max_bases = int(rng.integers(1, 400))
+        assert _batches(lengths, max_bases) == _greedy_batches(lengths, max_bases)
