@@ -164,8 +164,10 @@ class QueryShard:
         return int(self.lengths.sum())
 
     @classmethod
-    def from_fasta(cls, gpu, fx: FastaIndex, r0: int = 0, r1: Optional[int] = None, batch_bases: int = 40_000_000):
-        """One H2D copy of the records' contiguous byte range, then device-side compaction."""
+    def from_fasta(cls, gpu, fx: FastaIndex, r0: int = 0, r1: Optional[int] = None, batch_bases: int = 40_000_000,
+                   d_all=None):
+        """One H2D copy of the records' contiguous byte range, then device-side compaction.
+        d_all: the whole input already in HBM (uploaded while the records were scanned)."""
         torch = gpu.torch
         r1 = fx.n if r1 is None else r1
         n = r1 - r0
@@ -175,11 +177,15 @@ class QueryShard:
             return cls._empty(gpu, r0, batch_bases)
         lo = int(min(fx.name_off[r0], fx.seq_off[r0]))
         hi = int(fx.seq_end[r1 - 1])
-        # one upload through the library's double-buffered pinned staging (a pageable copy
-        # staged the gigabyte on one thread)
-        d_raw = gpu.empty(max(hi - lo, 1), torch.uint8)
-        addr = ctypes.cast(fx._buf, ctypes.c_void_p).value + lo  # the record scan's pointer to the bytes
-        check(gpu.lib.hymet_copy_to_device(gpu.ctx, ptr(d_raw), ctypes.c_void_p(addr), hi - lo, 16), "hymet_copy_to_device")
+        if d_all is not None:
+            d_raw, lo = d_all, 0
+        else:
+            # one upload through the library's double-buffered pinned staging (a pageable copy
+            # staged the gigabyte on one thread)
+            d_raw = gpu.empty(max(hi - lo, 1), torch.uint8)
+            addr = ctypes.cast(fx._buf, ctypes.c_void_p).value + lo  # the record scan's pointer to the bytes
+            check(gpu.lib.hymet_copy_to_device(gpu.ctx, ptr(d_raw), ctypes.c_void_p(addr), hi - lo, 16),
+                  "hymet_copy_to_device")
         d_pool = gpu.empty(max(pool_len, 1) + 16, torch.uint8)
         d_start = gpu.empty(n, torch.int64)
         so = np.ascontiguousarray(fx.seq_off[r0:r1])

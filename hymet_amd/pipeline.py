@@ -333,17 +333,27 @@ class Pipeline:
                     for i, p in enumerate(self.db_paths)]
         self.timings["msh_read_s"] = time.perf_counter() - t0
 
-    def _build_tables(self):
-        """S1 device part: the pinned hashes uploaded by DMA and the HBM tables built."""
+    def _build_tables(self, side=None):
+        """S1 device part: the pinned hashes uploaded by DMA and the HBM tables built -- on
+        this context's stream, or on `side` (an idle mapping context, from the loader thread,
+        overlapping the ingest; that thread waits for side's stream before run() joins it)."""
         t1 = time.perf_counter()
-        self.tables = [scr.ScreenTable(self.gpu, db, pinned=self._pin[i]) for i, db in enumerate(self.dbs)]
-        self.gpu.sync()
+        if side is None:
+            self.tables = [scr.ScreenTable(self.gpu, db, pinned=self._pin[i]) for i, db in enumerate(self.dbs)]
+            self.gpu.sync()
+        else:
+            with self.gpu.torch.cuda.stream(side.stream):
+                self.tables = [scr.ScreenTable(side, db, pinned=self._pin[i]) for i, db in enumerate(self.dbs)]
+            side.stream.synchronize()
         self.timings["screen_table_s"] = time.perf_counter() - t1
 
-    def _read_inputs(self):
-        """The host-only input loads of a run (.msh parse, taxonomy tables), for a second thread."""
+    def _read_inputs(self, side=None):
+        """The run's input loads for a second host thread: .msh parse (+ the HBM tables on
+        `side`'s stream when given), taxonomy tables."""
         if self.db_paths:
             self._read_dbs()
+            if side is not None:
+                self._build_tables(side)
         self._load_classifier()
 
     def _load_classifier(self):
@@ -378,11 +388,37 @@ class Pipeline:
         rank) -> QueryShard resident in HBM."""
         if isinstance(queries, QueryShard):
             return queries
+        d_all = None
         if isinstance(queries, (bytes, bytearray, memoryview)):
-            queries = FastaIndex(bytes(queries))
+            data = bytes(queries)
+            if self.world == 1 and len(data):
+                # one rank takes every record: the bytes go up on a second thread while the
+                # record table is scanned (the staged copy and the scan both read host memory)
+                import threading
+                torch = self.gpu.torch
+                d_all = self.gpu.empty(len(data), torch.uint8)
+                up_err = []
+
+                def upload():
+                    try:
+                        check(self.gpu.lib.hymet_copy_to_device(self.gpu.ctx, ptr(d_all), data, len(data), 16),
+                              "hymet_copy_to_device")
+                    except BaseException as e:  # noqa: BLE001 -- re-raised below
+                        up_err.append(e)
+                up = threading.Thread(target=upload, name="hymet-upload")
+                up.start()
+                try:
+                    queries = FastaIndex(data)
+                finally:
+                    up.join()
+                if up_err:
+                    raise up_err[0]
+            else:
+                queries = FastaIndex(data)
         if isinstance(queries, FastaIndex):
             r0, r1 = queries.shard(self.rank, self.world)
-            sh = QueryShard.from_fasta(self.gpu, queries, r0, r1, self.cfg.map_batch_bases)
+            sh = QueryShard.from_fasta(self.gpu, queries, r0, r1, self.cfg.map_batch_bases,
+                                       d_all=d_all if (r0, r1) == (0, queries.n) else None)
             sh.fasta = queries
             return sh
         if isinstance(queries, SeqSet):
@@ -544,14 +580,15 @@ class Pipeline:
         """queries: FASTA bytes, a FastaIndex, a SeqSet, or a QueryShard already resident.
         Rank 0's RunResult.tsv is the whole classified_sequences.tsv."""
         reader, err = None, []
+        side = self.map_gpus[0] if self.map_gpus else None
         if self.cfg.reload_inputs and self._ran:
-            # the host-only loads (.msh parse into pinned memory, taxonomy tables) overlap the
-            # contigs' ingest; the tables are built on the GPU once both are done
+            # the input loads (.msh parse into pinned memory and, with a mapping context to
+            # spare, the HBM tables on its stream; taxonomy tables) overlap the contigs' ingest
             import threading
 
             def read():
                 try:
-                    self._read_inputs()
+                    self._read_inputs(side)
                 except BaseException as e:  # noqa: BLE001 -- re-raised on the calling thread
                     err.append(e)
             reader = threading.Thread(target=read, name="hymet-inputs")
@@ -564,7 +601,7 @@ class Pipeline:
                 reader.join()
         if err:
             raise err[0]
-        if reader is not None and self.db_paths:
+        if reader is not None and self.db_paths and side is None:
             self._build_tables()
         selected, rows, thr = self.screen_select(sh.mash)
         if not selected:
