@@ -237,7 +237,10 @@ def format_screen(db: SketchDB, shared, median, set_size, v_max=0.9, identity_mi
     r = 1.0 - math.pow(1.0 - 1.0 / kmer_space, float(set_size))
     out = []
     off = db.offsets
-    for i in range(db.n_refs):
+    # rows with no shared hash are dropped unless identity_min < 0: visit only the others
+    # (a Python pass over every reference of a 100k-reference DB cost ~5 ms per step)
+    rows = np.flatnonzero(np.asarray(shared)[:db.n_refs]) if identity_min >= 0.0 else range(db.n_refs)
+    for i in rows:
         x = int(shared[i])
         if x == 0 and identity_min >= 0.0:
             continue
