@@ -521,6 +521,121 @@ def cpu_baseline_cami(args, pipe, res, fasta, db, tax, hier, budget_s=None, must
     return out
 
 
+# ------------------------------------------------------------- one rank of N, emulated
+def bench_emulate(args, gpu, torch):
+    """`--emulate-rank R[,R2...]/N`: bound the N-GPU step from one GPU.  A one-rank run of the
+    workload (untimed cold run, then `--steps` timed steps for the one-rank reference) records
+    the job-wide results of every exchange step -- screen hit counts in the DB's hash order,
+    the pool's bottom-s sketch and k-mer total, per-target PAF line counts, the LCA rows.
+    Then each listed rank runs alone, `--steps` timed steps of exactly what it does in an
+    N-rank job (its contiguous record shard, plus everything the code replicates on every
+    rank), with every collective replaced by a local stand-in that returns the job-wide value
+    (hymet_amd.dist.EmulatedComm).  The bytes each collective would move are modelled over
+    xGMI (EmulatedComm.model_ms) and added: predicted step = max over the emulated ranks of
+    (measured rank step + modelled transfers).  A prediction, not a measured scaling curve."""
+    from hymet_amd import pipeline, screen as scr
+    from hymet_amd.dist import Comm, EmulatedComm
+    from hymet_amd.ingest import FastaIndex
+    ranks_s, world_s = args.emulate_rank.split("/")
+    N = int(world_s)
+    ranks = [int(r) for r in ranks_s.split(",")]
+    if N < 2 or any(r < 0 or r >= N for r in ranks):
+        raise SystemExit(f"--emulate-rank {args.emulate_rank}: want R[,R...]/N with 0 <= R < N, N >= 2")
+    w, db, pipe1, fasta, refs_ss, tax, hier, td = build_cami(args, Comm(), gpu)
+    glob = {}
+    orig_reduce = scr.reduce_partials
+    orig_rows = pipe1.classify_rows
+
+    def capture_screen(comm, counts, bottom, nk, s, tables=None):
+        glob["screen_by_hash"] = [c[t.slot_of[:t.n_hashes]].clone() for c, t in zip(counts, tables)]
+        glob["bottom"] = np.asarray(bottom, np.uint64).copy()
+        glob["nk"] = int(nk)
+        return orig_reduce(comm, counts, bottom, nk, s, tables)
+
+    def capture_rows(ix, sh):
+        import ctypes
+        rws, n = orig_rows(ix, sh)
+        glob["rows"] = {k: v.clone() for k, v in rws.items()}
+        glob["n_rows"] = n
+        counts = gpu.zeros(max(len(ix.names), 1), torch.int32)
+        gpu.call("hymet_acc_ref_counts", pipe1.acc.h, ctypes.c_void_p(counts.data_ptr()))
+        glob["ref_counts"] = counts
+        return rws, n
+
+    scr.reduce_partials, pipe1.classify_rows = capture_screen, capture_rows
+    t0 = time.time()
+    try:
+        res1 = pipe1.run(fasta, with_paf=True)
+    finally:
+        scr.reduce_partials, pipe1.classify_rows = orig_reduce, orig_rows
+    gpu.sync()
+    log(f"one-rank cold run {time.time()-t0:.1f}s: {len(res1.selected)} candidates, {res1.n_queries} rows")
+
+    def timed(pipe, steps, warmup):
+        for _ in range(warmup):
+            pipe.run(fasta, with_paf=True)
+        gpu.sync()
+        gpu.prof_reset()
+        gpu.prof(True)
+        phases = {}
+        if isinstance(pipe.comm, EmulatedComm):
+            pipe.comm.reset_log()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r = pipe.run(fasta, with_paf=True)
+            for k, v in pipe.phases.items():
+                phases[k] = phases.get(k, 0.0) + v
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        gpu.prof(False)
+        prof = gpu.prof_table()
+        return r, dt, {k: v * 1e3 / steps for k, v in phases.items()}, {k: v[0] / steps for k, v in prof.items()}
+
+    _, t1, ph1, st1 = timed(pipe1, args.steps, max(0, args.warmup - 1))
+    log(f"one rank: {t1*1e3:.1f} ms/step")
+    fx = FastaIndex(fasta)
+    out_ranks = {}
+    for R in ranks:
+        r0, r1 = fx.shard(R, N)
+        glob["shard_n"] = r1 - r0
+        comm = EmulatedComm(R, N, glob)
+        pipe_e = pipeline.Pipeline(gpu, pipe1.db_paths, pipe1.ref_lookup, tax, hier, pipe1.cfg, comm)
+        pipe_e.index_cache = pipe1.index_cache
+        pipe_e.run(fasta, with_paf=True)               # cold: pinned buffers, contexts
+        res_e, te, phe, ste = timed(pipe_e, args.steps, max(0, args.warmup - 1))
+        per_step = [(k, b) for k, b in comm.log[:len(comm.log) // max(args.steps, 1)]]
+        model = EmulatedComm.model_ms(per_step, N)
+        out_ranks[str(R)] = {
+            "shard_records": [int(r0), int(r1)], "shard_mbp": float(fx.nbases[r0:r1].sum()) / 1e6,
+            "ms_per_step": te * 1e3, "phases_ms": phe, "stage_ms_per_step": ste,
+            "collectives_per_step": [{"kind": k, "bytes_per_rank": int(b)} for k, b in per_step],
+            "xgmi_model_ms": model, "predicted_ms_per_step": te * 1e3 + model,
+            "tsv_rows": res_e.n_queries, "paf_lines": res_e.n_paf_lines}
+        if R == 0:
+            out_ranks[str(R)]["tsv_identical_to_one_rank"] = res_e.tsv == res1.tsv
+        log(f"rank {R}/{N}: {te*1e3:.1f} ms/step + {model:.1f} ms modelled xGMI")
+        pipe_e.acc.close()
+        for a in pipe_e.map_accs:
+            a.close()
+        del pipe_e, comm
+        import gc
+        gc.collect()
+        gpu.lib.hymet_scratch_trim(gpu.ctx, None)
+    pred = max(v["predicted_ms_per_step"] for v in out_ranks.values())
+    meas = max(v["ms_per_step"] for v in out_ranks.values())
+    # T_N = A + B / N and T_1 = A + B: the part of the step that does not shrink with N
+    fixed = (N * meas - t1 * 1e3) / (N - 1)
+    return {"metric": METRIC + " (emulated)", "emulated_world": N, "emulated_ranks": ranks, "steps": args.steps,
+            "warmup": args.warmup, "one_rank_ms_per_step": t1 * 1e3, "one_rank_phases_ms": ph1,
+            "one_rank_stage_ms_per_step": st1, "ranks": out_ranks, "predicted_ms_per_step": pred,
+            "predicted_speedup_vs_one_rank": t1 * 1e3 / pred, "predicted_contigs_per_s": len(w.contigs) / (pred / 1e3),
+            "non_shardable_ms_per_step": fixed,
+            "model": "predicted = max over the emulated ranks of (its measured step with local stand-ins for the "
+                     "collectives + ring transfers of the recorded bytes at 100 GB/s per rank + 30 us per collective); "
+                     "non_shardable = (N * max rank step - one-rank step) / (N - 1), from T = A + B / N",
+            "config": {"workload": args.workload_name, "contigs": len(w.contigs), "contig_mbp": w.contig_bases / 1e6}}
+
+
 # ------------------------------------------------------------------- screen only
 def bench_screen(args, comm, gpu, torch):
     from hymet_amd import screen as scr, synth
@@ -627,7 +742,7 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="cami-medium", choices=["cami-medium", "cami-medium-zymo", "cami-high", "screen"])
-    ap.add_argument("--contig-gbp", type=float, default=1.0)
+    ap.add_argument("--contig-gbp", type=float, default=None, help="Gbp of contigs (default: 1.0; cami-high 2.0)")
     ap.add_argument("--taxa", type=int, default=12)
     ap.add_argument("--per-taxon", type=int, default=62)
     ap.add_argument("--batch-mbp", type=float, default=None,
@@ -647,6 +762,9 @@ def parse_args(argv=None):
                     help="rank r uses GPU r %% device_count (rehearse N ranks on fewer GPUs; use with --backend gloo)")
     ap.add_argument("--dry-run", action="store_true", help="CPU rehearsal of the N-rank launch and sharding (gloo, no GPU)")
     ap.add_argument("--tsv-out", default=None, help="rank 0 writes the last step's classified_sequences.tsv here")
+    ap.add_argument("--emulate-rank", default=None, metavar="R[,R...]/N",
+                    help="run rank R of an N-rank job alone on this GPU, collectives replaced by stand-ins "
+                         "(bench_emulate: a predicted N-GPU step, not a measurement)")
     args = ap.parse_args(argv)
     # CAMI-high (C5, BASELINE.json configs[4]): 14 taxa (tools/generate_cami_subsets.py:343),
     # the full CAND_MAX of 5000 candidates (~20 Gbp, ten -I2g parts), ~2 Gbp of contigs,
@@ -654,12 +772,13 @@ def parse_args(argv=None):
     if args.workload == "cami-high":
         args.taxa = 14
         args.per_taxon = [358] * 2 + [357] * 12
-        args.contig_gbp = 2.0
+        args.contig_gbp = args.contig_gbp or 2.0
         args.db_hashes = args.db_hashes or "1e8,5e7,1e7"
         args.workload_name = "CAMI-high (C5)"
         # 5000 candidates: ~6x C4's anchors per query base, so smaller mapping batches
         args.batch_mbp = args.batch_mbp or 40.0
     else:
+        args.contig_gbp = args.contig_gbp or 1.0
         args.db_hashes = args.db_hashes or "1e8"
         # C4: 60 Mbp batches measured 2327 ms/step vs 2460 (30) and ~2390 (40); scratch 148 GB
         args.batch_mbp = args.batch_mbp or 60.0
@@ -686,6 +805,12 @@ def main():
         return
     import torch
     from hymet_amd._lib import Gpu
+    if args.emulate_rank:
+        if comm.world != 1:
+            raise SystemExit("--emulate-rank runs in one process")
+        gpu = Gpu(0)
+        print(json.dumps(bench_emulate(args, gpu, torch)), flush=True)
+        return
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.share_gpu:
         local %= max(1, torch.cuda.device_count())

@@ -142,6 +142,7 @@ class Gpu:
     def bind_stream(self, stream=None):
         s = stream if stream is not None else self.torch.cuda.current_stream(self.device)
         check(self.lib.hymet_set_stream(self.ctx, _vp(s.cuda_stream)), "hymet_set_stream")
+        self.bound_stream = s   # the torch stream object the library's kernels run on
 
     def call(self, name, *args):
         check(getattr(self.lib, name)(self.ctx, *args), name)

@@ -12,8 +12,14 @@
 // iteration order, so every confidence is bit-identical (built with -ffp-contract=off).
 //
 // lca_refcount_kernel: global per-target PAF line counts (atomics; an int32 histogram).
-// lca_kernel: one thread per query, lines of the query in PAF order (CSR); insertion-ordered
-// "dicts" are arrays in a per-query scratch slice sized by its line count.
+// lca_wave_kernel: one wave per query (row), lines of the query in PAF order (CSR).  The
+// reference's insertion-ordered dicts (taxid -> weight, then per rank name -> weight) become
+// LDS hash tables whose entries are numbered in first-appearance order; every floating-point
+// sum is still taken sequentially in the reference's order (lines, then taxids, then names),
+// lane-parallel only across distinct keys.  A thread per query with linear-search dicts cost
+// O(lines x taxids) per query: 550 ms per step at CAMI-high, ~350 lines and ~350 distinct
+// strain taxids per contig.  Rows of more than kLcaLines lines take lca_row_seq, the
+// one-thread form, on global scratch sized by the line count.
 #include "common.hpp"
 #include "mm_common.hpp"
 #include "sort.hpp"
@@ -50,9 +56,7 @@ __global__ void lca_refcount_kernel(const int32_t *line_t, int64_t n, int32_t *c
     if (i < n && line_t[i] >= 0) atomicAdd(&counts[line_t[i]], 1);
 }
 
-__global__ __launch_bounds__(64) void lca_kernel(LcaParams P) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= P.n_q) return;
+__device__ void lca_row_seq(const LcaParams &P, int q) {
     const int64_t l0 = P.q_off[q], l1 = P.q_off[q + 1];
     int32_t *tids = P.scr_tid + l0;
     double *tw = P.scr_w + l0;
@@ -164,6 +168,224 @@ __global__ __launch_bounds__(64) void lca_kernel(LcaParams P) {
             conf *= nw[b];
             depth = r + 1;
         }
+        P.out_depth[q] = depth;
+        P.out_conf[q] = depth ? (conf < 1.0 ? conf : 1.0) : 0.0;
+    }
+}
+
+constexpr int kLcaLines = 512;            // rows of up to this many lines run in LDS
+constexpr int kLcaSlots = 2 * kLcaLines;  // open-addressing slots (a power of two)
+
+__device__ __forceinline__ double lca_rld(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+// One 64-lane round of inserts into an insertion-ordered LDS dict: lanes with `act` look up
+// `key` (>= 0); keys not seen before are numbered cnt, cnt + 1, ... in the order of their
+// first occurrence `pos` (lane order within the round = the reference's iteration order).
+// Returns the key's number (-1 for inactive lanes).  One wave per block: __syncthreads orders
+// the LDS accesses of the round.
+__device__ __forceinline__ int lca_dict_round(int32_t *skey, int32_t *sfirst, int32_t *sidx, int32_t key, int32_t pos,
+                                              bool act, int &cnt) {
+    const int lane = threadIdx.x;
+    uint32_t h = 0;
+    if (act) {
+        h = ((uint32_t)key * 2654435761u) >> 22;  // 10 bits: kLcaSlots
+        for (;;) {
+            const int32_t cur = atomicCAS(&skey[h], -1, key);
+            if (cur == -1 || cur == key) break;
+            h = (h + 1) & (kLcaSlots - 1);
+        }
+        atomicMin(&sfirst[h], pos);
+    }
+    __syncthreads();
+    const bool first = act && sidx[h] == -1 && sfirst[h] == pos;
+    const uint64_t mf = __ballot(first);
+    if (first) sidx[h] = cnt + __popcll(mf & ((1ull << lane) - 1));
+    __syncthreads();
+    const int idx = act ? sidx[h] : -1;
+    cnt += __popcll(mf);
+    return idx;
+}
+
+__device__ __forceinline__ void lca_dict_reset(int32_t *skey, int32_t *sfirst, int32_t *sidx) {
+    __syncthreads();
+    for (int s = threadIdx.x; s < kLcaSlots; s += 64) skey[s] = -1, sfirst[s] = INT32_MAX, sidx[s] = -1;
+    __syncthreads();
+}
+
+// sums[i] for i = base + lane < n_out: the values val[k] (k in [0, n_in), ascending) whose
+// idx[k] == i, added in k order from 0.0 -- the reference's `d[key] += v` over its loop
+__device__ __forceinline__ double lca_sum_by(const int32_t *idx, const double *val, int n_in, int base) {
+    const int lane = threadIdx.x;
+    const int me = base + lane;
+    double acc = 0.0;
+    for (int kb = 0; kb < n_in; kb += 64) {
+        const int k = kb + lane;
+        const int ik = k < n_in ? idx[k] : -1;
+        const double vk = k < n_in ? val[k] : 0.0;
+        for (uint64_t m = __ballot(ik >= base && ik < base + 64); m; m &= m - 1) {
+            const int u = __ffsll((unsigned long long)m) - 1;
+            const double v = lca_rld(vk, u);
+            if (__builtin_amdgcn_readlane(ik, u) == me) acc += v;
+        }
+    }
+    return acc;
+}
+
+// first maximal (value, index) over lanes: larger value, ties -> smaller index (max() over an
+// insertion-ordered dict); e < 0 = none
+__device__ __forceinline__ void lca_first_max(double &v, int &e) {
+    for (int d = 1; d < 64; d <<= 1) {
+        const double ov = __hiloint2double(__shfl_xor(__double2hiint(v), d, 64), __shfl_xor(__double2loint(v), d, 64));
+        const int oe = __shfl_xor(e, d, 64);
+        if (oe >= 0 && (e < 0 || ov > v || (ov == v && oe < e))) v = ov, e = oe;
+    }
+}
+
+__global__ __launch_bounds__(64) void lca_wave_kernel(LcaParams P) {
+    __shared__ int32_t skey[kLcaSlots], sfirst[kLcaSlots], sidx[kLcaSlots];
+    __shared__ int32_t line_j[kLcaLines], j_tid[kLcaLines], j_e[kLcaLines], e_name[kLcaLines];
+    __shared__ double line_w[kLcaLines], j_w[kLcaLines];
+    const int q = blockIdx.x, lane = threadIdx.x;
+    const int64_t l0 = P.q_off[q], l1 = P.q_off[q + 1];
+    const int m = (int)(l1 - l0);
+    if (l1 - l0 > kLcaLines) {
+        if (lane == 0) lca_row_seq(P, q);
+        return;
+    }
+    if (lane == 0) P.out_tax[q] = -1;
+    if (P.mode == 1) {  // legacy exact shortcut: only the first exact line with a taxid is tried
+        for (int kb = 0; kb < m; kb += 64) {
+            const int k = kb + lane;
+            int32_t tid = -1;
+            if (k < m) {
+                const int32_t t = P.line_t[l0 + k];
+                if (P.line_exact[l0 + k] && t >= 0) tid = P.t_tax[t];
+            }
+            const uint64_t mx = __ballot(tid >= 0);
+            if (mx) {
+                const int32_t tid0 = __builtin_amdgcn_readlane(tid, __ffsll((unsigned long long)mx) - 1);
+                if (P.tax_in_hier[tid0]) {
+                    if (lane == 0) P.out_depth[q] = -1, P.out_tax[q] = tid0, P.out_conf[q] = 1.0;
+                    return;
+                }
+                break;  // classification.py:145-151
+            }
+        }
+    }
+    // taxid dict in line order: line_j = the line's taxid number, line_w its weight
+    lca_dict_reset(skey, sfirst, sidx);
+    int nt = 0;
+    bool any = false;
+    for (int kb = 0; kb < m; kb += 64) {
+        const int k = kb + lane;
+        int32_t t = -1, tid = -1;
+        double w = 0.0;
+        if (k < m) {
+            t = P.line_t[l0 + k];
+            if (t >= 0) tid = P.t_tax[t];
+            if (tid >= 0) {
+                const int64_t ql = P.line_qlen[l0 + k];
+                const double cov = ql > 0 ? (double)P.line_blen[l0 + k] / (double)ql : 0.0;
+                w = cov * (double)P.ref_counts[t];
+            }
+        }
+        const bool valid = tid >= 0;
+        any = any || __ballot(valid) != 0;
+        const int j = lca_dict_round(skey, sfirst, sidx, tid, k, valid, nt);
+        if (valid) j_tid[j] = tid;
+        if (k < m) line_j[k] = j, line_w[k] = w;
+    }
+    if (lane == 0) P.out_depth[q] = 0, P.out_conf[q] = 0.0;
+    if (!any) return;
+    __syncthreads();
+    for (int jb = 0; jb < nt; jb += 64) {  // tw[j] += w over the lines, in line order
+        const double acc = lca_sum_by(line_j, line_w, m, jb);
+        if (jb + lane < nt) j_w[jb + lane] = acc;
+    }
+    __syncthreads();
+    double conf = 1.0;
+    int depth = 0;
+    if (P.mode == 0) {
+        double tot = 0.0;  // sum(taxid_weights.values()), dict order
+        for (int jb = 0; jb < nt; jb += 64) {
+            const double v = jb + lane < nt ? j_w[jb + lane] : 0.0;
+            for (int u = 0; u < min(64, nt - jb); u++) tot += lca_rld(v, u);
+        }
+        if (!(tot > 0.0)) return;
+        for (int r = 0; r < kRanks; r++) {
+            lca_dict_reset(skey, sfirst, sidx);
+            int nn = 0;
+            double denom = 0.0;
+            for (int jb = 0; jb < nt; jb += 64) {
+                const int j = jb + lane;
+                const int32_t name = j < nt ? P.tax_names[(int64_t)j_tid[j] * kRanks + r] : -1;
+                const bool ok = name >= 0;  // no hierarchy row or empty name at this rank: skipped
+                const double wj = j < nt ? j_w[j] : 0.0;
+                const int e = lca_dict_round(skey, sfirst, sidx, name, j, ok, nn);
+                if (ok) e_name[e] = name;
+                if (j < nt) j_e[j] = e;
+                for (uint64_t mm = __ballot(ok); mm; mm &= mm - 1) denom += lca_rld(wj, __ffsll((unsigned long long)mm) - 1);
+            }
+            if (!(denom > 0.0) || nn == 0) break;
+            __syncthreads();
+            double bv = 0.0;
+            int be = -1;
+            for (int eb = 0; eb < nn; eb += 64) {
+                const double acc = lca_sum_by(j_e, j_w, nt, eb);
+                if (eb + lane < nn && (be < 0 || acc > bv)) bv = acc, be = eb + lane;
+            }
+            lca_first_max(bv, be);
+            if (lane == 0) P.out_names[q * kRanks + r] = e_name[be];
+            conf *= bv / denom;
+            depth = r + 1;
+        }
+    } else {
+        double total = 0.0;  // sum of the weights of every line with a taxid, line order
+        for (int kb = 0; kb < m; kb += 64) {
+            const int k = kb + lane;
+            const bool v = k < m && line_j[k] >= 0;
+            const double w = v ? line_w[k] : 0.0;
+            for (uint64_t mm = __ballot(v); mm; mm &= mm - 1) total += lca_rld(w, __ffsll((unsigned long long)mm) - 1);
+        }
+        if (total == 0.0) return;
+        int nl = 0;
+        for (int jb = 0; jb < nt; jb += 64) {  // wn = w / total per lineage in the hierarchy
+            const int j = jb + lane;
+            const bool inh = j < nt && P.tax_in_hier[j_tid[j]];
+            nl += __popcll(__ballot(inh));
+            if (j < nt) line_w[j] = j_w[j] / total;
+        }
+        if (nl == 0) return;
+        __syncthreads();
+        for (int r = 0; r < kRanks; r++) {
+            lca_dict_reset(skey, sfirst, sidx);
+            int nn = 0;
+            for (int jb = 0; jb < nt; jb += 64) {
+                const int j = jb + lane;
+                const int32_t tid = j < nt ? j_tid[j] : -1;
+                const int32_t part = tid >= 0 && P.tax_in_hier[tid] ? P.tax_names[(int64_t)tid * kRanks + r] : -1;
+                const bool ok = part >= 0;
+                const int e = lca_dict_round(skey, sfirst, sidx, part, j, ok, nn);
+                if (ok) e_name[e] = part;
+                if (j < nt) j_e[j] = e;
+            }
+            if (nn == 0) break;
+            __syncthreads();
+            double bv = 0.0;
+            int be = -1;
+            for (int eb = 0; eb < nn; eb += 64) {
+                const double acc = lca_sum_by(j_e, line_w, nt, eb);
+                if (eb + lane < nn && (be < 0 || acc > bv)) bv = acc, be = eb + lane;
+            }
+            lca_first_max(bv, be);
+            if (lane == 0) P.out_names[q * kRanks + r] = e_name[be];
+            conf *= bv;
+            depth = r + 1;
+        }
+    }
+    if (lane == 0) {
         P.out_depth[q] = depth;
         P.out_conf[q] = depth ? (conf < 1.0 ? conf : 1.0) : 0.0;
     }
@@ -359,8 +581,8 @@ int hymet_acc_classify(hymet_ctx *ctx, const hymet_paf_acc *acc, int mode, int32
                 lq.as<int64_t>(), le.as<uint8_t>(), d_ref_counts,      d_t_tax,            d_tax_names,
                 d_tax_in_hier, s_tid.as<int32_t>(), s_w.as<double>(),  s_nm.as<int32_t>(), s_nw.as<double>(),
                 d_row_depth,   d_row_names,     d_row_conf,            d_row_tax};
-    hipLaunchKernelGGL(lca_kernel, dim3((unsigned)hymet::cdiv(R, 64)), dim3(64), 0, st, P);
-    HY_CHECK_LAUNCH("lca_kernel");
+    hipLaunchKernelGGL(lca_wave_kernel, dim3((unsigned)R), dim3(64), 0, st, P);
+    HY_CHECK_LAUNCH("lca_wave_kernel");
     return HYMET_OK;
 }
 
@@ -388,8 +610,8 @@ int hymet_lca(hymet_ctx *ctx, int mode, int32_t n_q, const int64_t *d_q_off, con
                 d_ref_counts,  d_t_tax,      d_tax_names, d_tax_in_hier, d_scr_tid,   d_scr_w,     d_scr_nm,
                 d_scr_nw,      d_out_depth,  d_out_names, d_out_conf,  d_out_tax};
     hymet::ProfScope _ps(ctx, "lca");
-    hipLaunchKernelGGL(lca_kernel, dim3((unsigned)hymet::cdiv(n_q, 64)), dim3(64), 0, ctx->stream, P);
-    HY_CHECK_LAUNCH("lca_kernel");
+    hipLaunchKernelGGL(lca_wave_kernel, dim3((unsigned)n_q), dim3(64), 0, ctx->stream, P);
+    HY_CHECK_LAUNCH("lca_wave_kernel");
     return HYMET_OK;
 }
 

@@ -120,6 +120,12 @@ namespace {
 #ifndef HYMET_CHAIN_HNOP
 #define HYMET_CHAIN_HNOP 1
 #endif
+// A window that anchor i-1 leaves empties whole (x never decreases along a group): st / st_in
+// jump to i and the deques and the inner list are cleared in O(1), instead of one probe round
+// (and a head-cache load beyond the rings) per 64 entries passed.
+#ifndef HYMET_CHAIN_DRAIN
+#define HYMET_CHAIN_DRAIN 0
+#endif
 // Wave-uniform loop state pinned to scalar registers (readfirstlane at the derivation points):
 // branches on it become scalar branches instead of exec-mask bookkeeping (first pass 11.55 ->
 // 11.27 ms, long join 7.27 -> 7.07 ms on the real-anchor dump; VALU -9 % per anchor).
@@ -1001,6 +1007,14 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     hsuf_ok = false;
                 }
             };
+#if HYMET_CHAIN_DRAIN
+            // every entry before i has x <= prev.x: when anchor i-1 is out of the window, all are
+            if (st < i && (int64_t)(uint32_t)xi > (int64_t)(uint32_t)prev.x + P.max_dist) {
+                st = i;
+                bh = bt;    // no complete block is left in the window
+                bok = true;  // the (empty) block deque is exact again
+            }
+#endif
             for (;;) {
                 if (st >= i) break;
 #if HYMET_CHAIN_BLX
@@ -1064,6 +1078,15 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             // ---- 3. inner window start
             AMARK(stin_begin);
             if (P.max_dist_inner > 0) {
+#if HYMET_CHAIN_DRAIN
+                if (st_in < i && (int64_t)(uint32_t)xi > (int64_t)(uint32_t)prev.x + P.max_dist_inner) {
+                    st_in = i;
+                    ni = 0, lh = 0;
+                    overflow = false;  // the list holds exactly [st_in, i0): empty
+                    ih = it;
+                    iok = true;
+                }
+#endif
                 for (;;) {
                     if (st_in >= i) break;
                     const int32_t j = st_in + lane;

@@ -383,6 +383,11 @@ __global__ __launch_bounds__(64) void query_sumk_kernel(const uint64_t *mini_pos
 constexpr int kRegWave = 48;
 constexpr int kRegSmall = 256;  // the wave kernel holds a query's regions in LDS up to this many
 constexpr int kRegEntryBytes = 16 + 16 + 4 * 3 + 8;  // slot, aux, wl, psub, pns, covb per entry
+// global scratch of the wave kernel per chain: a query of n > kRegSmall chains takes m < 2n
+// entries at qc[q] * kRegScrStride -- 112 = 2 x 56 B keeps every query's base 16-byte aligned
+// for the int4 / U128 accesses (104 B per chain left odd qc[q] 8-byte aligned)
+constexpr int kRegScrStride = 2 * ((kRegEntryBytes + 15) & ~15) - 16;
+static_assert(kRegScrStride % 16 == 0 && kRegScrStride >= 2 * kRegEntryBytes, "regions scratch stride");
 
 __device__ __forceinline__ bool wave_query(const RegParams &P, int q, int n, int32_t qlen) {
     return n > P.wave_min && qlen != 0 && !(P.skip_q && P.skip_q[q]);
@@ -690,8 +695,8 @@ __global__ __launch_bounds__(64) void regions_wave_kernel(RegParams P, const int
             regions_wave(P, q, rsm, kRegSmall);
         } else {
             int m = 64;
-            while (m < n) m <<= 1;  // < 2n: the query's share of gscratch (104 B per chain) holds it
-            regions_wave(P, q, gscratch + (size_t)P.qc[q] * 2 * kRegEntryBytes, m);
+            while (m < n) m <<= 1;  // < 2n: the query's share of gscratch (kRegScrStride per chain) holds it
+            regions_wave(P, q, gscratch + (size_t)P.qc[q] * kRegScrStride, m);
         }
         __threadfence_block();
         wsync();
@@ -1090,7 +1095,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
     }
     DevBuf big, gscr;
     HY_HIP(big.alloc(4 * (size_t)n_q, st));
-    HY_HIP(gscr.alloc(2 * (size_t)kRegEntryBytes * (size_t)(NC + 1), st));
+    HY_HIP(gscr.alloc((size_t)kRegScrStride * (size_t)(NC + 1), st));
     int32_t *n_big = ctx->dctr + kCtrRegBig;  // self-clearing (regions_wave_kernel's last block)
     hipLaunchKernelGGL(regions_kernel, dim3((unsigned)cdiv(n_q, 64)), dim3(64), 0, st, P, big.as<int32_t>(), n_big);
     HY_CHECK_LAUNCH("regions_kernel");

@@ -52,10 +52,25 @@ __device__ __forceinline__ uint64_t block_excl(uint64_t v, uint64_t *ws, uint64_
     return before + inc - v;
 }
 
-// The hand-off of the tile sums to the last block (MI355X_MICROARCH.md, inter-workgroup
-// visibility, first row of the measured sc1 table): lane 0 of every block stores its sum with
+// The hand-off of the tile sums to the last block: lane 0 of every block stores its sum with
 // an sc1 store, waits for it (vmcnt(0)), then adds to the ticket; the block whose add returns
 // nb - 1 reads every sum with sc1 loads.  No fence, no dependence on dispatch order.
+// Why this is sound on gfx950 without a release/acquire pair (the LLVM AMDGPU memory model
+// for the GFX942 family, which gfx950 belongs to):
+//   * a relaxed atomic store / load at agent scope is emitted as global_store / global_load
+//     with sc1 set: it bypasses the XCD-private L2 caching of the line and is performed at the
+//     device's coherence point, so it is coherent across the eight XCDs by itself;
+//   * the store's vmcnt decrement happens when that write is acknowledged at the coherence
+//     point, so the s_waitcnt vmcnt(0) orders the completed store before the ticket's atomic
+//     RMW, which is itself performed at the coherence point;
+//   * the last block issues its sc1 loads only after its own RMW returned nb - 1 (the value
+//     is consumed through LDS and s_barrier), i.e. after every other block's RMW, each of
+//     which followed that block's completed store.
+// A release fetch_add would add buffer_wbl2 (an L2 write-back of the whole XCD's dirty lines)
+// per block -- the cost DESIGN.md §3 measured for agent-scope fences in the backtrack kernel
+// -- for no ordering the sc1 accesses do not already give.  The guide's measured hand-off
+// table (MI355X_MICROARCH.md, inter-workgroup visibility, first row) is this pattern;
+// tests/test_sort_gpu.py runs it at ~9,800 tiles per call under a concurrent second stream.
 __device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -165,3 +165,107 @@ class Comm:
     def close(self):
         if self.dist is not None and self.dist.is_initialized():
             self.dist.destroy_process_group()
+
+
+class EmulatedComm(Comm):
+    """Rank `rank` of a `world`-rank job, run alone in one process (bench.py --emulate-rank):
+    every collective is replaced by a local stand-in that returns the job-wide result, taken
+    from a one-rank run of the same input (`glob`), and the bytes each collective would move
+    over xGMI are recorded for the transfer model.  No process group exists; the rank does
+    exactly its own shard's work plus everything the real code replicates on every rank.
+
+    glob: "screen_by_hash" -> [device tensor per DB, hash order], "bottom" -> np.uint64,
+    "nk" -> int, "ref_counts" -> device int32 per target, "rows" -> the one-rank LCA rows
+    (query index = global index), "n_rows" -> int."""
+
+    def __init__(self, rank: int, world: int, glob: dict):
+        super().__init__(rank, world)
+        import torch
+        self.torch = torch
+        self.glob = glob
+        self.log: List[tuple] = []   # (kind, bytes per rank) of every collective since reset_log
+
+    def reset_log(self):
+        self.log = []
+
+    def allreduce_sum_(self, t):
+        for g in self.glob["screen_by_hash"] + [self.glob["ref_counts"]]:
+            if g.numel() == t.numel() and g.dtype == t.dtype:
+                t.copy_(g)
+                self.log.append(("allreduce", t.numel() * t.element_size()))
+                return t
+        raise ValueError(f"EmulatedComm: no job-wide value for an all-reduce of {t.numel()} x {t.dtype}")
+
+    def allgather_np(self, arr: np.ndarray) -> List[np.ndarray]:
+        arr = np.asarray(arr)
+        self.log.append(("allgather", arr.nbytes))
+        if arr.dtype == np.uint64:           # screen: the ranks' bottom-s candidates
+            return [np.asarray(self.glob["bottom"], np.uint64)]
+        if arr.dtype == np.int64 and arr.shape == (1,):   # screen: the ranks' k-mer totals
+            return [np.array([self.glob["nk"]], np.int64)]
+        raise ValueError(f"EmulatedComm: no job-wide value for an all-gather of {arr.dtype} {arr.shape}")
+
+    def gather_rows(self, rows, q_base: int, gpu=None):
+        """Rank 0 merges its own rows with the other ranks' (from the one-rank run) and sorts
+        them exactly as Comm.gather_rows does; other ranks return nothing."""
+        torch = self.torch
+        R = int(rows["q"].shape[0])
+        dev = rows["q"].device
+        g = self.glob["rows"]
+        n_all = int(g["q"].shape[0])
+        self.log.append(("allgather", max(R, 1) * (12 * 4 + 8)))
+        if self.rank != 0:
+            e = torch.zeros(0, dtype=torch.int32, device=dev)
+            return {"q": e, "part": e, "depth": e, "tax": e, "names": e,
+                    "conf": torch.zeros(0, dtype=torch.float64, device=dev)}, 0
+        rec = torch.zeros((max(R, 1), 12), dtype=torch.int32, device=dev)
+        if R:
+            rec[:R, 0] = rows["q"] + int(q_base)
+            rec[:R, 1] = rows["part"]
+            rec[:R, 2] = rows["depth"]
+            rec[:R, 3] = rows["tax"]
+            rec[:R, 4:] = rows["names"].view(R, 8)
+        grec = torch.zeros((max(n_all, 1), 12), dtype=torch.int32, device=dev)
+        if n_all:
+            grec[:n_all, 0] = g["q"]
+            grec[:n_all, 1] = g["part"]
+            grec[:n_all, 2] = g["depth"]
+            grec[:n_all, 3] = g["tax"]
+            grec[:n_all, 4:] = g["names"].view(n_all, 8)
+        lo, hi = int(q_base), int(q_base) + int(self.glob.get("shard_n", 0))
+        other = (grec[:n_all, 0] < lo) | (grec[:n_all, 0] >= hi)
+        allr = torch.cat([rec[:R], grec[:n_all][other]])
+        allc = torch.cat([rows["conf"][:R], g["conf"][:n_all][other]])
+        key = allr[:, 1].to(torch.int64) * (1 << 32) + allr[:, 0].to(torch.int64)
+        order = torch.sort(key, stable=True).indices
+        allr, allc = allr[order], allc[order]
+        n = int(allr.shape[0])
+        return {"q": allr[:, 0].contiguous(), "part": allr[:, 1].contiguous(), "depth": allr[:, 2].contiguous(),
+                "tax": allr[:, 3].contiguous(), "names": allr[:, 4:].contiguous().view(-1), "conf": allc.contiguous()}, n
+
+    def broadcast_obj(self, obj, src: int = 0):
+        return obj if self.rank == src else self.glob["n_rows"]
+
+    def gather_obj(self, obj, dst: int = 0):
+        raise NotImplementedError("EmulatedComm: the fallback path is not emulated")
+
+    def barrier(self):
+        pass
+
+    def max_float(self, v: float) -> float:
+        return v
+
+    def close(self):
+        pass
+
+    @staticmethod
+    def model_ms(log, world: int, gbps: float = 100.0, latency_us: float = 30.0) -> float:
+        """xGMI transfer model of the recorded collectives (ring algorithms): an all-reduce of
+        B bytes per rank moves 2 (N-1)/N B per rank, an all-gather of B bytes per rank
+        (N-1) B, at `gbps` per rank (a conservative RCCL bus bandwidth over xGMI), plus a
+        fixed latency per collective."""
+        ms = 0.0
+        for kind, b in log:
+            moved = 2.0 * (world - 1) / world * b if kind == "allreduce" else (world - 1) * b
+            ms += latency_us / 1e3 + moved / (gbps * 1e9) * 1e3
+        return ms

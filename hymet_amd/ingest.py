@@ -238,7 +238,9 @@ class QueryShard:
         mm = PackedPool(gpu, d_pool, pool_len, DevicePool.ALPHA_MINIMAP2)
         qlen = torch.from_numpy(lengths).to(gpu.dev)
         pool_np = np.frombuffer(pool_b, np.uint8) if isinstance(pool_b, (bytes, bytearray)) else pool_b
-        qname = torch.from_numpy(np.ascontiguousarray(pool_np) if len(pool_np) else np.zeros(1, np.uint8)).to(gpu.dev)
+        # np.frombuffer over bytes is read-only: copy before torch.from_numpy (it warns on
+        # non-writable arrays); the copy is the name pool only (~10 B per contig)
+        qname = torch.from_numpy(np.array(pool_np, np.uint8, copy=True) if len(pool_np) else np.zeros(1, np.uint8)).to(gpu.dev)
         qname_off = torch.from_numpy(pool_off).to(gpu.dev)
         return cls(n, q_base, lengths, starts, mash, mm, qlen, d_hash, qname, qname_off, _batches(lengths, batch_bases))
 

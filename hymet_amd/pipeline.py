@@ -78,6 +78,10 @@ class HostText:
         self._buf, self.n, self._bytes = buf, int(n), None
 
     def view(self) -> memoryview:
+        """A zero-copy view of the text.  It stays valid only while this HostText (or the
+        RunResult holding it) is referenced: copy-on-reuse tracks the HostText, not views of
+        it, so a view kept past the HostText's lifetime may see a later run's text.  Use
+        bytes() for a copy that lives on its own."""
         if self._bytes is not None:
             return memoryview(self._bytes)
         return memoryview(self._buf)[:self.n]
@@ -556,7 +560,7 @@ class Pipeline:
             # (an event on this stream), overlapping the classification; run() waits for it
             side = self.map_gpus[0].stream
             ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(gpu.device))
+            ev.record(gpu.bound_stream)          # the stream hymet_emit_paf wrote the text on
             side.wait_event(ev)
             with torch.cuda.stream(side):
                 buf[:m].copy_(out[:m], non_blocking=True)
@@ -594,6 +598,13 @@ class Pipeline:
             reader = threading.Thread(target=read, name="hymet-inputs")
             reader.start()
         self._ran = True
+        ph = self.phases = {}   # host wall seconds of the run's phases (bench.py --emulate-rank)
+        tp = [time.perf_counter()]
+
+        def lap(name):
+            t = time.perf_counter()
+            ph[name] = ph.get(name, 0.0) + t - tp[0]
+            tp[0] = t
         try:
             sh = self.ingest(queries)
         finally:
@@ -601,26 +612,33 @@ class Pipeline:
                 reader.join()
         if err:
             raise err[0]
+        lap("ingest_s")
         if reader is not None and self.db_paths and side is None:
             self._build_tables()
         selected, rows, thr = self.screen_select(sh.mash)
         if not selected:
             raise RuntimeError("candidate list empty after applying limit")  # run_hymet_cami.sh:126
+        lap("screen_select_s")
         ix = self.index_for(selected)
         n_lines = self.map_all(ix, sh)
+        lap("map_s")
         paf_text = self.emit_paf(ix, sh) if with_paf else None
+        lap("emit_paf_s")
         tsv, n_rows, n_cls = b"", 0, 0
         if self.classifier is not None:
             rws, R = self.classify_rows(ix, sh)
+            lap("classify_s")
             if self.world > 1:
                 rws, R = self.comm.gather_rows(rws, sh.q_base, self.gpu)
                 qname, qname_off = self._global_names(sh)
             else:
                 qname, qname_off = sh.qname, sh.qname_off
+            lap("gather_rows_s")
             if self.rank == 0:
                 tsv = self.emit_tsv(rws, R, qname, qname_off)
                 n_rows = R
                 n_cls = int((rws["depth"] != 0).sum().item()) if R else 0
+            lap("emit_tsv_s")
         total_rows = self.comm.broadcast_obj(n_rows) if self.world > 1 else n_rows
         if total_rows < 1:  # fewer than 2 TSV lines: run_hymet_cami.sh:182-206
             tsv = self._fallback(ix, sh)
@@ -628,6 +646,7 @@ class Pipeline:
         if getattr(self, "_paf_copy", None) is not None:
             self._paf_copy.synchronize()          # the PAF text has landed in host memory
             self._paf_copy = None
+        lap("finish_s")
         return RunResult(selected, rows, thr, tsv, n_rows, n_cls, n_lines, paf_text, self.last_screen)
 
     def _global_names(self, sh: QueryShard):

@@ -8,8 +8,8 @@ C4 / C5 in tests/test_configs_large_gpu.py).
   hashes, the sketch1 size of BASELINE.md / SURVEY.md §8(d)).
   Counts, shared, median, set size, screen.tab rows and the mash.sh selection bit-exact vs
   the CPU oracle.
-* C3 CAMI-low: 8 taxa, 147 candidate genomes (bench/results_summary.md:90), 10,000
-  contigs, one index part, end to end (screen -> select -> limit -> index -> map ->
+* C3 CAMI-low: 8 taxa, 147 candidate genomes of 3-5 Mbp (0.58 Gbp; bench/results_summary.md:90),
+  15,130 contigs / 100 Mbp, one index part, end to end (screen -> select -> limit -> index -> map ->
   classify) vs oracle/pipeline_oracle: selected candidates, PAF lines and TSV bytes
   identical, with one mapping batch and again with many.
 * A Pipeline reused on a second, repeat-rich candidate set resolves mid_occ from that set
@@ -172,12 +172,14 @@ def test_config_c1_tiny_main_pl_path(gpu, tmp_path):
 
 
 def _cami_low():
+    """147 candidate genomes of 3-5 Mbp (~0.6 Gbp, bench/results_summary.md:90)
+    and ~100 Mbp of contigs (~15k at CAMI's lognormal lengths)."""
     from hymet_amd import synth
     rng = np.random.default_rng(2)
     per = [19, 19, 19, 18, 18, 18, 18, 18]
-    w = synth.make_cami(rng, n_taxa=8, per_taxon=per, genome_mbp=(0.6, 1.0), contig_gbp=0.1, max_contigs=10_000,
-                        name="cami-low")
-    assert len(w.refs) == 147 and len(w.contigs) == 10_000
+    w = synth.make_cami(rng, n_taxa=8, per_taxon=per, contig_gbp=0.1, max_contigs=20_000, name="cami-low")
+    assert len(w.refs) == 147 and 0.5e9 < w.ref_bases < 0.7e9
+    assert 0.099e9 <= w.contig_bases < 0.11e9 and len(w.contigs) > 14_000
     return w, rng
 
 
@@ -215,7 +217,9 @@ def _lookups(*ws):
 @pytest.mark.timeout(900)
 def test_config_c3_cami_low_end_to_end(gpu, tmp_path):
     """BASELINE.json configs[2] "CAMI-low subset: full sketch->limit_candidates->
-    minimizer-chain->classify on 1 MI355X"."""
+    minimizer-chain->classify on 1 MI355X", at SURVEY.md §8(d)'s shape: 147 candidates /
+    0.58 Gbp in one -I2g part, 15,130 contigs / 100 Mbp.  The oracle maps the whole pool on
+    the host's cores (~100 s on 8 threads, ~60 s on the GPU box's 16)."""
     from hymet_amd import pipeline
     from hymet_amd.seqio import from_records
     from oracle import pipeline_oracle
@@ -233,7 +237,7 @@ def test_config_c3_cami_low_end_to_end(gpu, tmp_path):
     assert res.selected == o_sel
     assert len(res.paf) == len(o_paf) and res.paf == o_paf
     assert res.tsv == o_tsv
-    assert res.n_classified >= 9500
+    assert res.n_classified >= 0.95 * len(w.contigs)
     # the same pool cut into many mapping batches on two streams: identical bytes
     p.cfg.map_batch_bases = 7_000_000
     res2 = p.run(queries, with_paf=True)

@@ -257,3 +257,39 @@ def test_map_streams_one_and_two_identical(gpu, tmp_path):
     assert out[1].paf == out[2].paf
     assert out[1].tsv == out[2].tsv
     assert len(out[1].paf) > 50
+
+
+def test_msh_pipeline_three_runs_keep_results(gpu, tmp_path):
+    """The bench's own configuration on a small input: a Pipeline built from .msh PATHS
+    (reload_inputs: every run re-parses the DB files on the loader thread and builds the
+    screen tables on the idle mapping stream), two mapping streams, FASTA bytes in, PAF text
+    in the alternating pinned buffers.  Run three times while the FIRST result's PAF text is
+    still referenced: its bytes must survive runs 2 and 3 (copy-on-reuse), and every run's
+    screen arrays, PAF and TSV must equal the first run's."""
+    from hymet_amd import pipeline
+    from hymet_amd.msh import write_msh
+    from hymet_amd.seqio import from_records
+    w, db, by_name, tax, hier = _setup(gpu, tmp_path)
+    msh = tmp_path / "sketch1.msh"
+    write_msh(db, str(msh))
+    data = _fasta_text(w, quote_name=False)
+
+    def ref_lookup(names):
+        return from_records([(by_name[n][0], "", by_name[n][1]) for n in names])
+
+    cfg = pipeline.Config(map_batch_bases=200_000, map_streams=2, reload_inputs=True)
+    p = pipeline.Pipeline(gpu, [str(msh)], ref_lookup, str(tax), str(hier), cfg)
+    first = p.run(data, with_paf=True)
+    first_view = first.paf_text.view()      # zero-copy while `first` is alive
+    first_copy = bytes(first_view)
+    sh0 = [r.shared.copy() for r in first.screen]
+    md0 = [r.median.copy() for r in first.screen]
+    assert len(first_copy) > 1000 and first.tsv.count(b"\r\n") > 50
+    for _ in range(2):
+        r = p.run(data, with_paf=True)
+        assert r.paf_bytes == first_copy
+        assert r.tsv == first.tsv and r.selected == first.selected
+        for a, b, res in zip(sh0, md0, r.screen):
+            np.testing.assert_array_equal(res.shared, a)
+            np.testing.assert_array_equal(res.median, b)
+        assert first.paf_bytes == first_copy       # the held result was copied out before reuse

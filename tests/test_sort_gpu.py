@@ -57,3 +57,48 @@ def test_scan_exclusive_sum_and_running_max(gpu, n):
     d_m = torch.empty(n, dtype=torch.int32, device=gpu.dev)
     gpu.call("hymet_scan_u32", ctypes.c_void_p(d_v.data_ptr()), ctypes.c_void_p(d_m.data_ptr()), n, 1, None)
     np.testing.assert_array_equal(d_m.cpu().numpy(), np.maximum.accumulate(v))
+
+
+def test_scan_many_tiles_while_another_stream_scans(gpu):
+    """The tile-sum hand-off (sc1 stores, a vmcnt wait, then the ticket add; the last block's
+    sc1 loads) at ~9,800 tiles per call, 12 calls in a row, while a second library context
+    runs the same scans on its own stream from another thread: every offset and total exact
+    (a stale tile sum read by the last block would shift every later offset)."""
+    import threading
+    torch = gpu.torch
+    n = 40_000_000
+    side = gpu.fork()
+    rng = np.random.default_rng(5)
+    cnt = [rng.integers(0, 3000, n, dtype=np.uint32) for _ in range(2)]
+    want = []
+    for c in cnt:
+        w = np.zeros(n, np.int64)
+        np.cumsum(c[:-1], out=w[1:])
+        want.append((w, int(c.sum(dtype=np.int64))))
+    errs = []
+
+    def run(g, k):
+        try:
+            with torch.cuda.stream(g.stream):   # torch's copies on the context's own stream
+                body(g, k)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(repr(e))
+
+    def body(g, k):
+        d_in = torch.from_numpy(cnt[k].view(np.int32)).to(g.dev)
+        d_out = torch.empty(n, dtype=torch.int64, device=g.dev)
+        tot = ctypes.c_int64()
+        for _ in range(12):
+            d_out.fill_(-1)
+            g.call("hymet_scan_u32", ctypes.c_void_p(d_in.data_ptr()), ctypes.c_void_p(d_out.data_ptr()), n, 0,
+                   ctypes.byref(tot))
+            got = d_out.cpu().numpy()
+            if tot.value != want[k][1] or not np.array_equal(got, want[k][0]):
+                errs.append(f"context {k}: mismatch at {int(np.argmax(got != want[k][0]))}")
+                return
+
+    th = threading.Thread(target=run, args=(side, 1))
+    th.start()
+    run(gpu, 0)
+    th.join()
+    assert not errs, errs
