@@ -394,9 +394,9 @@ def shard_balance(gpu, pipe, fasta, worlds=(2, 4, 8)):
     fx = FastaIndex(fasta)
     anchors = np.bincount(q, weights=cm[:len(q)].astype(np.float64), minlength=fx.n)
     bases = np.asarray(fx.nbases, np.float64)
-    out = {"model": "contiguous base-balanced shards; cost = chained anchors (sum of cm) per contig"}
+    out = {"model": "contiguous byte-range shards (ingest.shard_bytes); cost = chained anchors (sum of cm) per contig"}
     for n in worlds:
-        cuts = [fx.shard(r, n) for r in range(n)]
+        cuts = fx.byte_shards(n)
         a = np.array([anchors[r0:r1].sum() for r0, r1 in cuts])
         b = np.array([bases[r0:r1].sum() for r0, r1 in cuts])
         out[str(n)] = {"anchors_max_over_mean": float(a.max() / a.mean()), "bases_max_over_mean": float(b.max() / b.mean())}
@@ -593,10 +593,19 @@ def bench_emulate(args, gpu, torch):
 
     _, t1, ph1, st1 = timed(pipe1, args.steps, max(0, args.warmup - 1))
     log(f"one rank: {t1*1e3:.1f} ms/step")
+    # the one-rank pipeline's mapping contexts keep their scratch blocks cached; the emulated
+    # rank's contexts are new streams and would otherwise push the cache past its cap
+    gpu.sync()
+    gpu.lib.hymet_scratch_trim(gpu.ctx, None)
     fx = FastaIndex(fasta)
+    shards = fx.byte_shards(N)          # the records each rank's byte range holds (ingest.shard_bytes)
+    glob["shard_records"] = [r1 - r0 for r0, r1 in shards]
+    pool, off = fx.name_pool()
+    glob["names"] = (torch.from_numpy(pool.copy() if len(pool) else np.zeros(1, np.uint8)).to(gpu.dev),
+                     torch.from_numpy(off).to(gpu.dev))
     out_ranks = {}
     for R in ranks:
-        r0, r1 = fx.shard(R, N)
+        r0, r1 = shards[R]
         glob["shard_n"] = r1 - r0
         comm = EmulatedComm(R, N, glob)
         pipe_e = pipeline.Pipeline(gpu, pipe1.db_paths, pipe1.ref_lookup, tax, hier, pipe1.cfg, comm)
@@ -715,20 +724,25 @@ def launch_ranks(n: int) -> int:
 
 def bench_dry(args, comm):
     """CPU rehearsal of the multi-rank launch (no GPU, gloo): every rank builds the same
-    synthetic FASTA, takes its record shard exactly as Pipeline.ingest does
-    (FastaIndex.shard), and the ranks all-reduce their contig and base counts; rank 0
-    reports the world and checks the shards cover the input once."""
+    synthetic FASTA, indexes only its byte range exactly as Pipeline.ingest does
+    (ingest.shard_bytes, the ranks' record counts all-gathered for the query base), and the
+    ranks all-reduce their contig and base counts; rank 0 reports the world and checks the
+    shards cover the input once."""
     import torch
     from hymet_amd import ingest, synth
     from hymet_amd.ingest import FastaIndex
     w = synth.make_cami(np.random.default_rng(1234), n_taxa=2, per_taxon=2, genome_mbp=(0.2, 0.3),
                         contig_gbp=0.002, contig_rng=np.random.default_rng(5000), max_contigs=400)
-    fx = FastaIndex(ingest.to_fasta(list(w.contig_names), w.contigs))
-    r0, r1 = fx.shard(comm.rank, comm.world)
-    t = torch.tensor([r1 - r0, int(sum(len(w.contigs[i]) for i in range(r0, r1)))], dtype=torch.int64)
+    data = ingest.to_fasta(list(w.contig_names), w.contigs)
+    fx = FastaIndex(data, byte_range=ingest.shard_bytes(data, comm.rank, comm.world))
+    counts = comm.allgather_np(np.array([fx.n], np.int64), tag="shard_records")
+    r0 = int(sum(int(c[0]) for c in counts[:comm.rank]))
+    r1 = r0 + fx.n
+    assert fx.names() == list(w.contig_names[r0:r1])
+    t = torch.tensor([r1 - r0, int(fx.nbases.sum())], dtype=torch.int64)
     comm.allreduce_sum_(t)
     spans = comm.allgather_np(np.array([r0, r1], np.int64))
-    ok = int(t[0]) == fx.n and int(t[1]) == w.contig_bases and all(int(a[1]) == int(b[0]) for a, b in zip(spans, spans[1:]))
+    ok = int(t[0]) == len(w.contigs) and int(t[1]) == w.contig_bases and all(int(a[1]) == int(b[0]) for a, b in zip(spans, spans[1:]))
     return {"metric": METRIC, "value": None, "unit": "contigs/s", "n_gpus": comm.world, "dry_run": True,
             "backend": comm.dist.get_backend() if comm.dist is not None else None, "shards": [[int(a[0]), int(a[1])] for a in spans],
             "contigs": int(t[0]), "bases": int(t[1]), "covers_input_once": bool(ok)}

@@ -467,6 +467,121 @@ __device__ __forceinline__ int4 pack_st(double pr, int32_t j, int32_t y) {
 }
 __device__ __forceinline__ double st_pr(const int4 &v) { return __hiloint2double(v.y, v.x); }
 
+// Groups of at most kMidMax anchors (and more than the lane kernel's kSmall) are chained by a
+// wave with one LANE PER ANCHOR, the whole group in registers (chain_mid_group): the window
+// trees become 64-bit lane masks, the RMQ one wave argmin, the inner walk one pass in the
+// (y, idx) order through the same prefix scans the wave kernel's walk uses.  The general path
+// single-steps these groups (repeat hits that do not chain colinearly) at ~2.2 us per anchor
+// through its LDS list / deque / block-summary upkeep.  0 disables.
+#ifndef HYMET_CHAIN_MID
+#define HYMET_CHAIN_MID 0
+#endif
+constexpr int kMidMax = HYMET_CHAIN_MID;
+
+// mg_lchain_rmq on one group of n <= 64 anchors, lane l = anchor l (lchain.c; the same
+// decisions as chain_small_kernel's lane replay and the general path).  scr: 128 ints of LDS.
+__device__ __forceinline__ void chain_mid_group(const ChainParams &P, int64_t g0, int n, bool qfirst, double c,
+                                                int32_t *scr) {
+    const int lane = threadIdx.x;
+    const bool act = lane < n;
+    const int jl = act ? lane : n - 1;
+    const uint64_t xv = P.ax[g0 + jl], yv = P.ay[g0 + jl];
+    const int32_t X = (int32_t)xv, Y = (int32_t)yv, SP = (int32_t)(yv >> 32 & 0xff);
+    // walk order: the anchors by (y, idx) descending; lane w of the walk holds anchor wa
+    int rank = 0;
+    for (int m = 0; m < n; ++m) {
+        const int32_t ym = __builtin_amdgcn_readlane(Y, m);
+        rank += (ym < Y || (ym == Y && m < lane)) ? 1 : 0;
+    }
+    int32_t *perm = scr, *stamp = scr + 64;
+    __builtin_amdgcn_wave_barrier();
+    if (act) perm[n - 1 - rank] = lane;
+    __builtin_amdgcn_wave_barrier();
+    const int wa = act ? perm[lane] : 0;
+    const int32_t wX = __shfl(X, wa, 64), wY = __shfl(Y, wa, 64), wSP = __shfl(SP, wa, 64);
+    int32_t F = 0, PJ = -1;
+    double PR = 0.0;
+    uint64_t in_out = 0, in_in = 0;
+    int i0 = 0, st = 0, st_in = 0;
+    for (int i = 0; i < n; ++i) {
+        const int32_t xi = __builtin_amdgcn_readlane(X, i), yi = __builtin_amdgcn_readlane(Y, i);
+        int32_t max_f = __builtin_amdgcn_readlane(SP, i), max_j = -1;
+        if (i0 < i && __builtin_amdgcn_readlane(X, i0) != xi) {  // [i0, i) enter both trees
+            const uint64_t mk = (i >= 64 ? ~0ull : (1ull << i) - 1) & ~((1ull << i0) - 1);
+            in_out |= mk;
+            if (P.max_dist_inner > 0) in_in |= mk;
+            if (mk >> lane & 1) PR = prio(F, X, Y, c);
+            i0 = i;
+        }
+        // window starts: x never decreases along the group, so the leaving entries are a
+        // prefix of [st, i) (the tree-size cap is >= 64 on this path: never binding)
+        {
+            const uint64_t lv = __ballot(lane >= st && lane < i && (int64_t)(uint32_t)xi > (int64_t)(uint32_t)X + P.max_dist);
+            const int st2 = st + __popcll(lv);
+            in_out &= ~((st2 >= 64 ? ~0ull : (1ull << st2) - 1) & ~((1ull << st) - 1));
+            st = st2;
+        }
+        if (P.max_dist_inner > 0) {
+            const uint64_t lv =
+                __ballot(lane >= st_in && lane < i && (int64_t)(uint32_t)xi > (int64_t)(uint32_t)X + P.max_dist_inner);
+            const int s2 = st_in + __popcll(lv);
+            in_in &= ~((s2 >= 64 ? ~0ull : (1ull << s2) - 1) & ~((1ull << st_in) - 1));
+            st_in = s2;
+        }
+        // RMQ over (yi - max_dist, yi); the query's anchor 0 also at y == yi; ties -> larger index
+        const int32_t ylo = yi - P.max_dist;
+        const bool cand = (in_out >> lane & 1) && Y > ylo && (Y < yi || (Y == yi && qfirst && lane == 0));
+        double bp = cand ? PR : 0.0;
+        int32_t bj = cand ? lane : -1, dummy = 0;
+        wave_argmin(bp, bj, dummy);
+        bj = U(bj);
+        if (bj >= 0) {
+            int32_t exact, width;
+            const int32_t fb = __builtin_amdgcn_readlane(F, bj);
+            const int32_t sc = fb + comput_sc(xi, yi, __builtin_amdgcn_readlane(X, bj), __builtin_amdgcn_readlane(Y, bj),
+                                              __builtin_amdgcn_readlane(SP, bj), P.pen_gap, P.pen_skip, &exact, &width);
+            if (width <= P.bw && sc > max_f) max_f = sc, max_j = bj;
+            if (!exact && in_in != 0 && yi > 0) {
+                // inner walk: tree entries with y <= yi - 1 by (y, idx) descending, down to
+                // yi - max_dist_inner -- in walk lanes, a prefix scan of the sequential loop
+                const int32_t wF = __shfl(F, wa, 64), wPJ = __shfl(PJ, wa, 64);
+                const bool inw = act && (in_in >> wa & 1) && wY <= yi - 1 && wY >= yi - P.max_dist_inner;
+                int32_t ex2, w2;
+                const int32_t sc2 = wF + comput_sc(xi, yi, wX, wY, wSP, P.pen_gap, P.pen_skip, &ex2, &w2);
+                const bool valid = inw && w2 <= P.bw;
+                // t[p[q]] = i by every valid candidate q: candidate j is stamped when an earlier
+                // one (walk order) points to it
+                stamp[lane] = 64;
+                __builtin_amdgcn_wave_barrier();
+                if (valid && wPJ >= 0) atomicMin(&stamp[wPJ], lane);
+                __builtin_amdgcn_wave_barrier();
+                const bool stamped = valid && stamp[wa] < lane;
+                const int incl = scan_max(valid ? sc2 : INT32_MIN);
+                const int excl = max(shr1(incl, INT32_MIN), max_f);
+                const bool imp = valid && sc2 > excl;
+                int a = imp ? -1 : (stamped ? 1 : 0);
+                int bb = imp ? 0 : kNegInf;
+                scan_maxplus(a, bb);
+                const int sk = max(a, bb);
+                const uint64_t mB = __ballot(valid && !imp && stamped && sk > P.max_chn_skip);
+                const int lim = mB ? __ffsll((unsigned long long)mB) : 64;  // lanes < lim are reached
+                const uint64_t mI = __ballot(imp && lane < lim);
+                if (mI) {
+                    const int Lh = 63 - __clzll((long long)mI);
+                    max_f = __builtin_amdgcn_readlane(sc2, Lh);
+                    max_j = __builtin_amdgcn_readlane(wa, Lh);
+                }
+            }
+        }
+        if (lane == i) F = max_f, PJ = max_j;
+    }
+    if (act) {
+        P.f[g0 + lane] = F;
+        P.p[g0 + lane] = PJ < 0 ? -1 : g0 + PJ;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 #if HYMET_CHAIN_WPE > 0
 #define HYMET_CHAIN_ATTR __attribute__((amdgpu_waves_per_eu(HYMET_CHAIN_WPE)))
 #else
@@ -517,6 +632,13 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         const int64_t g0 = P.g_start[g];
         const int32_t n = (int32_t)(P.g_start[g + 1] - g0);
         const bool qfirst = P.g_qfirst[g] != 0;
+        if constexpr (kMidMax > 0) {
+            if (n <= kMidMax && P.cap_rmq_size >= 64) {
+                chain_mid_group(P, g0, n, qfirst, c, reinterpret_cast<int32_t *>(smem + kRing * sizeof(int4)));
+                GTIME_STOP;
+                continue;
+            }
+        }
         int4 *gsum = P.sum + ((g0 >> 6) + g) * kGSumInts;
         int32_t hb = -1;        // block held by the head cache
         bool hsuf_ok = false;   // hsuf holds the suffix argmins of block hb
@@ -946,6 +1068,24 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             int32_t max_f = span_i;
             int32_t max_j = -1;
             // ---- 1. i0 advances: insert [i0, i) into the window structures
+#if HYMET_CHAIN_DRAIN
+            // x never decreases along a group: when anchor i-1 is beyond max_dist of anchor i,
+            // every entry before i is, so both windows empty at once -- [i0, i) is not inserted
+            // (it would leave again at step 2), st / st_in jump to i and the deques and the
+            // inner list are cleared (and exact again).  Entries below st are never read through
+            // the structures again: a block they complete is only ever a head block, scanned by
+            // entry, and the tail argmin is used only while st <= the tail block's start.  First
+            // pass only: on the long join (bw_long = 100 kbp) the branch measured slower.
+            if (!kLongPass && st < i && (int64_t)(uint32_t)xi > (int64_t)(uint32_t)prev.x + P.max_dist) {
+                i0 = st = st_in = i;
+                bh = bt;
+                bok = true;
+                ni = 0, lh = 0;
+                overflow = false;
+                ih = it;
+                iok = true;
+            }
+#endif
             if (i0 < i && prev.x != xi) {
                 for (int32_t j = i0; j < i; ++j) insert_one(j, j == i - 1 ? prev : fetch(j));
                 i0 = i;
@@ -1007,14 +1147,6 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     hsuf_ok = false;
                 }
             };
-#if HYMET_CHAIN_DRAIN
-            // every entry before i has x <= prev.x: when anchor i-1 is out of the window, all are
-            if (st < i && (int64_t)(uint32_t)xi > (int64_t)(uint32_t)prev.x + P.max_dist) {
-                st = i;
-                bh = bt;    // no complete block is left in the window
-                bok = true;  // the (empty) block deque is exact again
-            }
-#endif
             for (;;) {
                 if (st >= i) break;
 #if HYMET_CHAIN_BLX
@@ -1078,15 +1210,6 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             // ---- 3. inner window start
             AMARK(stin_begin);
             if (P.max_dist_inner > 0) {
-#if HYMET_CHAIN_DRAIN
-                if (st_in < i && (int64_t)(uint32_t)xi > (int64_t)(uint32_t)prev.x + P.max_dist_inner) {
-                    st_in = i;
-                    ni = 0, lh = 0;
-                    overflow = false;  // the list holds exactly [st_in, i0): empty
-                    ih = it;
-                    iok = true;
-                }
-#endif
                 for (;;) {
                     if (st_in >= i) break;
                     const int32_t j = st_in + lane;

@@ -130,7 +130,28 @@ class Comm:
         return {"q": allr[:, 0].contiguous(), "part": allr[:, 1].contiguous(), "depth": allr[:, 2].contiguous(),
                 "tax": allr[:, 3].contiguous(), "names": allr[:, 4:].contiguous().view(-1), "conf": allc.contiguous()}, n
 
-    def allgather_np(self, arr: np.ndarray) -> List[np.ndarray]:
+    def gather_name_pools(self, qname, qname_off, n: int):
+        """Rank 0: the whole input's query-name pool (uint8) and offsets (int64, n_all + 1) on
+        its device, the ranks' shard pools concatenated in rank order (each rank's shard is a
+        contiguous record range, so rank order is input order); other ranks get (None, None).
+        Two padded all-gathers: name bytes and name starts."""
+        torch = self.torch
+        nb = int(qname_off[n].item()) if n else 0
+        pools = self.all_gather_padded(qname.view(-1), nb)
+        starts = self.all_gather_padded(qname_off[:max(n, 1)], n)
+        if self.rank != 0:
+            return None, None
+        base, offs = 0, []
+        for p_, o_ in zip(pools, starts):
+            offs.append(o_ + base)
+            base += int(p_.shape[0])
+        dev = qname.device
+        pool = torch.cat(pools) if base else torch.zeros(1, dtype=torch.uint8, device=dev)
+        off = torch.cat(offs + [torch.tensor([base], dtype=torch.int64, device=dev)])
+        return pool.contiguous(), off.contiguous()
+
+    def allgather_np(self, arr: np.ndarray, tag: str = None) -> List[np.ndarray]:
+        """All-gather of a small host array (tag names the exchange for EmulatedComm)."""
         if self.world <= 1:
             return [arr]
         objs = [None] * self.world
@@ -196,14 +217,23 @@ class EmulatedComm(Comm):
                 return t
         raise ValueError(f"EmulatedComm: no job-wide value for an all-reduce of {t.numel()} x {t.dtype}")
 
-    def allgather_np(self, arr: np.ndarray) -> List[np.ndarray]:
+    def allgather_np(self, arr: np.ndarray, tag: str = None) -> List[np.ndarray]:
         arr = np.asarray(arr)
         self.log.append(("allgather", arr.nbytes))
-        if arr.dtype == np.uint64:           # screen: the ranks' bottom-s candidates
+        if tag == "shard_records":           # ingest: every rank's record count
+            return [np.array([c], np.int64) for c in self.glob["shard_records"]]
+        if tag == "bottom":                  # screen: the ranks' bottom-s candidates
             return [np.asarray(self.glob["bottom"], np.uint64)]
-        if arr.dtype == np.int64 and arr.shape == (1,):   # screen: the ranks' k-mer totals
+        if tag == "n_kmers":                 # screen: the ranks' k-mer totals
             return [np.array([self.glob["nk"]], np.int64)]
-        raise ValueError(f"EmulatedComm: no job-wide value for an all-gather of {arr.dtype} {arr.shape}")
+        raise ValueError(f"EmulatedComm: no job-wide value for the all-gather {tag!r}")
+
+    def gather_name_pools(self, qname, qname_off, n: int):
+        nb = int(qname_off[n].item()) if n else 0
+        self.log.append(("allgather", nb + 8 * n))
+        if self.rank != 0:
+            return None, None
+        return self.glob["names"]
 
     def gather_rows(self, rows, q_base: int, gpu=None):
         """Rank 0 merges its own rows with the other ranks' (from the one-rank run) and sorts

@@ -36,24 +36,49 @@ def _np_ptr(a: np.ndarray):
     return a.ctypes.data_as(_vp)
 
 
-class FastaIndex:
-    """Record table of FASTA text held in host memory (semantics of seqio.parse_fasta_bytes)."""
+def shard_bytes(data: bytes, rank: int, world: int):
+    """Byte range [b0, b1) of this rank's records: the cuts k * len / world moved forward to the
+    next record start ('>' at the start of a line), so each rank scans, uploads and maps only
+    its own part of the FASTA (no rank reads the whole file).  Records are cut whole; a range
+    may be empty when there are fewer records than ranks."""
+    n = len(data)
 
-    def __init__(self, data: bytes, threads: Optional[int] = None):
+    def cut(k):
+        if k <= 0:
+            return 0
+        if k >= world:
+            return n
+        c = n * k // world
+        if c > 0 and data[c - 1:c] == b"\n" and data[c:c + 1] == b">":
+            return c
+        j = data.find(b"\n>", c)
+        return n if j < 0 else j + 1
+    return cut(rank), cut(rank + 1)
+
+
+class FastaIndex:
+    """Record table of FASTA text held in host memory (semantics of seqio.parse_fasta_bytes).
+    byte_range: index only the records starting in [b0, b1) (shard_bytes); offsets stay
+    absolute into `data`."""
+
+    def __init__(self, data: bytes, threads: Optional[int] = None, byte_range=None):
         self.data = data
         lib = load()
         threads = int(threads or min(16, os.cpu_count() or 1))
         n = _c.c_int64()
         buf = _c.c_char_p(data)
         self._buf = buf
-        cap = max(16, len(data) // 64)
+        b0, b1 = byte_range if byte_range is not None else (0, len(data))
+        self.byte_range = (int(b0), int(b1))
+        base = _c.cast(buf, _vp).value + b0 if len(data) else None
+        cap = max(16, (b1 - b0) // 64)
         while True:
             self.name_off = np.zeros(cap, np.int64)
             self.name_len = np.zeros(cap, np.int32)
             self.seq_off = np.zeros(cap, np.int64)
             self.seq_end = np.zeros(cap, np.int64)
             self.nbases = np.zeros(cap, np.int64)
-            rc = lib.hymet_fasta_index(buf, len(data), threads, cap, _c.byref(n), _np_ptr(self.name_off),
+            rc = lib.hymet_fasta_index(_vp(base), b1 - b0, threads, cap, _c.byref(n), _np_ptr(self.name_off),
                                        _np_ptr(self.name_len), _np_ptr(self.seq_off), _np_ptr(self.seq_end),
                                        _np_ptr(self.nbases))
             if rc == -3:
@@ -65,6 +90,9 @@ class FastaIndex:
         self.n = k
         for a in ("name_off", "name_len", "seq_off", "seq_end", "nbases"):
             setattr(self, a, getattr(self, a)[:k])
+        if b0:
+            for a in ("name_off", "seq_off", "seq_end"):
+                getattr(self, a)[:] += b0
         self._names: Optional[List[str]] = None
 
     @property
@@ -89,6 +117,17 @@ class FastaIndex:
         check(load().hymet_fasta_names(self._buf, _np_ptr(no), _np_ptr(nl), n, _np_ptr(pool), _np_ptr(off)),
               "hymet_fasta_names")
         return pool[:off[-1]], off
+
+    def byte_shards(self, world: int):
+        """Record ranges of the `world` byte shards (shard_bytes) of a whole-file index:
+        [(r0, r1)] per rank, from where each cut lands."""
+        out, r = [], 0
+        for k in range(world):
+            _, b1 = shard_bytes(self.data, k, world)
+            r1 = int(np.searchsorted(self.name_off, b1, side="right"))  # a record's name starts in (its '>', next '>']
+            out.append((r, r1))
+            r = r1
+        return out
 
     def shard(self, rank: int, world: int):
         """Contiguous record range [r0, r1) of this rank, balanced by bases (every rank
@@ -157,7 +196,8 @@ class QueryShard:
     qname_off: object           # device int64 [n + 1]
     batches: list
     names_host: Optional[List[str]] = None   # SeqSet input: names on the host
-    fasta: Optional[FastaIndex] = None       # FASTA input: the whole input's record table
+    fasta: Optional[FastaIndex] = None       # FASTA input: the record table the shard was cut from
+    fasta_r0: int = 0                        # index in `fasta` of the shard's first record
 
     @property
     def total_bases(self) -> int:
@@ -165,16 +205,18 @@ class QueryShard:
 
     @classmethod
     def from_fasta(cls, gpu, fx: FastaIndex, r0: int = 0, r1: Optional[int] = None, batch_bases: int = 40_000_000,
-                   d_all=None):
+                   d_all=None, q_base: Optional[int] = None):
         """One H2D copy of the records' contiguous byte range, then device-side compaction.
-        d_all: the whole input already in HBM (uploaded while the records were scanned)."""
+        d_all: the whole input already in HBM (uploaded while the records were scanned).
+        q_base: index of record r0 in the whole input (default r0: fx indexes the whole file)."""
         torch = gpu.torch
         r1 = fx.n if r1 is None else r1
+        q_base = r0 if q_base is None else q_base
         n = r1 - r0
         nb = fx.nbases[r0:r1]
         pool_len = int(nb.sum()) + max(n - 1, 0)
         if n == 0:
-            return cls._empty(gpu, r0, batch_bases)
+            return cls._empty(gpu, q_base, batch_bases)
         lo = int(min(fx.name_off[r0], fx.seq_off[r0]))
         hi = int(fx.seq_end[r1 - 1])
         if d_all is not None:
@@ -203,7 +245,7 @@ class QueryShard:
         d_hash = gpu.empty(n, torch.int32)
         gpu.call("hymet_name_hash", ptr(d_raw), ptr(noff), ptr(nlen), n, ptr(d_hash))
         pool_b, pool_off = fx.name_pool(r0, r1)
-        return cls._finish(gpu, n, r0, lengths, starts, d_pool, pool_len, d_hash, pool_b, pool_off, batch_bases)
+        return cls._finish(gpu, n, q_base, lengths, starts, d_pool, pool_len, d_hash, pool_b, pool_off, batch_bases)
 
     @classmethod
     def from_seqset(cls, gpu, ss: SeqSet, q_base: int = 0, batch_bases: int = 40_000_000):

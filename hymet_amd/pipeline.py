@@ -29,7 +29,7 @@ from . import mapper as mp
 from . import screen as scr
 from . import select as sel
 from ._lib import check, ptr
-from .ingest import FastaIndex, QueryShard
+from .ingest import FastaIndex, QueryShard, shard_bytes
 from .msh import SketchDB, read_msh
 from .seqio import SeqSet
 
@@ -395,7 +395,17 @@ class Pipeline:
         d_all = None
         if isinstance(queries, (bytes, bytearray, memoryview)):
             data = bytes(queries)
-            if self.world == 1 and len(data):
+            if self.world > 1:
+                # this rank scans, uploads and maps only its byte range of the FASTA; the ranks'
+                # record counts give its first query's index in the whole input
+                b0, b1 = shard_bytes(data, self.rank, self.world)
+                fx = FastaIndex(data, byte_range=(b0, b1))
+                counts = self.comm.allgather_np(np.array([fx.n], np.int64), tag="shard_records")
+                q_base = int(sum(int(c[0]) for c in counts[:self.rank]))
+                sh = QueryShard.from_fasta(self.gpu, fx, 0, fx.n, self.cfg.map_batch_bases, q_base=q_base)
+                sh.fasta, sh.fasta_r0 = fx, 0
+                return sh
+            if len(data):
                 # one rank takes every record: the bytes go up on a second thread while the
                 # record table is scanned (the staged copy and the scan both read host memory)
                 import threading
@@ -423,7 +433,7 @@ class Pipeline:
             r0, r1 = queries.shard(self.rank, self.world)
             sh = QueryShard.from_fasta(self.gpu, queries, r0, r1, self.cfg.map_batch_bases,
                                        d_all=d_all if (r0, r1) == (0, queries.n) else None)
-            sh.fasta = queries
+            sh.fasta, sh.fasta_r0 = queries, r0
             return sh
         if isinstance(queries, SeqSet):
             if self.world > 1:
@@ -650,8 +660,12 @@ class Pipeline:
         return RunResult(selected, rows, thr, tsv, n_rows, n_cls, n_lines, paf_text, self.last_screen)
 
     def _global_names(self, sh: QueryShard):
-        """Rank 0's name pool of the whole input (rows from every rank index into it)."""
+        """Rank 0's name pool of the whole input (rows from every rank index into it): the
+        ranks' pools gathered (a byte-range shard indexes only its own records), or the
+        whole-file record table's names.  A collective: every rank calls it."""
         fx = sh.fasta
+        if fx is not None and fx.byte_range != (0, len(fx.data)):
+            return self.comm.gather_name_pools(sh.qname, sh.qname_off, sh.n)
         if self._bufs.get("names_of") is not fx:
             torch = self.gpu.torch
             pool, off = fx.name_pool()
@@ -668,7 +682,7 @@ class Pipeline:
         if sh.names_host is not None:
             names = sh.names_host
         else:
-            names = sh.fasta.names()[sh.q_base:sh.q_base + sh.n]
+            names = sh.fasta.names()[sh.fasta_r0:sh.fasta_r0 + sh.n]
         pairs = [(names[int(a)], ix.names[int(b)]) for a, b in zip(q, t)]
         if self.world > 1:
             # lines of a query sit together per part; queries sort by (part, input index)

@@ -132,8 +132,8 @@ def reduce_partials(comm, counts, bottom: np.ndarray, nk: int, s: int, tables=No
         by_hash = c[so]
         comm.allreduce_sum_(by_hash)
         c[so] = by_hash
-    bottom = _bottom_s(np.concatenate(comm.allgather_np(np.asarray(bottom, np.uint64))), s)
-    nk = int(sum(int(x[0]) for x in comm.allgather_np(np.array([nk], dtype=np.int64))))
+    bottom = _bottom_s(np.concatenate(comm.allgather_np(np.asarray(bottom, np.uint64), tag="bottom")), s)
+    nk = int(sum(int(x[0]) for x in comm.allgather_np(np.array([nk], dtype=np.int64), tag="n_kmers")))
     return counts, bottom, nk
 
 

@@ -60,6 +60,38 @@ def test_fasta_index_threaded_large():
     assert pool.tobytes() == b"".join(n.split()[0].encode() for n in names[5:9]) and off[-1] == len(pool)
 
 
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8, 64])
+@pytest.mark.parametrize("data", CASES + [to_fasta([f"c{i} len={i}" for i in range(40)],
+                                                  [b"ACGT" * (1 + 37 * i % 50) for i in range(40)], width=13)])
+def test_byte_shards_partition_the_records(data, world):
+    """ingest.shard_bytes + FastaIndex(byte_range=...): what each rank indexes of its own byte
+    range, concatenated over the ranks, is the whole-file record table (names, sequences,
+    base counts, absolute offsets) -- including junk before the first record, CRLF, '>' inside
+    lines, empty records and more ranks than records -- and byte_shards predicts the split."""
+    from hymet_amd.ingest import shard_bytes
+    whole = FastaIndex(data)
+    got = []
+    prev_end = 0
+    for r in range(world):
+        b0, b1 = shard_bytes(data, r, world)
+        assert b0 == prev_end and b0 <= b1
+        prev_end = b1
+        fx = FastaIndex(data, byte_range=(b0, b1))
+        got.append(fx)
+    assert prev_end == len(data)
+    names = [n for fx in got for n in fx.names()]
+    assert names == whole.names()
+    for a in ("name_off", "name_len", "nbases"):
+        np.testing.assert_array_equal(np.concatenate([getattr(fx, a) for fx in got]), getattr(whole, a))
+    # sequences: a rank's last record ends at the range end, so its byte range may keep the
+    # line break before the next '>' (a header-only record may then start one byte later);
+    # the bases are the same
+    seqs = [data[fx.seq_off[i]:fx.seq_end[i]].replace(b"\n", b"").replace(b"\r", b"") for fx in got for i in range(fx.n)]
+    assert seqs == [data[a:b].replace(b"\n", b"").replace(b"\r", b"") for a, b in zip(whole.seq_off, whole.seq_end)]
+    counts = [fx.n for fx in got]
+    assert [b - a for a, b in whole.byte_shards(world)] == counts
+
+
 def _greedy_batches(lengths, max_bases):
     """The batching rule spelled out record by record: a batch closes before the record
     that would take it past max_bases (a record longer than that sits alone)."""

@@ -31,6 +31,23 @@ __global__ __launch_bounds__(256) void calib_write(T *__restrict__ a, size_t n) 
     }
 }
 
+// Scattered reads (round 5): one T per `Stride`-byte slot of the 2 GiB buffer, the slots visited
+// in a pseudo-random order (k * 0x9E3779B1 mod the slot count: a bijection, no index array to
+// stream), one access per lane per step -- the chaining / backtrack kernels' pattern (window
+// heads, predecessor walks).  Each slot is read once, so the bytes the memory system must move
+// are (slots x min(Stride, line)) and the bytes the kernel uses are (slots x sizeof(T)); the
+// counters tell which of the two FETCH_SIZE follows for scattered traffic.
+template <typename T, int Stride>
+__global__ __launch_bounds__(256) void calib_gather(const unsigned char *__restrict__ a, size_t slots, unsigned long long *out) {
+    unsigned long long s = 0;
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < slots; k += (size_t)gridDim.x * blockDim.x) {
+        const size_t slot = (k * 0x9E3779B1ull) & (slots - 1);
+        const T v = *reinterpret_cast<const T *>(a + slot * Stride);
+        s += reinterpret_cast<const unsigned int *>(&v)[0];
+    }
+    if (s == 0x123456789ull) out[0] = s;
+}
+
 #define CK(x)                                                                   \
     do {                                                                        \
         hipError_t e_ = (x);                                                    \
@@ -53,8 +70,16 @@ int main() {
     hipLaunchKernelGGL(calib_read<unsigned int>, grid, block, 0, 0, (const unsigned int *)buf, kBytes / 4, out);
     hipLaunchKernelGGL(calib_read<uint2>, grid, block, 0, 0, (const uint2 *)buf, kBytes / 8, out);
     hipLaunchKernelGGL(calib_read<uint4>, grid, block, 0, 0, (const uint4 *)buf, kBytes / 16, out);
+    const unsigned char *b = (const unsigned char *)buf;
+    hipLaunchKernelGGL((calib_gather<unsigned int, 128>), grid, block, 0, 0, b, kBytes / 128, out);
+    hipLaunchKernelGGL((calib_gather<uint2, 128>), grid, block, 0, 0, b, kBytes / 128, out);
+    hipLaunchKernelGGL((calib_gather<unsigned int, 64>), grid, block, 0, 0, b, kBytes / 64, out);
+    hipLaunchKernelGGL((calib_gather<unsigned int, 32>), grid, block, 0, 0, b, kBytes / 32, out);
+    hipLaunchKernelGGL((calib_gather<uint4, 256>), grid, block, 0, 0, b, kBytes / 256, out);
     CK(hipDeviceSynchronize());
     printf("calibration kernels: %zu bytes each (read / write at 4, 8, 16 B per lane)\n", kBytes);
+    printf("gather kernels: one T per Stride-byte slot, random slot order: <u32,128> %zu, <u64,128> %zu, <u32,64> %zu, "
+           "<u32,32> %zu, <u128,256> %zu accesses\n", kBytes / 128, kBytes / 128, kBytes / 64, kBytes / 32, kBytes / 256);
     CK(hipFree(buf));
     CK(hipFree(out));
     return 0;
