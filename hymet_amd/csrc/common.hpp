@@ -17,6 +17,11 @@ struct hymet_ctx {
     bool prof = false;
     std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> ev;
     std::map<std::string, double> bytes;  // algorithmic bytes of the timed launches
+    // algorithmic units counted on the device (e.g. the anchors a kernel took from a work list
+    // the host never sees): scope -> (slot of prof_dev, bytes per unit); prof_dev[kProfSlots]
+    // accumulates while profiling is on and is read by hymet_prof_query
+    std::map<std::string, std::pair<int, double>> dev_bytes;
+    int64_t *prof_dev = nullptr;
     // pinned staging for hymet_copy_to_host (two chunks, allocated on first use)
     void *stage[2] = {nullptr, nullptr};
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
@@ -42,6 +47,10 @@ struct ProfScope {
             c->bytes[name] += alg_bytes;
         }
     }
+    // bytes = per_unit x the units kernels add to prof_dev[slot] (prof_dev_slot) inside the scope
+    ProfScope(hymet_ctx *ctx, const char *n, int slot, double per_unit) : ProfScope(ctx, n, 0.0) {
+        if (c && c->prof) c->dev_bytes[name] = {slot, per_unit};
+    }
     ~ProfScope() {
         if (c && c->prof && a && b) {
             (void)hipEventRecord(b, c->stream);
@@ -49,6 +58,9 @@ struct ProfScope {
         }
     }
 };
+constexpr int kProfSlots = 8;
+// the device counter of slot k while profiling is on, else nullptr (kernels skip the count)
+inline int64_t *prof_dev_slot(hymet_ctx *c, int k) { return c && c->prof && c->prof_dev ? c->prof_dev + k : nullptr; }
 }  // namespace hymet
 
 namespace hymet {

@@ -148,6 +148,10 @@ int hymet_init(int device, hymet_ctx **out) {
         return hymet::fail(HYMET_E_HIP, "hymet_init: mailbox allocation failed");
     }
     for (int i = 0; i < hymet::kMbox; i++) c->mbox_h[i] = 0;
+    if (hipMalloc((void **)&c->prof_dev, 8 * hymet::kProfSlots) != hipSuccess ||
+        hipMemset(c->prof_dev, 0, 8 * hymet::kProfSlots) != hipSuccess) {
+        c->prof_dev = nullptr;  // device-counted profile bytes unavailable: reported as 0
+    }
     if (hipMalloc((void **)&c->dctr, 4 * hymet::kMbox) != hipSuccess || hipMemset(c->dctr, 0, 4 * hymet::kMbox) != hipSuccess) {
         hymet_destroy(c);
         return hymet::fail(HYMET_E_HIP, "hymet_init: counter allocation failed");
@@ -165,6 +169,7 @@ int hymet_destroy(hymet_ctx *ctx) {
     }
     if (ctx->mbox_h) (void)hipHostFree(ctx->mbox_h);
     if (ctx->dctr) (void)hipFree(ctx->dctr);
+    if (ctx->prof_dev) (void)hipFree(ctx->prof_dev);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return HYMET_OK;
@@ -195,6 +200,9 @@ int hymet_prof_reset(hymet_ctx *ctx) {
         }
     ctx->ev.clear();
     ctx->bytes.clear();
+    ctx->dev_bytes.clear();
+    if (ctx->prof_dev) HY_HIP(hipMemsetAsync(ctx->prof_dev, 0, 8 * hymet::kProfSlots, ctx->stream));
+    HY_HIP(hipStreamSynchronize(ctx->stream));
     return HYMET_OK;
 }
 
@@ -203,7 +211,15 @@ int hymet_prof_query(hymet_ctx *ctx, const char *name, double *total_ms, int64_t
     HY_HIP(hipStreamSynchronize(ctx->stream));
     *total_ms = 0.0;
     *count = 0;
-    if (alg_bytes) *alg_bytes = ctx->bytes.count(name) ? ctx->bytes[name] : 0.0;
+    if (alg_bytes) {
+        *alg_bytes = ctx->bytes.count(name) ? ctx->bytes[name] : 0.0;
+        auto db = ctx->dev_bytes.find(name);
+        if (db != ctx->dev_bytes.end() && ctx->prof_dev) {
+            int64_t units = 0;
+            HY_HIP(hipMemcpy(&units, ctx->prof_dev + db->second.first, 8, hipMemcpyDeviceToHost));
+            *alg_bytes += db->second.second * (double)units;
+        }
+    }
     auto it = ctx->ev.find(name);
     if (it == ctx->ev.end()) return HYMET_OK;
     for (auto &p : it->second) {

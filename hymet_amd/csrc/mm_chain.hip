@@ -124,7 +124,21 @@ namespace {
 // jump to i and the deques and the inner list are cleared in O(1), instead of one probe round
 // (and a head-cache load beyond the rings) per 64 entries passed.
 #ifndef HYMET_CHAIN_DRAIN
-#define HYMET_CHAIN_DRAIN 0
+#define HYMET_CHAIN_DRAIN 1
+#endif
+// A committed batch also inserts its last anchor into the window structures when the next
+// anchor's x differs (lchain.c inserts [i0, i) once x changes): the next iteration then has
+// nothing to insert (step 1 is skipped) instead of one insert_one per batch.
+#ifndef HYMET_CHAIN_INSALL
+#define HYMET_CHAIN_INSALL 0
+#endif
+// A colinear batch is cut at the first anchor whose y does not rise: no anchor from there on
+// can commit (the batch needs py < ky lane to lane), and Y -- the y bound B is taken under --
+// becomes the y of the last anchor that can.  Without the cut, a stray anchor inside the
+// 64-anchor window past a chain's end set Y to its random y, every chain anchor above it
+// failed `ky <= Y`, and the rest of the chain was single-stepped behind the back-off.
+#ifndef HYMET_CHAIN_YPREFIX
+#define HYMET_CHAIN_YPREFIX 0
 #endif
 // Wave-uniform loop state pinned to scalar registers (readfirstlane at the derivation points):
 // branches on it become scalar branches instead of exec-mask bookkeeping (first pass 11.55 ->
@@ -467,14 +481,18 @@ __device__ __forceinline__ int4 pack_st(double pr, int32_t j, int32_t y) {
 }
 __device__ __forceinline__ double st_pr(const int4 &v) { return __hiloint2double(v.y, v.x); }
 
-// Groups of at most kMidMax anchors (and more than the lane kernel's kSmall) are chained by a
-// wave with one LANE PER ANCHOR, the whole group in registers (chain_mid_group): the window
-// trees become 64-bit lane masks, the RMQ one wave argmin, the inner walk one pass in the
-// (y, idx) order through the same prefix scans the wave kernel's walk uses.  The general path
-// single-steps these groups (repeat hits that do not chain colinearly) at ~2.2 us per anchor
-// through its LDS list / deque / block-summary upkeep.  0 disables.
+// First-pass groups of at most kMidMax anchors (and more than the lane kernel's kSmall) are
+// chained by a wave with one LANE PER ANCHOR, the whole group in registers (chain_mid_group):
+// the window trees become 64-bit lane masks, the RMQ one wave argmin, the inner walk one pass
+// in the (y, idx) order through the same prefix scans the wave kernel's walk uses.  The
+// general path single-steps these groups (repeat hits that do not chain colinearly) at
+// ~2.2 us per anchor through its LDS list / deque / block-summary upkeep; this path takes
+// ~1 us (tools/chain_prof on the real-anchor dumps, f/p digests identical: C4 first pass
+// 10.53 -> 10.18 ms with the drain, Zymo backbones 19.53 -> 17.48 ms).  The long join's
+// groups are chained anchors, which the general path commits in colinear batches: there the
+// lane-per-anchor path measured 2-6 % slower, so it serves the first pass only.  0 disables.
 #ifndef HYMET_CHAIN_MID
-#define HYMET_CHAIN_MID 0
+#define HYMET_CHAIN_MID 64
 #endif
 constexpr int kMidMax = HYMET_CHAIN_MID;
 
@@ -632,7 +650,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         const int64_t g0 = P.g_start[g];
         const int32_t n = (int32_t)(P.g_start[g + 1] - g0);
         const bool qfirst = P.g_qfirst[g] != 0;
-        if constexpr (kMidMax > 0) {
+        if constexpr (kMidMax > 0 && !kLongPass) {
             if (n <= kMidMax && P.cap_rmq_size >= 64) {
                 chain_mid_group(P, g0, n, qfirst, c, reinterpret_cast<int32_t *>(smem + kRing * sizeof(int4)));
                 GTIME_STOP;
@@ -1343,6 +1361,16 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 double b0p = 0.0;
                 int32_t b0j = -1;
                 int32_t batch_y = INT32_MAX;  // B's y bound: every committed anchor must lie at or below it
+#if HYMET_CHAIN_YPREFIX
+                if (walk_ok && Lb >= 2) {
+                    const int offy = (i - cb) + lane;
+                    const int32_t ylo_ = __shfl((int32_t)cy, offy & 63, 64), yhi_ = __shfl((int32_t)ny, offy & 63, 64);
+                    const int32_t yl = offy < 64 ? ylo_ : yhi_;
+                    const int32_t yp = shr1(yl, INT32_MIN);
+                    const uint64_t brk = __ballot(lane >= 1 && lane < Lb && !(yp < yl));
+                    if (brk) Lb = __ffsll((unsigned long long)brk) - 1;
+                }
+#endif
                 if (walk_ok && Lb >= 2) {
                     const int offl = (i - cb) + Lb - 1;
                     const int32_t ymax = (int32_t)(offl < 64 ? rl((int32_t)cy, offl) : rl((int32_t)ny, offl - 64));
@@ -1433,6 +1461,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     if (P.max_dist_inner > 0 && !ex && ky > 0) wok = max(vex, it > ih ? if_v : INT32_MIN) <= fk;
                     // inner-list keys (y, idx) of entries i.. strictly increase (py < ky); they must
                     // all fall into the gap of the list before G
+                    bool gap_own = true;  // this lane's own entry falls into the gap
                     if (P.max_dist_inner > 0 && ni > 0) {
                         const int32_t e0y = rl(ky, 0);
                         if (!key_less(lby, lbj, e0y, i)) {
@@ -1455,6 +1484,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         }
                         // entry k-1 (k = i + lane, lane >= 1) is inserted at anchor k
                         if (lane >= 1 && !key_less(py, i + lane - 1, gy, gj)) ok = false;
+                        gap_own = key_less(ky, i + lane, gy, gj);
                     }
 #ifdef HYMET_CHAIN_PROF
                     const bool ok_geom = ok;
@@ -1484,6 +1514,18 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     }
                     AMARK(batch_verified);
                     if (acc > 0) {
+#if HYMET_CHAIN_INSALL
+                        // the anchor after the batch (lane acc, or the next chunk for a full batch):
+                        // a different x lets the last committed entry enter the window now
+                        bool ins_all = false;
+                        if (i + acc < n) {
+                            const int offn = (i - cb) + 64;
+                            const int32_t xn = acc < 64 ? rl(kx, acc) : rl(nx, offn - 64);
+                            ins_all = xn != rl(kx, acc - 1) && rl(gap_own ? 1 : 0, acc - 1) != 0;
+                        }
+#else
+                        const bool ins_all = false;
+#endif
                         // the next iteration's chunks first: nothing below reads the chunk
                         // registers, and the rotation then waits on no store of this commit
                         advance(i + acc);
@@ -1503,7 +1545,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         CCOUNT(7);
                         GCNT(z, 1);
                         GCNT(w, acc);
-                        const int nins = acc - 1;
+                        const int nins = ins_all ? acc : acc - 1;
                         if (nins > 0) {
                             if (P.max_dist_inner > 0) {
                                 // list: shift [gpos, ni) right by nins, batch keys into [gpos, gpos + nins)
@@ -2226,6 +2268,30 @@ __global__ void chain_small_split_kernel(const int64_t *g_start, const int32_t *
     *split = lo;
 }
 
+// profiling only: anchors of the work items the wave kernel takes ([0, *split)) into cnt[0] and
+// of those the lane kernel takes into cnt[1] (one block; the bytes of the two profile scopes)
+__global__ __launch_bounds__(1024) void chain_work_anchors_kernel(const int64_t *g_start, const int32_t *order,
+                                                                   int32_t n_work, const int32_t *split, int64_t *cnt) {
+    __shared__ unsigned long long sw, ss;
+    if (threadIdx.x == 0) sw = 0, ss = 0;
+    __syncthreads();
+    const int32_t sp = *split;
+    unsigned long long w = 0, s = 0;
+    for (int32_t k = threadIdx.x; k < n_work; k += 1024) {
+        const int g = order[k];
+        const unsigned long long a = (unsigned long long)(g_start[g + 1] - g_start[g]);
+        if (k < sp) w += a;
+        else s += a;
+    }
+    atomicAdd(&sw, w);
+    atomicAdd(&ss, s);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(reinterpret_cast<unsigned long long *>(cnt), sw);
+        atomicAdd(reinterpret_cast<unsigned long long *>(cnt + 1), ss);
+    }
+}
+
 __global__ __launch_bounds__(64) void chain_small_kernel(ChainParams P, const int32_t *split) {
     const int32_t w = *split + (int32_t)(blockIdx.x * 64 + threadIdx.x);
     if (w >= P.n_work) return;
@@ -2356,8 +2422,30 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
     if (waves_env > 0 && waves_env < per_cu) per_cu = waves_env;
     const int64_t cap = (int64_t)ctx->n_cu * per_cu;
     if (blocks > cap) blocks = cap;
-    ProfScope _ps(ctx, max_dist > 10000 ? "mm_chain_long" : "mm_chain", 28.0 * (double)n_anchors);  // x,y read + f,p write per anchor
-    return launch_chain_raw(ctx->stream, P, blocks, split.as<int32_t>());
+    // two profile scopes, one kernel each: the wave kernel (groups above kSmall anchors, the
+    // mid-group path included) and the lane kernel; each scope's algorithmic bytes are 28 per
+    // anchor it chains (x, y read; f, p written), counted on the device from the work list
+    const int slot = long_pass ? 2 : 0;
+    hipStream_t st = ctx->stream;
+    {
+        ProfScope _ps(ctx, long_pass ? "mm_chain_long" : "mm_chain", slot, 28.0);
+        hipLaunchKernelGGL(chain_small_split_kernel, dim3(1), dim3(64), 0, st, P.g_start, P.order, P.n_work,
+                           split.as<int32_t>(), P.work_counter);
+        HY_CHECK_LAUNCH("chain_small_split_kernel");
+        if (int64_t *pc = prof_dev_slot(ctx, slot)) {
+            hipLaunchKernelGGL(chain_work_anchors_kernel, dim3(1), dim3(1024), 0, st, P.g_start, P.order, P.n_work,
+                               (const int32_t *)split.as<int32_t>(), pc);
+            HY_CHECK_LAUNCH("chain_work_anchors_kernel");
+        }
+        P.work_end = split.as<int32_t>();
+        if (long_pass) hipLaunchKernelGGL(chain_groups_kernel<1>, dim3((unsigned)blocks), dim3(64), kChainLds, st, P);
+        else hipLaunchKernelGGL(chain_groups_kernel<0>, dim3((unsigned)blocks), dim3(64), kChainLds, st, P);
+        HY_CHECK_LAUNCH("chain_groups_kernel");
+    }
+    ProfScope _pl(ctx, long_pass ? "mm_chain_long_small" : "mm_chain_small", slot + 1, 28.0);
+    hipLaunchKernelGGL(chain_small_kernel, dim3((unsigned)cdiv(P.n_work, 64)), dim3(64), 0, st, P, (const int32_t *)split.as<int32_t>());
+    HY_CHECK_LAUNCH("chain_small_kernel");
+    return HYMET_OK;
 }
 
 int launch_backtrack(hymet_ctx *ctx, const int64_t *g_start, const int32_t *f, const int64_t *p, int32_t *t,

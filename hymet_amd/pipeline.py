@@ -353,12 +353,27 @@ class Pipeline:
 
     def _read_inputs(self, side=None):
         """The run's input loads for a second host thread: .msh parse (+ the HBM tables on
-        `side`'s stream when given), taxonomy tables."""
-        if self.db_paths:
-            self._read_dbs()
-            if side is not None:
-                self._build_tables(side)
-        self._load_classifier()
+        `side`'s stream when given), and the taxonomy tables on a third thread beside them
+        (the .msh gather runs in native code without the GIL, so the two overlap)."""
+        import threading
+        err = []
+
+        def classifier():
+            try:
+                self._load_classifier()
+            except BaseException as e:  # noqa: BLE001 -- re-raised below
+                err.append(e)
+        th = threading.Thread(target=classifier, name="hymet-taxonomy")
+        th.start()
+        try:
+            if self.db_paths:
+                self._read_dbs()
+                if side is not None:
+                    self._build_tables(side)
+        finally:
+            th.join()
+        if err:
+            raise err[0]
 
     def _load_classifier(self):
         """C1-C2: detailed_taxonomy.tsv and taxonomy_hierarchy.tsv.  classification_cami.py

@@ -9,8 +9,12 @@ while read -r name secs cmd; do
   [ -z "$name" ] && continue
   case "$name" in \#*) continue;; esac
   echo "[step $name] $cmd" >> $OUT/steps.log
+  # heartbeat: a step that prints nothing for minutes (a long oracle check) still writes here
+  ( while true; do sleep 60; echo "[$(date +%T)] $name running" >> $OUT/heartbeat.log; done ) &
+  hb=$!
   timeout -k 10 $secs bash -c "$cmd" > $OUT/$name.log 2>&1
   rc=$?
+  kill $hb 2>/dev/null; wait $hb 2>/dev/null
   echo "[step $name] rc=$rc" >> $OUT/steps.log
   case $rc in 124|134|137|139) echo "stopping after $name (rc=$rc)" >> $OUT/steps.log; exit $rc;; esac
 done < $STEPS
