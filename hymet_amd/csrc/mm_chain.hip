@@ -130,7 +130,7 @@ namespace {
 // anchor's x differs (lchain.c inserts [i0, i) once x changes): the next iteration then has
 // nothing to insert (step 1 is skipped) instead of one insert_one per batch.
 #ifndef HYMET_CHAIN_INSALL
-#define HYMET_CHAIN_INSALL 0
+#define HYMET_CHAIN_INSALL 1
 #endif
 // A colinear batch is cut at the first anchor whose y does not rise: no anchor from there on
 // can commit (the batch needs py < ky lane to lane), and Y -- the y bound B is taken under --
@@ -138,7 +138,7 @@ namespace {
 // 64-anchor window past a chain's end set Y to its random y, every chain anchor above it
 // failed `ky <= Y`, and the rest of the chain was single-stepped behind the back-off.
 #ifndef HYMET_CHAIN_YPREFIX
-#define HYMET_CHAIN_YPREFIX 0
+#define HYMET_CHAIN_YPREFIX 1
 #endif
 // Wave-uniform loop state pinned to scalar registers (readfirstlane at the derivation points):
 // branches on it become scalar branches instead of exec-mask bookkeeping (first pass 11.55 ->
@@ -472,6 +472,22 @@ __device__ __forceinline__ double Ud(double v) {
 #else
 __device__ __forceinline__ int32_t U(int32_t v) { return v; }
 __device__ __forceinline__ double Ud(double v) { return v; }
+#endif
+// HYMET_CHAIN_UNI2: values every lane loads from the same LDS word (deque ends, list ends, the
+// head suffix record, entries passed to insert_one) are wave-uniform but look divergent to the
+// compiler, which then keeps the loop state derived from them (deque indices, list length) in
+// VGPRs and runs their loops under exec masks; readfirstlane makes them SGPRs
+#ifndef HYMET_CHAIN_UNI2
+#define HYMET_CHAIN_UNI2 0
+#endif
+#if HYMET_CHAIN_UNI2
+__device__ __forceinline__ int32_t UL(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int4 UL4(int4 v) { return make_int4(UL(v.x), UL(v.y), UL(v.z), UL(v.w)); }
+__device__ __forceinline__ int2 UL2(int2 v) { return make_int2(UL(v.x), UL(v.y)); }
+#else
+__device__ __forceinline__ int32_t UL(int32_t v) { return v; }
+__device__ __forceinline__ int4 UL4(int4 v) { return v; }
+__device__ __forceinline__ int2 UL2(int2 v) { return v; }
 #endif
 __device__ __forceinline__ double rld(double v, int l) {
     return __hiloint2double(rl(__double2hiint(v), l), rl(__double2loint(v), l));
@@ -821,7 +837,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         auto L = [&](int k) -> int2 & { return lst[(lh + k) & (kInnerCap - 1)]; };
         auto reload_ends = [&]() {
             if (ni > 0) {
-                const int2 a = L(0), b = L(ni - 1);
+                const int2 a = UL2(L(0)), b = UL2(L(ni - 1));
                 lfy = a.x, lfj = a.y, lby = b.x, lbj = b.y;
             }
         };
@@ -963,7 +979,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             while (bt > bh && better(apr, aj, bb_pr, bb_j)) {
                 --bt;
                 if (bt > bh) {
-                    const int4 v = bdq[((bt - 1) & (kBdq - 1)) * 2];
+                    const int4 v = UL4(bdq[((bt - 1) & (kBdq - 1)) * 2]);
                     bb_pr = st_pr(v), bb_j = v.z;
                 }
             }
@@ -982,8 +998,9 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             AMARK(cb_end);
         };
         // entry j (now final) enters the window: inner list, inner max-deque, tail argmin
-        auto insert_one = [&](int32_t j, const Ent ej) {
+        auto insert_one = [&](int32_t j, const Ent ej_in) {
             AMARK(ins_begin);
+            const Ent ej{UL(ej_in.x), UL(ej_in.y), UL(ej_in.f), UL(ej_in.pw)};
             if (P.max_dist_inner > 0) {
                 if (!overflow && ni >= kInnerCap) overflow = true;
                 if (!overflow) {
@@ -1029,7 +1046,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     const int32_t v = ej.f + ej.sp();
                     while (it > ih && ib_v <= v) {
                         --it;
-                        if (it > ih) ib_v = idq[(it - 1) & (kIdq - 1)].y;
+                        if (it > ih) ib_v = UL(idq[(it - 1) & (kIdq - 1)].y);
                     }
                     if (it - ih >= kIdq) {
                         iok = false;
@@ -1195,9 +1212,9 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             while (bt > bh && (bf_j >> 6) < fb) {
                 ++bh;
                 if (bt > bh) {
-                    const int4 v = bdq[(bh & (kBdq - 1)) * 2];
+                    const int4 v = UL4(bdq[(bh & (kBdq - 1)) * 2]);
                     bf_pr = st_pr(v), bf_j = v.z, bf_y = v.w;
-                    bf_e = bdq[(bh & (kBdq - 1)) * 2 + 1];
+                    bf_e = UL4(bdq[(bh & (kBdq - 1)) * 2 + 1]);
                 }
             }
             if ((st & 63) && (st >> 6) < fe && ((st >> 6) != hb || !hsuf_ok || (st & 63) < hlow)) {
@@ -1249,7 +1266,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                                 lh = (lh + nl) & (kInnerCap - 1);
                                 ni -= nl;
                                 if (ni > 0) {
-                                    const int2 a = L(0);
+                                    const int2 a = UL2(L(0));
                                     lfy = a.x, lfj = a.y;
                                 }
                                 st_in += t;
@@ -1286,7 +1303,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                             lh = (lh + 1) & (kInnerCap - 1);
                             ni--;
                             if (ni > 0) {
-                                const int2 a = L(0);
+                                const int2 a = UL2(L(0));
                                 lfy = a.x, lfj = a.y;
                             }
                             continue;
@@ -1328,9 +1345,9 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     st_in += t;
                     if (t < 64) break;
                 }
-                while (it > ih && idq[ih & (kIdq - 1)].x < st_in) {
+                while (it > ih && UL(idq[ih & (kIdq - 1)].x) < st_in) {
                     ++ih;
-                    if (it > ih) if_v = idq[ih & (kIdq - 1)].y;
+                    if (it > ih) if_v = UL(idq[ih & (kIdq - 1)].y);
                 }
             }
             CPROF(6);
@@ -1362,7 +1379,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 int32_t b0j = -1;
                 int32_t batch_y = INT32_MAX;  // B's y bound: every committed anchor must lie at or below it
 #if HYMET_CHAIN_YPREFIX
-                if (walk_ok && Lb >= 2) {
+                if (!kLongPass && walk_ok && Lb >= 2) {  // the long join's chained anchors rarely break y order
                     const int offy = (i - cb) + lane;
                     const int32_t ylo_ = __shfl((int32_t)cy, offy & 63, 64), yhi_ = __shfl((int32_t)ny, offy & 63, 64);
                     const int32_t yl = offy < 64 ? ylo_ : yhi_;
@@ -1384,7 +1401,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                     int32_t gj = -1, gy = 0;
                     if (cert) {
                         if (st < (fb << 6)) {
-                            const int4 v = hsuf[st & 63];
+                            const int4 v = UL4(hsuf[st & 63]);
                             gp = st_pr(v), gj = v.z, gy = v.w;
                         }
                         if (fb < fe) {
@@ -1584,7 +1601,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                                 const int vmax = rl(run, 0);
                                 while (it > ih && ib_v <= vmax) {
                                     --it;
-                                    if (it > ih) ib_v = idq[(it - 1) & (kIdq - 1)].y;
+                                    if (it > ih) ib_v = UL(idq[(it - 1) & (kIdq - 1)].y);
                                 }
                                 const bool recd = lane < nins && v > sfx;
                                 const uint64_t rm = __ballot(recd);
@@ -1659,7 +1676,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 int32_t wy = 0, src = -1;
                 if (cert) {
                     if (st < (fb << 6)) {  // partial head block (complete, cached with suffix argmins)
-                        const int4 v = hsuf[st & 63];
+                        const int4 v = UL4(hsuf[st & 63]);
                         bp = st_pr(v), bj = v.z, wy = v.w, src = 0;
                     }
                     if (fb < fe) {
