@@ -40,6 +40,7 @@ _SIGS = {
     "hymet_msh_open": (_i32, [_c.c_char_p, _c.POINTER(_vp)]),
     "hymet_msh_info_get": (_i32, [_vp, _vp]),
     "hymet_msh_copy": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "hymet_msh_upload": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32]),
     "hymet_msh_close": (None, [_vp]),
     "hymet_screen_table_slots": (_i64, [_i64]),
     "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),

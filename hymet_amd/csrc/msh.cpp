@@ -303,6 +303,40 @@ int parse(hymet_msh *m) {
     return HYMET_OK;
 }
 
+// the hashes of the references whose first hash lies in [lo_h, hi_h) of the concatenation (off:
+// n_refs + 1 hash offsets) into dst[lo_h, hi_h), `threads` host threads over equal hash counts;
+// 32-bit sketches widened, any list that is not ascending sorted
+void gather_hashes(const hymet_msh *m, const std::vector<int64_t> &off, int64_t lo_h, int64_t hi_h, int threads,
+                   uint64_t *dst_all) {
+    const int64_t n = m->info.n_refs, span = hi_h - lo_h;
+    if (span <= 0) return;
+    if (span < (1 << 20)) threads = 1;
+    const bool use64 = m->info.use64;
+    parallel_for(threads, threads, [&](int64_t tb, int64_t te) {
+        for (int64_t t = tb; t < te; t++) {
+            // the references whose first hash falls in [a, b) (empty ones need no copy)
+            const int64_t a = lo_h + span * t / threads, b = lo_h + span * (t + 1) / threads;
+            const int64_t i0 = std::lower_bound(off.begin(), off.begin() + n, a) - off.begin();
+            const int64_t i1 = std::lower_bound(off.begin(), off.begin() + n, b) - off.begin();
+            for (int64_t i = i0; i < i1; i++) {
+                const auto &R = m->refs[(size_t)i];
+                uint64_t *dst = dst_all + off[(size_t)i];
+                if (use64) {
+                    memcpy(dst, m->map + R.hash_off, 8 * (size_t)R.n_hash);
+                } else {
+                    const uint8_t *src = m->map + R.hash_off;
+                    for (int64_t j = 0; j < R.n_hash; j++) {
+                        uint32_t v;
+                        memcpy(&v, src + 4 * j, 4);
+                        dst[j] = v;
+                    }
+                }
+                if (!std::is_sorted(dst, dst + R.n_hash)) std::sort(dst, dst + R.n_hash);
+            }
+        }
+    });
+}
+
 }  // namespace
 
 extern "C" {
@@ -369,30 +403,31 @@ int hymet_msh_copy(const hymet_msh *m, int threads, uint64_t *hashes, int64_t *o
     threads = std::max(1, std::min(threads, 64));
     const int64_t total = off[(size_t)n];
     if (total < (1 << 20)) threads = 1;
-    const bool use64 = m->info.use64;
-    parallel_for(threads, threads, [&](int64_t tb, int64_t te) {
-        for (int64_t t = tb; t < te; t++) {
-            // the references whose first hash falls in [lo_h, hi_h) (empty ones need no copy)
-            const int64_t lo_h = total * t / threads, hi_h = total * (t + 1) / threads;
-            const int64_t i0 = std::lower_bound(off.begin(), off.begin() + n, lo_h) - off.begin();
-            const int64_t i1 = std::lower_bound(off.begin(), off.begin() + n, hi_h) - off.begin();
-            for (int64_t i = i0; i < i1; i++) {
-                const auto &R = m->refs[(size_t)i];
-                uint64_t *dst = hashes + off[(size_t)i];
-                if (use64) {
-                    memcpy(dst, m->map + R.hash_off, 8 * (size_t)R.n_hash);
-                } else {
-                    const uint8_t *src = m->map + R.hash_off;
-                    for (int64_t j = 0; j < R.n_hash; j++) {
-                        uint32_t v;
-                        memcpy(&v, src + 4 * j, 4);
-                        dst[j] = v;
-                    }
-                }
-                if (!std::is_sorted(dst, dst + R.n_hash)) std::sort(dst, dst + R.n_hash);
-            }
-        }
-    });
+    gather_hashes(m, off, 0, total, threads, hashes);
+    return HYMET_OK;
+}
+
+int hymet_msh_upload(hymet_ctx *ctx, const hymet_msh *m, int threads, uint64_t *pinned, uint64_t *d_hashes,
+                     int n_chunks) {
+    HY_ARG(ctx && m && (m->info.n_hashes == 0 || (pinned && d_hashes)), "hymet_msh_upload: null argument");
+    const int64_t n = m->info.n_refs;
+    if (n == 0 || m->info.n_hashes == 0) return HYMET_OK;
+    HY_HIP(hipSetDevice(ctx->device));
+    std::vector<int64_t> off((size_t)n + 1, 0);
+    for (int64_t i = 0; i < n; i++) off[(size_t)i + 1] = off[(size_t)i] + m->refs[(size_t)i].n_hash;
+    const int64_t total = off[(size_t)n];
+    threads = std::max(1, std::min(threads, 64));
+    n_chunks = std::max(1, std::min<int>(n_chunks, (int)std::min<int64_t>(n, 64)));
+    int64_t lo = 0;
+    for (int c = 1; c <= n_chunks; c++) {
+        // chunk = the references whose first hash falls below total * c / n_chunks
+        const int64_t r1 = c == n_chunks ? n : std::lower_bound(off.begin(), off.begin() + n, total * c / n_chunks) - off.begin();
+        const int64_t hi = off[(size_t)r1];
+        if (hi <= lo) continue;
+        gather_hashes(m, off, lo, hi, threads, pinned);
+        HY_HIP(hipMemcpyAsync(d_hashes + lo, pinned + lo, 8 * (size_t)(hi - lo), hipMemcpyHostToDevice, ctx->stream));
+        lo = hi;
+    }
     return HYMET_OK;
 }
 

@@ -37,10 +37,39 @@ Besides .msh, `load_db` accepts the repo's own `.npz` sketch format (same fields
 from __future__ import annotations
 
 import struct
+from collections.abc import Sequence
 from dataclasses import dataclass, field
 from typing import List
 
 import numpy as np
+
+
+class NulStrings(Sequence):
+    """The NUL-separated strings of a byte buffer as a read-only sequence, decoded on access:
+    the DB's names and comments are needed only for the references a screen line is printed
+    for (a few thousand of 10^5), so read_msh does not build 2 x 10^5 Python strings per run."""
+
+    def __init__(self, buf: bytes, n: int):
+        self._buf = buf
+        ends = np.flatnonzero(np.frombuffer(buf, np.uint8) == 0)[:n] if n else np.zeros(0, np.int64)
+        self._end = ends
+        self._start = np.r_[0, ends[:-1] + 1] if n else ends
+
+    def __len__(self):
+        return len(self._end)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        return self._buf[int(self._start[i]):int(self._end[i])].decode("utf-8", "replace")
+
+    def __eq__(self, other):
+        return list(self) == list(other)
+
+    def __repr__(self):
+        return f"NulStrings({len(self)})"
 
 
 @dataclass
@@ -183,12 +212,15 @@ class _Struct:
         return [_Struct(self.m, s, t + 1 + j * step, dw, npt) for j in range(cnt)]
 
 
-def read_msh(path, threads: int = 16, alloc=None) -> SketchDB:
+def read_msh(path, threads: int = 16, alloc=None, upload=None) -> SketchDB:
     """.msh -> SketchDB through the library's native reader (hymet_msh_*: mmap, pointer walk
     and a threaded hash gather; S1 of SURVEY.md §8a, on the timed path since `mash screen`
     reads its DB on every call).  alloc(n) may supply the uint64 array the hashes are
-    gathered into (e.g. a view of pinned memory, so the table upload is one DMA).  The
-    library is required, like every product path."""
+    gathered into (e.g. a view of pinned memory, so the table upload is one DMA).
+    upload = (gpu, dev_alloc): alloc must then give pinned memory, and the hashes are gathered
+    in chunks whose DMAs into dev_alloc(n) (a device int64 tensor) are queued on gpu's stream
+    as each chunk is gathered (hymet_msh_upload); the tensor is returned as db.dev_hashes.
+    The library is required, like every product path."""
     import ctypes
     from ._lib import check, load
     lib = load()
@@ -206,18 +238,29 @@ def read_msh(path, threads: int = 16, alloc=None) -> SketchDB:
         names = ctypes.create_string_buffer(max(nb, 1))
         comments = ctypes.create_string_buffer(max(cb, 1))
         alpha = ctypes.create_string_buffer(max(al, 1))
-        check(lib.hymet_msh_copy(h, int(threads), hashes.ctypes.data_as(ctypes.c_void_p),
-                                 offsets.ctypes.data_as(ctypes.c_void_p), lengths.ctypes.data_as(ctypes.c_void_p),
-                                 names, comments, alpha), "hymet_msh_copy")
+        dev = None
+        if upload is not None:
+            g, dev_alloc = upload
+            check(lib.hymet_msh_copy(h, int(threads), None, offsets.ctypes.data_as(ctypes.c_void_p),
+                                     lengths.ctypes.data_as(ctypes.c_void_p), names, comments, alpha), "hymet_msh_copy")
+            dev = dev_alloc(max(n_hashes, 1))
+            check(lib.hymet_msh_upload(g.ctx, h, int(threads), hashes.ctypes.data_as(ctypes.c_void_p),
+                                       ctypes.c_void_p(dev.data_ptr()), 8), "hymet_msh_upload")
+        else:
+            check(lib.hymet_msh_copy(h, int(threads), hashes.ctypes.data_as(ctypes.c_void_p),
+                                     offsets.ctypes.data_as(ctypes.c_void_p), lengths.ctypes.data_as(ctypes.c_void_p),
+                                     names, comments, alpha), "hymet_msh_copy")
     finally:
         lib.hymet_msh_close(h)
 
     def split(buf, n):
-        return buf.raw[:-1].decode("utf-8", "replace").split("\0") if n else []
+        return NulStrings(buf.raw, n) if n else []
 
-    return SketchDB(k=k, seed=seed, sketch_size=ss, alphabet=alpha.raw[:al].decode() or "ACGT", preserve_case=bool(pc),
-                    noncanonical=bool(nonc), window_size=win, names=split(names, n_refs), comments=split(comments, n_refs),
-                    lengths=lengths[:n_refs].copy(), offsets=offsets, hashes=hashes[:n_hashes])
+    db = SketchDB(k=k, seed=seed, sketch_size=ss, alphabet=alpha.raw[:al].decode() or "ACGT", preserve_case=bool(pc),
+                  noncanonical=bool(nonc), window_size=win, names=split(names, n_refs), comments=split(comments, n_refs),
+                  lengths=lengths[:n_refs].copy(), offsets=offsets, hashes=hashes[:n_hashes])
+    db.dev_hashes = dev
+    return db
 
 
 def read_msh_py(path) -> SketchDB:

@@ -328,13 +328,23 @@ class Pipeline:
         self._read_dbs()
         self._build_tables()
 
-    def _read_dbs(self):
+    def _read_dbs(self, side=None):
         """S1 host part: the .msh files parsed and their hashes gathered into pinned memory
-        (no GPU work: run() does it on a second host thread while the contigs are ingested)."""
+        (run() does it on a second host thread while the contigs are ingested).  With `side`
+        (an idle mapping context) the gather goes in chunks whose DMAs into HBM are queued on
+        side's stream as each chunk is gathered (hymet_msh_upload), so the table build that
+        follows finds the hashes in HBM instead of uploading them after the gather."""
         self.tables, self.dbs = [], []
         t0 = time.perf_counter()
-        self.dbs = [read_msh(p, alloc=lambda n, i=i: self._pinned_hashes(i, n).numpy().view(np.uint64)[:n])
-                    for i, p in enumerate(self.db_paths)]
+        dbs = []
+        for i, p in enumerate(self.db_paths):
+            pin = lambda n, i=i: self._pinned_hashes(i, n).numpy().view(np.uint64)[:n]   # noqa: E731
+            if side is None:
+                dbs.append(read_msh(p, alloc=pin))
+            else:
+                with self.gpu.torch.cuda.stream(side.stream):
+                    dbs.append(read_msh(p, alloc=pin, upload=(side, lambda n: side.empty(n, side.torch.int64))))
+        self.dbs = dbs
         self.timings["msh_read_s"] = time.perf_counter() - t0
 
     def _build_tables(self, side=None):
@@ -367,7 +377,7 @@ class Pipeline:
         th.start()
         try:
             if self.db_paths:
-                self._read_dbs()
+                self._read_dbs(side)
                 if side is not None:
                     self._build_tables(side)
         finally:

@@ -30,7 +30,9 @@ class ScreenTable:
 
     def __init__(self, gpu, db: SketchDB, pinned=None):
         """pinned: a pinned host int64 tensor whose first len(db.hashes) entries ARE the
-        hashes (read_msh gathered them there): uploaded by one asynchronous DMA."""
+        hashes (read_msh gathered them there): uploaded by one asynchronous DMA.  A DB read
+        with read_msh(upload=...) carries its hashes in HBM already (db.dev_hashes, the DMAs
+        queued on this context's stream)."""
         torch = gpu.torch
         self.gpu, self.db = gpu, db
         n = int(len(db.hashes))
@@ -38,8 +40,12 @@ class ScreenTable:
         self.n_slots = int(gpu.lib.hymet_screen_table_slots(n))
         self.keys = gpu.empty(self.n_slots, torch.int64)
         self.slot_of = gpu.empty(max(n, 1), torch.int64)
+        dev = getattr(db, "dev_hashes", None)
         if not n:
             d_h = gpu.empty(1, torch.int64)
+        elif dev is not None:
+            d_h = dev
+            db.dev_hashes = None    # consumed: the table build is queued behind the DMAs
         elif pinned is not None:
             d_h = pinned[:n].to(gpu.dev, non_blocking=True)
         else:
