@@ -2268,40 +2268,49 @@ __global__ __launch_bounds__(64) void backtrack_groups_kernel(BacktrackParams P)
 #define HYMET_CHAIN_SMALL 24
 #endif
 constexpr int kSmall = HYMET_CHAIN_SMALL;  // <= 32 (window sets are 32-bit masks)
+// The long join's cut: its groups are chained anchors, which the wave kernel's colinear batches
+// commit faster than the lane kernel replays them from 17 anchors up (Zymo-backbone long join
+// 7.50 -> 7.03 ms per launch on the dump; C4 unchanged).  The first pass keeps kSmall: there
+// the 17-24-anchor groups are repeat hits the lane kernel handles best.
+#ifndef HYMET_CHAIN_SMALL_LONG
+#define HYMET_CHAIN_SMALL_LONG 16
+#endif
+constexpr int kSmallLong = HYMET_CHAIN_SMALL_LONG < kSmall ? HYMET_CHAIN_SMALL_LONG : kSmall;
 
-// first work item whose group has <= kSmall anchors (the list is size-descending)
+// first work item whose group has <= small_max anchors (the list is size-descending)
 // (also zeroes the wave kernel's work counter)
 __global__ void chain_small_split_kernel(const int64_t *g_start, const int32_t *order, int32_t n_work, int32_t *split,
-                                         int32_t *counter) {
+                                         int32_t *counter, int small_max) {
     if (threadIdx.x != 0) return;
     for (int k = 0; k < kChainStripes; k++) counter[k * kChainCtrPad] = 0;
     int32_t lo = 0, hi = n_work;
     while (lo < hi) {
         const int32_t mid = (lo + hi) >> 1;
         const int g = order[mid];
-        if (g_start[g + 1] - g_start[g] <= kSmall) hi = mid;
+        if (g_start[g + 1] - g_start[g] <= small_max) hi = mid;
         else lo = mid + 1;
     }
     *split = lo;
 }
 
 // profiling only: anchors of the work items the wave kernel takes ([0, *split)) into cnt[0] and
-// of those the lane kernel takes into cnt[1] (one block; the bytes of the two profile scopes)
-__global__ __launch_bounds__(1024) void chain_work_anchors_kernel(const int64_t *g_start, const int32_t *order,
-                                                                   int32_t n_work, const int32_t *split, int64_t *cnt) {
+// of those the lane kernel takes into cnt[1] (the bytes of the two profile scopes); a grid-stride
+// pass over the work list, one pair of global atomics per block
+__global__ __launch_bounds__(256) void chain_work_anchors_kernel(const int64_t *g_start, const int32_t *order,
+                                                                  int32_t n_work, const int32_t *split, int64_t *cnt) {
     __shared__ unsigned long long sw, ss;
     if (threadIdx.x == 0) sw = 0, ss = 0;
     __syncthreads();
     const int32_t sp = *split;
     unsigned long long w = 0, s = 0;
-    for (int32_t k = threadIdx.x; k < n_work; k += 1024) {
+    for (int32_t k = blockIdx.x * 256 + threadIdx.x; k < n_work; k += gridDim.x * 256) {
         const int g = order[k];
         const unsigned long long a = (unsigned long long)(g_start[g + 1] - g_start[g]);
         if (k < sp) w += a;
         else s += a;
     }
-    atomicAdd(&sw, w);
-    atomicAdd(&ss, s);
+    for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o), s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&sw, w), atomicAdd(&ss, s);
     __syncthreads();
     if (threadIdx.x == 0) {
         atomicAdd(reinterpret_cast<unsigned long long *>(cnt), sw);
@@ -2402,7 +2411,7 @@ __global__ __launch_bounds__(64) void chain_small_kernel(ChainParams P, const in
 int launch_chain_raw(hipStream_t st, const ChainParams &P0, int64_t blocks, int32_t *split) {
     ChainParams P = P0;
     hipLaunchKernelGGL(chain_small_split_kernel, dim3(1), dim3(64), 0, st, P.g_start, P.order, P.n_work, split,
-                       P.work_counter);
+                       P.work_counter, P.max_dist > 10000 ? kSmallLong : kSmall);
     HY_CHECK_LAUNCH("chain_small_split_kernel");
     P.work_end = split;
     const bool long_pass = P.max_dist > 10000;
@@ -2447,10 +2456,11 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
     {
         ProfScope _ps(ctx, long_pass ? "mm_chain_long" : "mm_chain", slot, 28.0);
         hipLaunchKernelGGL(chain_small_split_kernel, dim3(1), dim3(64), 0, st, P.g_start, P.order, P.n_work,
-                           split.as<int32_t>(), P.work_counter);
+                           split.as<int32_t>(), P.work_counter, long_pass ? kSmallLong : kSmall);
         HY_CHECK_LAUNCH("chain_small_split_kernel");
         if (int64_t *pc = prof_dev_slot(ctx, slot)) {
-            hipLaunchKernelGGL(chain_work_anchors_kernel, dim3(1), dim3(1024), 0, st, P.g_start, P.order, P.n_work,
+            const unsigned wb = (unsigned)std::min<int64_t>(cdiv(P.n_work, 256), 1024);
+            hipLaunchKernelGGL(chain_work_anchors_kernel, dim3(wb), dim3(256), 0, st, P.g_start, P.order, P.n_work,
                                (const int32_t *)split.as<int32_t>(), pc);
             HY_CHECK_LAUNCH("chain_work_anchors_kernel");
         }
