@@ -610,6 +610,11 @@ def bench_emulate(args, gpu, torch):
     # rank's contexts are new streams and would otherwise push the cache past its cap
     gpu.sync()
     gpu.lib.hymet_scratch_trim(gpu.ctx, None)
+    # each rank of an N-rank job loads one slice of every DB's hashes and all-gathers the rest
+    # (Pipeline._join_slices): the stand-in copies them from the whole DB
+    from hymet_amd.msh import read_msh
+    glob["msh_hashes"] = [torch.from_numpy(np.ascontiguousarray(read_msh(p).hashes).view(np.int64)).to(gpu.dev)
+                          for p in pipe1.db_paths]
     fx = FastaIndex(fasta)
     shards = fx.byte_shards(N)          # the records each rank's byte range holds (ingest.shard_bytes)
     glob["shard_records"] = [r1 - r0 for r0, r1 in shards]
@@ -630,6 +635,7 @@ def bench_emulate(args, gpu, torch):
         out_ranks[str(R)] = {
             "shard_records": [int(r0), int(r1)], "shard_mbp": float(fx.nbases[r0:r1].sum()) / 1e6,
             "ms_per_step": te * 1e3, "phases_ms": phe, "stage_ms_per_step": ste,
+            "input_load_ms_last_step": {k.replace("_s", "_ms"): v * 1e3 for k, v in pipe_e.timings.items()},
             "collectives_per_step": [{"kind": k, "bytes_per_rank": int(b)} for k, b in per_step],
             "xgmi_model_ms": model, "predicted_ms_per_step": te * 1e3 + model,
             "tsv_rows": res_e.n_queries, "paf_lines": res_e.n_paf_lines}

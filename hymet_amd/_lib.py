@@ -41,6 +41,7 @@ _SIGS = {
     "hymet_msh_info_get": (_i32, [_vp, _vp]),
     "hymet_msh_copy": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "hymet_msh_upload": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32]),
+    "hymet_msh_upload_range": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32, _i64, _i64]),
     "hymet_msh_close": (None, [_vp]),
     "hymet_screen_table_slots": (_i64, [_i64]),
     "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),

@@ -303,24 +303,31 @@ int parse(hymet_msh *m) {
     return HYMET_OK;
 }
 
-// the hashes of the references whose first hash lies in [lo_h, hi_h) of the concatenation (off:
-// n_refs + 1 hash offsets) into dst[lo_h, hi_h), `threads` host threads over equal hash counts;
-// 32-bit sketches widened, any list that is not ascending sorted
+// dst_all[lo_h, hi_h) = hashes [lo_h, hi_h) of the concatenation (off: n_refs + 1 hash
+// offsets), `threads` host threads over equal hash counts; 32-bit sketches widened, any list
+// that is not ascending sorted; a reference straddling a thread's or the range's bounds is
+// gathered (and sorted if need be) whole into a scratch list and copied in part
 void gather_hashes(const hymet_msh *m, const std::vector<int64_t> &off, int64_t lo_h, int64_t hi_h, int threads,
                    uint64_t *dst_all) {
     const int64_t n = m->info.n_refs, span = hi_h - lo_h;
-    if (span <= 0) return;
+    if (span <= 0 || n <= 0) return;
     if (span < (1 << 20)) threads = 1;
     const bool use64 = m->info.use64;
     parallel_for(threads, threads, [&](int64_t tb, int64_t te) {
+        std::vector<uint64_t> tmp;
         for (int64_t t = tb; t < te; t++) {
-            // the references whose first hash falls in [a, b) (empty ones need no copy)
             const int64_t a = lo_h + span * t / threads, b = lo_h + span * (t + 1) / threads;
-            const int64_t i0 = std::lower_bound(off.begin(), off.begin() + n, a) - off.begin();
-            const int64_t i1 = std::lower_bound(off.begin(), off.begin() + n, b) - off.begin();
-            for (int64_t i = i0; i < i1; i++) {
+            if (a >= b) continue;
+            // the reference holding hash a: the last one starting at or before it
+            int64_t i = std::upper_bound(off.begin(), off.begin() + n + 1, a) - off.begin() - 1;
+            for (; i < n && off[(size_t)i] < b; i++) {
                 const auto &R = m->refs[(size_t)i];
-                uint64_t *dst = dst_all + off[(size_t)i];
+                const int64_t r0 = off[(size_t)i], r1 = off[(size_t)i + 1];
+                const int64_t s = std::max(a, r0), e = std::min(b, r1);
+                if (s >= e) continue;
+                const bool whole = s == r0 && e == r1;
+                if (!whole) tmp.resize((size_t)R.n_hash);
+                uint64_t *dst = whole ? dst_all + r0 : tmp.data();
                 if (use64) {
                     memcpy(dst, m->map + R.hash_off, 8 * (size_t)R.n_hash);
                 } else {
@@ -332,6 +339,7 @@ void gather_hashes(const hymet_msh *m, const std::vector<int64_t> &off, int64_t 
                     }
                 }
                 if (!std::is_sorted(dst, dst + R.n_hash)) std::sort(dst, dst + R.n_hash);
+                if (!whole) memcpy(dst_all + s, dst + (s - r0), 8 * (size_t)(e - s));
             }
         }
     });
@@ -407,28 +415,33 @@ int hymet_msh_copy(const hymet_msh *m, int threads, uint64_t *hashes, int64_t *o
     return HYMET_OK;
 }
 
-int hymet_msh_upload(hymet_ctx *ctx, const hymet_msh *m, int threads, uint64_t *pinned, uint64_t *d_hashes,
-                     int n_chunks) {
-    HY_ARG(ctx && m && (m->info.n_hashes == 0 || (pinned && d_hashes)), "hymet_msh_upload: null argument");
+int hymet_msh_upload_range(hymet_ctx *ctx, const hymet_msh *m, int threads, uint64_t *pinned, uint64_t *d_hashes,
+                           int n_chunks, int64_t lo_h, int64_t hi_h) {
+    HY_ARG(ctx && m, "hymet_msh_upload_range: null argument");
     const int64_t n = m->info.n_refs;
-    if (n == 0 || m->info.n_hashes == 0) return HYMET_OK;
+    HY_ARG(lo_h >= 0 && lo_h <= hi_h && hi_h <= m->info.n_hashes, "hymet_msh_upload_range: bad hash range");
+    if (n == 0 || lo_h == hi_h) return HYMET_OK;
+    HY_ARG(pinned && d_hashes, "hymet_msh_upload_range: null buffer");
     HY_HIP(hipSetDevice(ctx->device));
     std::vector<int64_t> off((size_t)n + 1, 0);
     for (int64_t i = 0; i < n; i++) off[(size_t)i + 1] = off[(size_t)i] + m->refs[(size_t)i].n_hash;
-    const int64_t total = off[(size_t)n];
     threads = std::max(1, std::min(threads, 64));
-    n_chunks = std::max(1, std::min<int>(n_chunks, (int)std::min<int64_t>(n, 64)));
-    int64_t lo = 0;
-    for (int c = 1; c <= n_chunks; c++) {
-        // chunk = the references whose first hash falls below total * c / n_chunks
-        const int64_t r1 = c == n_chunks ? n : std::lower_bound(off.begin(), off.begin() + n, total * c / n_chunks) - off.begin();
-        const int64_t hi = off[(size_t)r1];
+    n_chunks = std::max(1, std::min(n_chunks, 64));
+    const int64_t span = hi_h - lo_h;
+    for (int c = 0; c < n_chunks; c++) {
+        // equal hash counts per chunk; each chunk's DMA is queued as soon as it is gathered
+        const int64_t lo = lo_h + span * c / n_chunks, hi = lo_h + span * (c + 1) / n_chunks;
         if (hi <= lo) continue;
         gather_hashes(m, off, lo, hi, threads, pinned);
         HY_HIP(hipMemcpyAsync(d_hashes + lo, pinned + lo, 8 * (size_t)(hi - lo), hipMemcpyHostToDevice, ctx->stream));
-        lo = hi;
     }
     return HYMET_OK;
+}
+
+int hymet_msh_upload(hymet_ctx *ctx, const hymet_msh *m, int threads, uint64_t *pinned, uint64_t *d_hashes,
+                     int n_chunks) {
+    HY_ARG(ctx && m && (m->info.n_hashes == 0 || (pinned && d_hashes)), "hymet_msh_upload: null argument");
+    return hymet_msh_upload_range(ctx, m, threads, pinned, d_hashes, n_chunks, 0, m->info.n_hashes);
 }
 
 void hymet_msh_close(hymet_msh *m) {

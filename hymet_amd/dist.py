@@ -98,6 +98,22 @@ class Comm:
             out = [o.to(t.device) for o in out]
         return [o[:k] for o, k in zip(out, ns)]
 
+    def allgather_slices_(self, t, c: int, key=None):
+        """t: a device tensor of world * c entries whose slice [rank * c, (rank + 1) * c) this
+        rank filled (its slice of a sketch DB's hashes, read_msh(shard=...)); every other
+        rank's slice is filled in place (RCCL all-gather over xGMI).  key names the DB for
+        EmulatedComm."""
+        if self.world <= 1:
+            return t
+        mine = t[self.rank * c:(self.rank + 1) * c]
+        if self._staged(t):
+            parts = [self.torch.empty(c, dtype=t.dtype) for _ in range(self.world)]
+            self.dist.all_gather(parts, mine.cpu())
+            t[:self.world * c].copy_(self.torch.cat(parts).to(t.device))
+        else:
+            self.dist.all_gather_into_tensor(t[:self.world * c], mine)
+        return t
+
     def gather_rows(self, rows, q_base: int, gpu=None):
         """every rank's LCA rows (fixed-size records: query index in
         the whole input, index part of its first PAF line, depth, taxid, 8 name ids,
@@ -216,6 +232,19 @@ class EmulatedComm(Comm):
                 self.log.append(("allreduce", t.numel() * t.element_size()))
                 return t
         raise ValueError(f"EmulatedComm: no job-wide value for an all-reduce of {t.numel()} x {t.dtype}")
+
+    def allgather_slices_(self, t, c: int, key=None):
+        """The other ranks' slices of sketch DB `key`'s hashes, copied from the job-wide DB
+        (glob["msh_hashes"][key])."""
+        g = self.glob["msh_hashes"][key]
+        n = g.numel()
+        if -(-n // self.world) != c or t.numel() < n:
+            raise ValueError(f"EmulatedComm: DB {key} has {n} hashes, not {self.world} slices of {c}")
+        lo, hi = min(n, self.rank * c), min(n, (self.rank + 1) * c)
+        t[:lo].copy_(g[:lo])
+        t[hi:n].copy_(g[hi:])
+        self.log.append(("allgather", c * t.element_size()))
+        return t
 
     def allgather_np(self, arr: np.ndarray, tag: str = None) -> List[np.ndarray]:
         arr = np.asarray(arr)

@@ -212,7 +212,7 @@ class _Struct:
         return [_Struct(self.m, s, t + 1 + j * step, dw, npt) for j in range(cnt)]
 
 
-def read_msh(path, threads: int = 16, alloc=None, upload=None) -> SketchDB:
+def read_msh(path, threads: int = 16, alloc=None, upload=None, shard=None) -> SketchDB:
     """.msh -> SketchDB through the library's native reader (hymet_msh_*: mmap, pointer walk
     and a threaded hash gather; S1 of SURVEY.md §8a, on the timed path since `mash screen`
     reads its DB on every call).  alloc(n) may supply the uint64 array the hashes are
@@ -220,9 +220,15 @@ def read_msh(path, threads: int = 16, alloc=None, upload=None) -> SketchDB:
     upload = (gpu, dev_alloc): alloc must then give pinned memory, and the hashes are gathered
     in chunks whose DMAs into dev_alloc(n) (a device int64 tensor) are queued on gpu's stream
     as each chunk is gathered (hymet_msh_upload); the tensor is returned as db.dev_hashes.
+    shard = (rank, world), with upload: only this rank's slice of c = ceil(n_hashes / world)
+    hashes, [rank * c, (rank + 1) * c), is gathered and uploaded (hymet_msh_upload_range) into
+    a device tensor of world * c entries, for Comm.allgather_slices_ to fill in the others;
+    db.dev_slice = (lo, hi, c), and db.hashes holds valid hashes only on [lo, hi).
     The library is required, like every product path."""
     import ctypes
     from ._lib import check, load
+    if shard is not None and upload is None:
+        raise ValueError("read_msh: shard needs upload (the slices meet in HBM)")
     lib = load()
     h = ctypes.c_void_p()
     check(lib.hymet_msh_open(str(path).encode(), ctypes.byref(h)), "hymet_msh_open")
@@ -243,9 +249,16 @@ def read_msh(path, threads: int = 16, alloc=None, upload=None) -> SketchDB:
             g, dev_alloc = upload
             check(lib.hymet_msh_copy(h, int(threads), None, offsets.ctypes.data_as(ctypes.c_void_p),
                                      lengths.ctypes.data_as(ctypes.c_void_p), names, comments, alpha), "hymet_msh_copy")
-            dev = dev_alloc(max(n_hashes, 1))
-            check(lib.hymet_msh_upload(g.ctx, h, int(threads), hashes.ctypes.data_as(ctypes.c_void_p),
-                                       ctypes.c_void_p(dev.data_ptr()), 8), "hymet_msh_upload")
+            if shard is None:
+                lo, hi, c, size = 0, n_hashes, n_hashes, n_hashes
+            else:
+                r, w = shard
+                c = -(-n_hashes // w)
+                lo = min(n_hashes, r * c)
+                hi, size = min(n_hashes, lo + c), w * c
+            dev = dev_alloc(max(size, 1))
+            check(lib.hymet_msh_upload_range(g.ctx, h, int(threads), hashes.ctypes.data_as(ctypes.c_void_p),
+                                             ctypes.c_void_p(dev.data_ptr()), 8, lo, hi), "hymet_msh_upload_range")
         else:
             check(lib.hymet_msh_copy(h, int(threads), hashes.ctypes.data_as(ctypes.c_void_p),
                                      offsets.ctypes.data_as(ctypes.c_void_p), lengths.ctypes.data_as(ctypes.c_void_p),
@@ -260,6 +273,7 @@ def read_msh(path, threads: int = 16, alloc=None, upload=None) -> SketchDB:
                   noncanonical=bool(nonc), window_size=win, names=split(names, n_refs), comments=split(comments, n_refs),
                   lengths=lengths[:n_refs].copy(), offsets=offsets, hashes=hashes[:n_hashes])
     db.dev_hashes = dev
+    db.dev_slice = (lo, hi, c) if shard is not None else None
     return db
 
 

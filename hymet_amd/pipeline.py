@@ -337,13 +337,17 @@ class Pipeline:
         self.tables, self.dbs = [], []
         t0 = time.perf_counter()
         dbs = []
+        # more than one rank: this rank gathers and uploads only its slice of each DB's
+        # hashes; run() all-gathers the slices over xGMI (_join_slices) before the tables
+        shard = (self.rank, self.world) if side is not None and self.world > 1 else None
         for i, p in enumerate(self.db_paths):
             pin = lambda n, i=i: self._pinned_hashes(i, n).numpy().view(np.uint64)[:n]   # noqa: E731
             if side is None:
                 dbs.append(read_msh(p, alloc=pin))
             else:
                 with self.gpu.torch.cuda.stream(side.stream):
-                    dbs.append(read_msh(p, alloc=pin, upload=(side, lambda n: side.empty(n, side.torch.int64))))
+                    dbs.append(read_msh(p, alloc=pin, upload=(side, lambda n: side.empty(n, side.torch.int64)),
+                                        shard=shard))
         self.dbs = dbs
         self.timings["msh_read_s"] = time.perf_counter() - t0
 
@@ -378,12 +382,27 @@ class Pipeline:
         try:
             if self.db_paths:
                 self._read_dbs(side)
-                if side is not None:
+                if side is not None and not self._sliced():
                     self._build_tables(side)
         finally:
             th.join()
         if err:
             raise err[0]
+
+    def _sliced(self):
+        return any(getattr(db, "dev_slice", None) is not None for db in self.dbs)
+
+    def _join_slices(self, side):
+        """The DBs' hash slices all-gathered on side's stream (behind this rank's DMAs), then
+        the tables built there.  On the calling thread, between the ingest's and the screen's
+        collectives, so every rank issues its collectives in the same order."""
+        t0 = time.perf_counter()
+        with self.gpu.torch.cuda.stream(side.stream):
+            for i, db in enumerate(self.dbs):
+                if db.dev_slice is not None and db.dev_hashes is not None:
+                    self.comm.allgather_slices_(db.dev_hashes, db.dev_slice[2], key=i)
+        self.timings["msh_allgather_s"] = time.perf_counter() - t0
+        self._build_tables(side)
 
     def _load_classifier(self):
         """C1-C2: detailed_taxonomy.tsv and taxonomy_hierarchy.tsv.  classification_cami.py
@@ -469,8 +488,12 @@ class Pipeline:
     prepare = ingest
 
     def screen_select(self, pool):
+        t0 = time.perf_counter()
         res = scr.screen(self.gpu, pool, self.dbs, self.tables, self.comm)
         self.last_screen = res
+        ph = getattr(self, "phases", None)
+        if ph is not None:                    # the screen's share of run()'s screen_select_s
+            ph["screen_only_s"] = ph.get("screen_only_s", 0.0) + time.perf_counter() - t0
         rows, thr, selections = [], [], []
         for r in res:
             s = sel.sort_gr(sel.sort_unique_k5(r.lines(v_max=0.9)))
@@ -642,14 +665,18 @@ class Pipeline:
             tp[0] = t
         try:
             sh = self.ingest(queries)
+            lap("ingest_s")
         finally:
             if reader is not None:
                 reader.join()
         if err:
             raise err[0]
-        lap("ingest_s")
+        lap("input_wait_s")                   # the loader thread's remainder after the ingest
         if reader is not None and self.db_paths and side is None:
             self._build_tables()
+        elif reader is not None and self._sliced():
+            self._join_slices(side)
+            lap("db_join_s")
         selected, rows, thr = self.screen_select(sh.mash)
         if not selected:
             raise RuntimeError("candidate list empty after applying limit")  # run_hymet_cami.sh:126

@@ -144,13 +144,19 @@ int hymet_msh_info_get(const hymet_msh *m, hymet_msh_info *info);
 int hymet_msh_copy(const hymet_msh *m, int threads, uint64_t *hashes, int64_t *offsets, int64_t *lengths,
                    char *names, char *comments, char *alphabet);
 /* The hashes of every reference (as hymet_msh_copy's `hashes`) gathered into the pinned host
- * array `pinned` in n_chunks chunks of whole references, each chunk's host-to-device DMA into
+ * array `pinned` in n_chunks chunks of equal hash counts, each chunk's host-to-device DMA into
  * `d_hashes` queued on ctx's stream as soon as it is gathered, so the copy of one chunk
  * overlaps the gather of the next.  Returns once every DMA is queued (work queued on the
  * stream afterwards sees the hashes in HBM).  Replaces the gather + one whole upload before
  * the screen table build of `mash screen`'s DB load (scripts/mash.sh:14). */
 int hymet_msh_upload(hymet_ctx *ctx, const hymet_msh *m, int threads, uint64_t *pinned, uint64_t *d_hashes,
                      int n_chunks);
+/* hymet_msh_upload restricted to hashes [lo_h, hi_h) of the concatenation: pinned[lo_h, hi_h)
+ * and d_hashes[lo_h, hi_h) are written, nothing else (references cut by the bounds are copied
+ * in part).  A multi-GPU job's ranks each load one slice of the DB and all-gather the slices
+ * over xGMI instead of every rank parsing the whole file. */
+int hymet_msh_upload_range(hymet_ctx *ctx, const hymet_msh *m, int threads, uint64_t *pinned, uint64_t *d_hashes,
+                           int n_chunks, int64_t lo_h, int64_t hi_h);
 void hymet_msh_close(hymet_msh *m);
 /* Hash every valid canonical k-mer of the packed pool (k in 1..32: MurmurHash3_x64_128
  * word 0 with `seed` for k > 16, MurmurHash3_x86_32 widened to 64 bits for k <= 16, as

@@ -167,7 +167,7 @@ def test_emit_tsv_confidence_rounding(gpu):
     assert got == buf.getvalue().encode()
 
 
-def _world2_worker(rank, port, data_path, tax, hier, q):
+def _world2_worker(rank, port, data_path, msh_path, tax, hier, q):
     import os
     import traceback
     try:
@@ -180,12 +180,18 @@ def _world2_worker(rank, port, data_path, tax, hier, q):
         comm = Comm(rank, 2).init_backend(gpu, "gloo")
         w, db, by_name = _w2_setup(gpu)
         from hymet_amd.seqio import from_records
-        p = pipeline.Pipeline(gpu, [db], lambda ns: from_records([(by_name[n][0], "", by_name[n][1]) for n in ns]),
-                              tax, hier, pipeline.Config(map_batch_bases=300_000), comm)
+        # the DB by path, re-read every run: run 2 loads one slice of its hashes per rank and
+        # all-gathers the other (Pipeline._join_slices)
+        p = pipeline.Pipeline(gpu, [msh_path], lambda ns: from_records([(by_name[n][0], "", by_name[n][1]) for n in ns]),
+                              tax, hier, pipeline.Config(map_batch_bases=300_000, map_streams=2, reload_inputs=True), comm)
         data = open(data_path, "rb").read()
-        res = p.run(data, with_paf=True)
+        out = []
+        for _ in range(2):
+            res = p.run(data, with_paf=True)
+            out.append((res.tsv, res.paf_bytes, res.selected))
+        sliced = p.timings.get("msh_allgather_s") is not None
         comm.close()
-        q.put((rank, "ok", (res.tsv, res.paf_bytes, res.selected)))
+        q.put((rank, "ok", (out, sliced)))
     except Exception:
         q.put((rank, "err", traceback.format_exc()))
 
@@ -201,7 +207,10 @@ def _w2_setup(gpu):
 def test_world2_pipeline_equals_world1(gpu, tmp_path):
     """Two ranks (two processes on this GPU, gloo staging the collectives through the host):
     each takes a contiguous half of the same FASTA; rank 0's TSV equals the one-rank TSV and
-    the ranks' PAF texts concatenate to the one-rank PAF (one index part)."""
+    the ranks' PAF texts concatenate to the one-rank PAF (one index part).  The ranks read the
+    DB from its .msh path on every run; the second run loads it as per-rank hash slices
+    all-gathered between the ranks, and must give the same bytes."""
+    from hymet_amd.msh import write_msh
     import multiprocessing as mpc
     import socket
     from hymet_amd import pipeline
@@ -210,6 +219,8 @@ def test_world2_pipeline_equals_world1(gpu, tmp_path):
     data = _fasta_text(w, quote_name=False)
     dp = tmp_path / "pool.fna"
     dp.write_bytes(data)
+    mp_ = tmp_path / "sketch.msh"
+    write_msh(db, str(mp_))
     p = pipeline.Pipeline(gpu, [db], lambda ns: from_records([(by_name[n][0], "", by_name[n][1]) for n in ns]),
                           str(tax), str(hier), pipeline.Config(map_batch_bases=300_000))
     one = p.run(data, with_paf=True)
@@ -218,7 +229,7 @@ def test_world2_pipeline_equals_world1(gpu, tmp_path):
         port = s.getsockname()[1]
     ctx = mpc.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_world2_worker, args=(r, port, str(dp), str(tax), str(hier), q)) for r in range(2)]
+    ps = [ctx.Process(target=_world2_worker, args=(r, port, str(dp), str(mp_), str(tax), str(hier), q)) for r in range(2)]
     for x in ps:
         x.start()
     got = {}
@@ -228,10 +239,13 @@ def test_world2_pipeline_equals_world1(gpu, tmp_path):
         got[r] = out
     for x in ps:
         x.join(timeout=60)
-    assert got[0][2] == one.selected == got[1][2]
-    assert got[0][0] == one.tsv
-    assert got[1][0] == b""
-    assert got[0][1] + got[1][1] == one.paf_bytes
+    assert got[0][1] and got[1][1]           # run 2 took the sliced DB load on both ranks
+    for k in range(2):
+        r0, r1 = got[0][0][k], got[1][0][k]
+        assert r0[2] == one.selected == r1[2]
+        assert r0[0] == one.tsv
+        assert r1[0] == b""
+        assert r0[1] + r1[1] == one.paf_bytes
 
 
 def test_map_streams_one_and_two_identical(gpu, tmp_path):
