@@ -42,11 +42,12 @@ _SIGS = {
     "hymet_msh_copy": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "hymet_msh_upload": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32]),
     "hymet_msh_upload_range": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32, _i64, _i64]),
+    "hymet_msh_text_offsets": (_i32, [_vp, _vp, _vp]),
     "hymet_msh_close": (None, [_vp]),
     "hymet_screen_table_slots": (_i64, [_i64]),
-    "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
+    "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
     "hymet_screen_count": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _u32, _i32, _c.POINTER(_vp), _c.POINTER(_i64),
-                                  _c.POINTER(_vp), _u64, _vp, _i64, _vp, _vp]),
+                                  _c.POINTER(_vp), _c.POINTER(_i64), _c.POINTER(_vp), _u64, _vp, _i64, _vp, _vp]),
     "hymet_screen_stats": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "hymet_mm_sketch": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i64, _c.POINTER(_i64)]),
     "hymet_mm_index_build": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _c.POINTER(_vp)]),

@@ -345,9 +345,25 @@ void gather_hashes(const hymet_msh *m, const std::vector<int64_t> &off, int64_t 
     });
 }
 
+// start of each reference's name / comment in the NUL-separated pools (n + 1 entries each)
+void text_offsets(const hymet_msh *m, int64_t *name_start, int64_t *comment_start) {
+    const int64_t n = m->info.n_refs;
+    name_start[0] = comment_start[0] = 0;
+    for (int64_t i = 0; i < n; i++) {
+        name_start[i + 1] = name_start[i] + m->refs[(size_t)i].name_len + 1;
+        comment_start[i + 1] = comment_start[i] + m->refs[(size_t)i].comment_len + 1;
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int hymet_msh_text_offsets(const hymet_msh *m, int64_t *name_start, int64_t *comment_start) {
+    HY_ARG(m && name_start && comment_start, "hymet_msh_text_offsets: null argument");
+    text_offsets(m, name_start, comment_start);
+    return HYMET_OK;
+}
 
 int hymet_msh_open(const char *path, hymet_msh **out) {
     HY_ARG(path && out, "hymet_msh_open: null argument");
@@ -390,18 +406,25 @@ int hymet_msh_copy(const hymet_msh *m, int threads, uint64_t *hashes, int64_t *o
     }
     if (lengths)
         for (int64_t i = 0; i < n; i++) lengths[i] = m->refs[(size_t)i].length;
-    // names / comments: NUL-separated, in reference order
-    for (int which = 0; which < 2; which++) {
-        char *dst = which ? comments : names;
-        if (!dst) continue;
-        int64_t o = 0;
-        for (int64_t i = 0; i < n; i++) {
-            const auto &R = m->refs[(size_t)i];
-            const int64_t a = which ? R.comment_off : R.name_off, l = which ? R.comment_len : R.name_len;
-            if (l) memcpy(dst + o, m->map + a, (size_t)l);
-            dst[o + l] = 0;
-            o += l + 1;
-        }
+    // names / comments: NUL-separated, in reference order; the texts lie scattered through the
+    // mapped file (a page fault and a cache miss or two each), so threads take reference ranges
+    if (names || comments) {
+        std::vector<int64_t> no((size_t)n + 1, 0), co((size_t)n + 1, 0);
+        text_offsets(m, no.data(), co.data());
+        const int th = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::max(threads, 1), 16, n / 2048}));
+        parallel_for(th, n, [&](int64_t b, int64_t e) {
+            for (int64_t i = b; i < e; i++) {
+                const auto &R = m->refs[(size_t)i];
+                if (names) {
+                    if (R.name_len) memcpy(names + no[(size_t)i], m->map + R.name_off, (size_t)R.name_len);
+                    names[no[(size_t)i] + R.name_len] = 0;
+                }
+                if (comments) {
+                    if (R.comment_len) memcpy(comments + co[(size_t)i], m->map + R.comment_off, (size_t)R.comment_len);
+                    comments[co[(size_t)i] + R.comment_len] = 0;
+                }
+            }
+        });
     }
     if (alphabet && m->alphabet_len) memcpy(alphabet, m->map + m->alphabet_off, (size_t)m->alphabet_len);
     if (!hashes || n == 0) return HYMET_OK;

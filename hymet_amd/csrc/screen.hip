@@ -2,7 +2,13 @@
 //
 // Kernels
 //   table_insert   : distinct sketch hashes -> open-addressing uint64 table in HBM
-//                    (linear probing from a multiplicative-hash home slot), one atomicCAS per hash.
+//                    (linear probing from a multiplicative-hash home slot), one atomicCAS per hash;
+//                    each slot also keeps the smallest DB hash index holding its key (atomicMin),
+//                    the key's canonical index.  Hit counts are kept per canonical index, in the
+//                    DB's own order: the same on every rank whatever slots the parallel insertion
+//                    gave the keys, so the ranks' counts add up as they are (one all-reduce).
+//   canon_of       : per DB hash, the canonical index of its key (duplicates across references
+//                    share one counter).
 //   screen_count<K>: one thread = one 64-position tile of the pooled, packed query bases.
 //                    Rolling 2-bit forward / reverse-complement words decide the canonical
 //                    strand by integer compare (== Mash's memcmp on ASCII, since A<C<G<T);
@@ -12,7 +18,7 @@
 //                    bumps a uint32 count; hashes under a threshold are appended as bottom-s
 //                    candidates for the pool set-size estimate (MinHashHeap::estimateSetSize).
 //   screen_stats   : one 256-thread block per reference: gather its counts through the
-//                    slot map, shared = #>0, median = k-th smallest positive count by a
+//                    canonical map, shared = #>0, median = k-th smallest positive count by a
 //                    bisection over the value range with block reductions (no sort).
 // Roofline: HBM/latency bound (random 8-B key probes); algorithmic bytes per k-mer are
 // 0.375 (packed read) + 8 per DB probe (+4 per hit), DESIGN.md §Screen.
@@ -110,8 +116,9 @@ struct CountParams {
     const uint64_t *keys[kMaxDb];
     uint64_t mask[kMaxDb];
     int shift[kMaxDb];
-    uint32_t *counts[kMaxDb];
-    uint64_t nslots[kMaxDb];
+    const int32_t *canon[kMaxDb];  // slot -> canonical index of its key
+    uint32_t *counts[kMaxDb];      // per canonical index, + [nhash] for the all-ones hash
+    uint64_t nhash[kMaxDb];
     uint64_t cand_thr;
     uint64_t *cand;
     int64_t cand_cap;
@@ -167,7 +174,7 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
             for (int d = 0; d < kMaxDb; d++) {
                 if (d >= P.ndb) break;
                 if (h == kEmpty) {
-                    atomicAdd(&P.counts[d][P.nslots[d]], 1u);
+                    atomicAdd(&P.counts[d][P.nhash[d]], 1u);
                     continue;
                 }
                 const uint64_t *keys = P.keys[d];
@@ -175,7 +182,7 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
                 for (;;) {
                     const uint64_t key = keys[s];
                     if (key == h) {
-                        atomicAdd(&P.counts[d][s], 1u);
+                        atomicAdd(&P.counts[d][P.canon[d][s]], 1u);
                         break;
                     }
                     if (key == kEmpty) break;
@@ -193,7 +200,7 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
 
 __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t *__restrict__ hashes, int64_t n,
                                                            unsigned long long *keys, uint64_t mask, int shift,
-                                                           int64_t nslots, int64_t *slot_of) {
+                                                           int64_t nslots, int64_t *slot_of, int32_t *canon) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t h = hashes[i];
@@ -207,7 +214,17 @@ __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t *__res
         if (prev == kEmpty || prev == h) break;
         s = (s + 1) & mask;
     }
+    atomicMin(&canon[s], (int32_t)i);
     slot_of[i] = (int64_t)s;
+}
+
+// per DB hash: its key's canonical index (n for the all-ones hash: the extra counter)
+__global__ __launch_bounds__(256) void canon_of_kernel(const int64_t *__restrict__ slot_of, int64_t n, int64_t nslots,
+                                                       const int32_t *__restrict__ canon, int32_t *canon_of) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t s = slot_of[i];
+    canon_of[i] = s == nslots ? (int32_t)n : canon[s];
 }
 
 template <typename T>
@@ -238,7 +255,7 @@ __device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t *red) {
 constexpr int kStatsLds = 4096;
 
 __global__ __launch_bounds__(256) void screen_stats_kernel(const int64_t *__restrict__ ref_off,
-                                                           const int64_t *__restrict__ slot_of,
+                                                           const int32_t *__restrict__ canon_of,
                                                            const uint32_t *__restrict__ counts, uint32_t *shared,
                                                            uint32_t *median) {
     __shared__ uint32_t vals[kStatsLds];
@@ -248,7 +265,7 @@ __global__ __launch_bounds__(256) void screen_stats_kernel(const int64_t *__rest
     const bool in_lds = n <= kStatsLds;
     uint32_t pos = 0, mx = 0;
     for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
-        const uint32_t c = counts[slot_of[b + j]];
+        const uint32_t c = counts[canon_of[b + j]];
         if (in_lds) vals[j] = c;
         pos += c > 0;
         mx = max(mx, c);
@@ -263,7 +280,7 @@ __global__ __launch_bounds__(256) void screen_stats_kernel(const int64_t *__rest
             const uint32_t mid = lo + (hi - lo) / 2;
             uint32_t cnt = 0;
             for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
-                const uint32_t c = in_lds ? vals[j] : counts[slot_of[b + j]];
+                const uint32_t c = in_lds ? vals[j] : counts[canon_of[b + j]];
                 cnt += (c > 0 && c <= mid);
             }
             cnt = block_sum<uint32_t>(cnt, red);
@@ -307,24 +324,30 @@ int64_t hymet_screen_table_slots(int64_t n_hashes) {
 }
 
 int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n, uint64_t *d_keys, int64_t n_slots,
-                             int64_t *d_slot_of) {
-    HY_ARG(ctx && d_keys && d_slot_of, "hymet_screen_table_build: null argument");
+                             int64_t *d_slot_of, int32_t *d_canon, int32_t *d_canon_of) {
+    HY_ARG(ctx && d_keys && d_slot_of && d_canon && d_canon_of, "hymet_screen_table_build: null argument");
     HY_ARG(n_slots >= 1024 && (n_slots & (n_slots - 1)) == 0, "hymet_screen_table_build: n_slots must be a power of two >= 1024");
     HY_ARG(n_slots >= 2 * n, "hymet_screen_table_build: n_slots must be >= 2*n_hashes");
+    HY_ARG(n < (1ll << 31) - 1, "hymet_screen_table_build: more than 2^31 - 2 hashes");
     HY_HIP(hipSetDevice(ctx->device));
     HY_HIP(hipMemsetAsync(d_keys, 0xFF, (size_t)n_slots * 8, ctx->stream));
+    HY_HIP(hipMemsetAsync(d_canon, 0x7F, (size_t)n_slots * 4, ctx->stream));  // INT32_MAX-ish: above any index
     if (n <= 0) return HYMET_OK;
     const int lg = log2_exact(n_slots);
     hymet::ProfScope _ps(ctx, "screen_table_build");
     hipLaunchKernelGGL(table_insert_kernel, dim3((unsigned)hymet::cdiv(n, 256)), dim3(256), 0, ctx->stream, d_hashes, n,
-                       (unsigned long long *)d_keys, (uint64_t)(n_slots - 1), 64 - lg, n_slots, d_slot_of);
+                       (unsigned long long *)d_keys, (uint64_t)(n_slots - 1), 64 - lg, n_slots, d_slot_of, d_canon);
     HY_CHECK_LAUNCH("table_insert_kernel");
+    hipLaunchKernelGGL(canon_of_kernel, dim3((unsigned)hymet::cdiv(n, 256)), dim3(256), 0, ctx->stream,
+                       (const int64_t *)d_slot_of, n, n_slots, (const int32_t *)d_canon, d_canon_of);
+    HY_CHECK_LAUNCH("canon_of_kernel");
     return HYMET_OK;
 }
 
 int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask, int64_t n_bases, int64_t pos_begin,
                        int64_t pos_end, int k, uint32_t seed, int ndb, const uint64_t *const *h_d_keys,
-                       const int64_t *h_n_slots, uint32_t *const *h_d_counts, uint64_t cand_thr, uint64_t *d_cand,
+                       const int64_t *h_n_slots, const int32_t *const *h_d_canon, const int64_t *h_n_hashes,
+                       uint32_t *const *h_d_counts, uint64_t cand_thr, uint64_t *d_cand,
                        int64_t cand_cap, unsigned long long *d_cand_n, unsigned long long *d_nkmers) {
     HY_ARG(ctx && d_2b && d_mask && d_cand_n && d_nkmers, "hymet_screen_count: null argument");
     HY_ARG(k >= 1 && k <= 32, "hymet_screen_count: k must be in 1..32");
@@ -344,11 +367,13 @@ int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_m
     for (int d = 0; d < ndb; d++) {
         const int64_t ns = h_n_slots[d];
         HY_ARG(ns >= 1024 && (ns & (ns - 1)) == 0, "hymet_screen_count: table size must be a power of two");
+        HY_ARG(h_d_keys[d] && h_d_canon[d] && h_d_counts[d] && h_n_hashes[d] >= 0, "hymet_screen_count: null table");
         P.keys[d] = h_d_keys[d];
         P.mask[d] = (uint64_t)(ns - 1);
         P.shift[d] = 64 - log2_exact(ns);
+        P.canon[d] = h_d_canon[d];
         P.counts[d] = h_d_counts[d];
-        P.nslots[d] = (uint64_t)ns;
+        P.nhash[d] = (uint64_t)h_n_hashes[d];
     }
     P.cand_thr = cand_thr;
     P.cand = d_cand;
@@ -369,14 +394,14 @@ int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_m
     return hymet::fail(HYMET_E_ARG, "unreachable k");
 }
 
-int hymet_screen_stats(hymet_ctx *ctx, const int64_t *d_ref_off, int64_t n_refs, const int64_t *d_slot_of,
+int hymet_screen_stats(hymet_ctx *ctx, const int64_t *d_ref_off, int64_t n_refs, const int32_t *d_canon_of,
                        const uint32_t *d_counts, uint32_t *d_shared, uint32_t *d_median) {
-    HY_ARG(ctx && d_ref_off && d_slot_of && d_counts && d_shared && d_median, "hymet_screen_stats: null argument");
+    HY_ARG(ctx && d_ref_off && d_canon_of && d_counts && d_shared && d_median, "hymet_screen_stats: null argument");
     if (n_refs <= 0) return HYMET_OK;
     HY_ARG(n_refs < (1ll << 31), "hymet_screen_stats: too many references");
     HY_HIP(hipSetDevice(ctx->device));
     hymet::ProfScope _ps(ctx, "screen_stats");  // O(H) gather, bytes not modelled
-    hipLaunchKernelGGL(screen_stats_kernel, dim3((unsigned)n_refs), dim3(256), 0, ctx->stream, d_ref_off, d_slot_of,
+    hipLaunchKernelGGL(screen_stats_kernel, dim3((unsigned)n_refs), dim3(256), 0, ctx->stream, d_ref_off, d_canon_of,
                        d_counts, d_shared, d_median);
     HY_CHECK_LAUNCH("screen_stats_kernel");
     return HYMET_OK;

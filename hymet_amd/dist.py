@@ -21,6 +21,7 @@ class Comm:
         self.replicated_pool = replicated_pool
         self.dist = None
         self.device = None
+        self.db_group = None
 
     @classmethod
     def from_env(cls) -> "Comm":
@@ -40,6 +41,9 @@ class Comm:
             if backend == "nccl" and gpu is not None:
                 kw["device_id"] = gpu.dev
             dist.init_process_group(backend, rank=self.rank, world_size=self.world, **kw)
+        # a second communicator over the same ranks for the per-run DB load: its all-gathers
+        # run on the loader thread while the main thread's collectives go over the default one
+        self.db_group = dist.new_group(list(range(self.world)))
         self.dist = dist
         self.device = gpu.dev if gpu is not None else torch.device("cpu")
         self.torch = torch
@@ -101,17 +105,17 @@ class Comm:
     def allgather_slices_(self, t, c: int, key=None):
         """t: a device tensor of world * c entries whose slice [rank * c, (rank + 1) * c) this
         rank filled (its slice of a sketch DB's hashes, read_msh(shard=...)); every other
-        rank's slice is filled in place (RCCL all-gather over xGMI).  key names the DB for
-        EmulatedComm."""
+        rank's slice is filled in place (RCCL all-gather over xGMI) on the DB-load communicator
+        (db_group: called from the loader thread).  key names the DB for EmulatedComm."""
         if self.world <= 1:
             return t
         mine = t[self.rank * c:(self.rank + 1) * c]
         if self._staged(t):
             parts = [self.torch.empty(c, dtype=t.dtype) for _ in range(self.world)]
-            self.dist.all_gather(parts, mine.cpu())
+            self.dist.all_gather(parts, mine.cpu(), group=self.db_group)
             t[:self.world * c].copy_(self.torch.cat(parts).to(t.device))
         else:
-            self.dist.all_gather_into_tensor(t[:self.world * c], mine)
+            self.dist.all_gather_into_tensor(t[:self.world * c], mine, group=self.db_group)
         return t
 
     def gather_rows(self, rows, q_base: int, gpu=None):
@@ -220,10 +224,15 @@ class EmulatedComm(Comm):
         import torch
         self.torch = torch
         self.glob = glob
-        self.log: List[tuple] = []   # (kind, bytes per rank) of every collective since reset_log
+        self.log: List[tuple] = []     # (kind, bytes per rank) of every collective since reset_log
+        self.db_log: List[tuple] = []  # the same for the DB-load communicator (loader thread)
+        import threading
+        self._lock = threading.Lock()
 
     def reset_log(self):
         self.log = []
+        with self._lock:
+            self.db_log = []
 
     def allreduce_sum_(self, t):
         for g in self.glob["screen_by_hash"] + [self.glob["ref_counts"]]:
@@ -243,7 +252,8 @@ class EmulatedComm(Comm):
         lo, hi = min(n, self.rank * c), min(n, (self.rank + 1) * c)
         t[:lo].copy_(g[:lo])
         t[hi:n].copy_(g[hi:])
-        self.log.append(("allgather", c * t.element_size()))
+        with self._lock:                       # the loader thread's entry
+            self.db_log.append(("allgather", c * t.element_size()))
         return t
 
     def allgather_np(self, arr: np.ndarray, tag: str = None) -> List[np.ndarray]:

@@ -49,8 +49,14 @@ class NulStrings(Sequence):
     the DB's names and comments are needed only for the references a screen line is printed
     for (a few thousand of 10^5), so read_msh does not build 2 x 10^5 Python strings per run."""
 
-    def __init__(self, buf: bytes, n: int):
-        self._buf = buf
+    def __init__(self, buf, n: int, starts=None):
+        """buf: bytes or a uint8 array; starts: the n + 1 string starts if known (the native
+        reader gives them), else found by a NUL scan."""
+        self._buf = buf if isinstance(buf, (bytes, bytearray)) else memoryview(np.ascontiguousarray(buf, np.uint8))
+        if starts is not None:
+            self._start = np.asarray(starts[:n], np.int64)
+            self._end = np.asarray(starts[1:n + 1], np.int64) - 1
+            return
         ends = np.flatnonzero(np.frombuffer(buf, np.uint8) == 0)[:n] if n else np.zeros(0, np.int64)
         self._end = ends
         self._start = np.r_[0, ends[:-1] + 1] if n else ends
@@ -63,7 +69,7 @@ class NulStrings(Sequence):
             return [self[j] for j in range(*i.indices(len(self)))]
         if i < 0:
             i += len(self)
-        return self._buf[int(self._start[i]):int(self._end[i])].decode("utf-8", "replace")
+        return bytes(self._buf[int(self._start[i]):int(self._end[i])]).decode("utf-8", "replace")
 
     def __eq__(self, other):
         return list(self) == list(other)
@@ -231,7 +237,10 @@ def read_msh(path, threads: int = 16, alloc=None, upload=None, shard=None) -> Sk
         raise ValueError("read_msh: shard needs upload (the slices meet in HBM)")
     lib = load()
     h = ctypes.c_void_p()
+    import time
+    t0 = time.perf_counter()
     check(lib.hymet_msh_open(str(path).encode(), ctypes.byref(h)), "hymet_msh_open")
+    t1 = t2 = time.perf_counter()
     try:
         raw = (ctypes.c_int64 * 9)()   # hymet_msh_info: 7 int32 (+4 pad) then 5 int64
         check(lib.hymet_msh_info_get(h, ctypes.byref(raw)), "hymet_msh_info_get")
@@ -241,14 +250,21 @@ def read_msh(path, threads: int = 16, alloc=None, upload=None, shard=None) -> Sk
         hashes = alloc(max(n_hashes, 1)) if alloc is not None else np.empty(max(n_hashes, 1), np.uint64)
         offsets = np.empty(n_refs + 1, np.int64)
         lengths = np.empty(max(n_refs, 1), np.int64)
-        names = ctypes.create_string_buffer(max(nb, 1))
-        comments = ctypes.create_string_buffer(max(cb, 1))
+        # uninitialised pools (the reader writes every byte; create_string_buffer zeroes ~10 MB)
+        names_a = np.empty(max(nb, 1), np.uint8)
+        comments_a = np.empty(max(cb, 1), np.uint8)
+        names, comments = (ctypes.c_void_p(a.ctypes.data) for a in (names_a, comments_a))
         alpha = ctypes.create_string_buffer(max(al, 1))
+        name_st = np.empty(n_refs + 1, np.int64)
+        comment_st = np.empty(n_refs + 1, np.int64)
+        check(lib.hymet_msh_text_offsets(h, name_st.ctypes.data_as(ctypes.c_void_p),
+                                         comment_st.ctypes.data_as(ctypes.c_void_p)), "hymet_msh_text_offsets")
         dev = None
         if upload is not None:
             g, dev_alloc = upload
             check(lib.hymet_msh_copy(h, int(threads), None, offsets.ctypes.data_as(ctypes.c_void_p),
                                      lengths.ctypes.data_as(ctypes.c_void_p), names, comments, alpha), "hymet_msh_copy")
+            t2 = time.perf_counter()
             if shard is None:
                 lo, hi, c, size = 0, n_hashes, n_hashes, n_hashes
             else:
@@ -265,15 +281,17 @@ def read_msh(path, threads: int = 16, alloc=None, upload=None, shard=None) -> Sk
                                      names, comments, alpha), "hymet_msh_copy")
     finally:
         lib.hymet_msh_close(h)
+    t3 = time.perf_counter()
 
-    def split(buf, n):
-        return NulStrings(buf.raw, n) if n else []
+    def split(buf, n, st):
+        return NulStrings(buf, n, st) if n else []
 
     db = SketchDB(k=k, seed=seed, sketch_size=ss, alphabet=alpha.raw[:al].decode() or "ACGT", preserve_case=bool(pc),
-                  noncanonical=bool(nonc), window_size=win, names=split(names, n_refs), comments=split(comments, n_refs),
+                  noncanonical=bool(nonc), window_size=win, names=split(names_a, n_refs, name_st), comments=split(comments_a, n_refs, comment_st),
                   lengths=lengths[:n_refs].copy(), offsets=offsets, hashes=hashes[:n_hashes])
     db.dev_hashes = dev
     db.dev_slice = (lo, hi, c) if shard is not None else None
+    db.load_s = {"open": t1 - t0, "meta": t2 - t1, "hashes": t3 - t2, "wrap": time.perf_counter() - t3}
     return db
 
 

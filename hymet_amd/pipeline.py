@@ -250,15 +250,18 @@ _bytes_new.restype = _c.py_object
 _bytes_new.argtypes = [_c.c_void_p, _c.c_ssize_t]
 
 
-def _to_host(gpu, bufs, key, dev, n) -> bytes:
-    """D2H of n bytes into a new bytes object through the library's double-buffered pinned
-    staging (16 host copy threads): no torch pinned buffer and no extra bytes copy, which
-    cost ~0.35 s per GB of PAF text."""
+def _to_host(gpu, bufs, key, dev, n, prefix: bytes = b"") -> bytes:
+    """prefix + n bytes of device memory, as a new bytes object filled through the library's
+    double-buffered pinned staging (16 host copy threads): no torch pinned buffer and no
+    extra bytes copy (a copy cost ~0.35 s per GB of PAF text; prefix + text would be one)."""
     if n == 0:
-        return b""
-    b = _bytes_new(None, int(n))  # uninitialised, filled below before anyone sees it
+        return bytes(prefix)
+    m = len(prefix)
+    b = _bytes_new(None, int(n) + m)  # uninitialised, filled below before anyone sees it
     addr = _c.cast(_c.c_char_p(b), _c.c_void_p).value
-    check(gpu.lib.hymet_copy_to_host(gpu.ctx, addr, ptr(dev), int(n), 16), "hymet_copy_to_host")
+    if m:
+        _c.memmove(addr, prefix, m)
+    check(gpu.lib.hymet_copy_to_host(gpu.ctx, addr + m, ptr(dev), int(n), 16), "hymet_copy_to_host")
     return b
 
 
@@ -350,6 +353,8 @@ class Pipeline:
                                         shard=shard))
         self.dbs = dbs
         self.timings["msh_read_s"] = time.perf_counter() - t0
+        for k in ("open", "meta", "hashes"):    # read_msh's own phases, summed over the DBs
+            self.timings[f"msh_{k}_s"] = sum(getattr(db, "load_s", {}).get(k, 0.0) for db in dbs)
 
     def _build_tables(self, side=None):
         """S1 device part: the pinned hashes uploaded by DMA and the HBM tables built -- on
@@ -362,6 +367,7 @@ class Pipeline:
         else:
             with self.gpu.torch.cuda.stream(side.stream):
                 self.tables = [scr.ScreenTable(side, db, pinned=self._pin[i]) for i, db in enumerate(self.dbs)]
+            self.timings["screen_table_enqueue_s"] = time.perf_counter() - t1
             side.stream.synchronize()
         self.timings["screen_table_s"] = time.perf_counter() - t1
 
@@ -382,7 +388,9 @@ class Pipeline:
         try:
             if self.db_paths:
                 self._read_dbs(side)
-                if side is not None and not self._sliced():
+                if side is not None and self._sliced():
+                    self._join_slices(side)
+                elif side is not None:
                     self._build_tables(side)
         finally:
             th.join()
@@ -394,8 +402,10 @@ class Pipeline:
 
     def _join_slices(self, side):
         """The DBs' hash slices all-gathered on side's stream (behind this rank's DMAs), then
-        the tables built there.  On the calling thread, between the ingest's and the screen's
-        collectives, so every rank issues its collectives in the same order."""
+        the tables built there -- on the loader thread, overlapping the contigs' ingest.  The
+        all-gathers go over the communicator Comm keeps for the DB load alone (Comm.db_group),
+        so they cannot interleave with the main thread's collectives: every rank issues the
+        DB all-gathers in DB order on one communicator, the rest in run order on the other."""
         t0 = time.perf_counter()
         with self.gpu.torch.cuda.stream(side.stream):
             for i, db in enumerate(self.dbs):
@@ -571,7 +581,7 @@ class Pipeline:
                 continue
             check(rc, "hymet_emit_tsv")
             break
-        return TSV_HEADER + self._to_host("tsv_h", out, nb.value)
+        return self._to_host("tsv_h", out, nb.value, prefix=TSV_HEADER)
 
     def emit_paf(self, ix: IndexSet, sh: QueryShard) -> HostText:
         """This rank's resultados.paf text (its queries' lines, part-major), written on the
@@ -634,8 +644,8 @@ class Pipeline:
     def _dev_buf(self, key, nbytes):
         return _dev_buf(self.gpu, self._bufs, key, nbytes)
 
-    def _to_host(self, key, dev, n) -> bytes:
-        return _to_host(self.gpu, self._bufs, key, dev, n)
+    def _to_host(self, key, dev, n, prefix: bytes = b"") -> bytes:
+        return _to_host(self.gpu, self._bufs, key, dev, n, prefix)
 
     # ------------------------------------------------------------------- run
     def run(self, queries, with_paf=False) -> RunResult:
@@ -649,10 +659,12 @@ class Pipeline:
             import threading
 
             def read():
+                t0 = time.perf_counter()
                 try:
                     self._read_inputs(side)
                 except BaseException as e:  # noqa: BLE001 -- re-raised on the calling thread
                     err.append(e)
+                self.timings["reader_s"] = time.perf_counter() - t0
             reader = threading.Thread(target=read, name="hymet-inputs")
             reader.start()
         self._ran = True
@@ -674,9 +686,6 @@ class Pipeline:
         lap("input_wait_s")                   # the loader thread's remainder after the ingest
         if reader is not None and self.db_paths and side is None:
             self._build_tables()
-        elif reader is not None and self._sliced():
-            self._join_slices(side)
-            lap("db_join_s")
         selected, rows, thr = self.screen_select(sh.mash)
         if not selected:
             raise RuntimeError("candidate list empty after applying limit")  # run_hymet_cami.sh:126

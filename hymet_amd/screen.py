@@ -26,7 +26,8 @@ U64_MAX = (1 << 64) - 1
 
 
 class ScreenTable:
-    """One sketch DB resident in HBM: open-addressing key table + slot map + CSR offsets."""
+    """One sketch DB resident in HBM: open-addressing key table, the canonical index of each
+    slot's key and of each DB hash (hit counts live in the DB's own hash order), CSR offsets."""
 
     def __init__(self, gpu, db: SketchDB, pinned=None):
         """pinned: a pinned host int64 tensor whose first len(db.hashes) entries ARE the
@@ -39,7 +40,9 @@ class ScreenTable:
         self.n_hashes = n
         self.n_slots = int(gpu.lib.hymet_screen_table_slots(n))
         self.keys = gpu.empty(self.n_slots, torch.int64)
-        self.slot_of = gpu.empty(max(n, 1), torch.int64)
+        self.canon = gpu.empty(self.n_slots, torch.int32)
+        self.canon_of = gpu.empty(max(n, 1), torch.int32)
+        slot_of = gpu.empty(max(n, 1), torch.int64)      # build scratch
         dev = getattr(db, "dev_hashes", None)
         if not n:
             d_h = gpu.empty(1, torch.int64)
@@ -50,9 +53,10 @@ class ScreenTable:
             d_h = pinned[:n].to(gpu.dev, non_blocking=True)
         else:
             d_h = torch.from_numpy(np.ascontiguousarray(db.hashes).view(np.int64)).to(gpu.dev)
-        gpu.call("hymet_screen_table_build", ptr(d_h), n, ptr(self.keys), self.n_slots, ptr(self.slot_of))
+        gpu.call("hymet_screen_table_build", ptr(d_h), n, ptr(self.keys), self.n_slots, ptr(slot_of), ptr(self.canon),
+                 ptr(self.canon_of))
         self.ref_off = torch.from_numpy(np.ascontiguousarray(db.offsets, dtype=np.int64)).to(gpu.dev)
-        del d_h
+        del d_h, slot_of
 
 
 @dataclass
@@ -81,7 +85,7 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
     if pos_end is None:
         pos_end = max(0, n_bases - k + 1)
     span = max(1, pos_end - pos_begin)
-    counts = [gpu.zeros(t.n_slots + 1, torch.int32) for t in tables]
+    counts = [gpu.zeros(t.n_hashes + 1, torch.int32) for t in tables]   # by canonical index
     cap = 64 * s + 65536
     cand = gpu.empty(cap, torch.int64)
     cand_n = gpu.zeros(1, torch.int64)
@@ -91,9 +95,11 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
     thr = U64_MAX if frac >= 1.0 else int(frac * float(top))
     keys_arr = (ctypes.c_void_p * 4)(*[ptr(t.keys).value for t in tables])
     slots_arr = (ctypes.c_int64 * 4)(*[t.n_slots for t in tables])
+    canon_arr = (ctypes.c_void_p * 4)(*[ptr(t.canon).value for t in tables])
+    nh_arr = (ctypes.c_int64 * 4)(*[t.n_hashes for t in tables])
     cnt_arr = (ctypes.c_void_p * 4)(*[ptr(c).value for c in counts])
     gpu.call("hymet_screen_count", ptr(pool.w2b), ptr(pool.wmask), n_bases, pos_begin, pos_end, k, seed,
-             len(tables), keys_arr, slots_arr, cnt_arr, thr, ptr(cand), cap, ptr(cand_n), ptr(nk))
+             len(tables), keys_arr, slots_arr, canon_arr, nh_arr, cnt_arr, thr, ptr(cand), cap, ptr(cand_n), ptr(nk))
     n_kmers = int(nk.item())
     dummy = gpu.zeros(1, torch.int64)
 
@@ -101,7 +107,7 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
         buf = gpu.empty(cap_, torch.int64)
         cand_n.zero_()
         gpu.call("hymet_screen_count", ptr(pool.w2b), ptr(pool.wmask), n_bases, pos_begin, pos_end, k, seed,
-                 0, keys_arr, slots_arr, cnt_arr, thr_, ptr(buf), cap_, ptr(cand_n), ptr(dummy))
+                 0, keys_arr, slots_arr, canon_arr, nh_arr, cnt_arr, thr_, ptr(buf), cap_, ptr(cand_n), ptr(dummy))
         return buf
 
     while True:
@@ -126,18 +132,14 @@ def reduce_partials(comm, counts, bottom: np.ndarray, nk: int, s: int, tables=No
     s of the union of the ranks' candidates, and the k-mer totals add up.
 
     Every rank builds its own open-addressing table and parallel insertion makes slot
-    positions rank-specific, so counts are exchanged in the DB's hash order (gathered
-    through slot_of, summed, scattered back), never by slot."""
+    positions rank-specific, but the counts are kept per canonical index (the smallest DB
+    hash index holding the key, csrc/screen.hip), i.e. in the DB's own order, the same on
+    every rank: they are all-reduced as they are (round 4 gathered them out of slot order
+    and scattered them back, ~7 ms of random accesses per step on a 1e8-hash DB)."""
     if comm is None or comm.world <= 1:
         return counts, bottom, nk
-    for i, c in enumerate(counts):
-        if tables is None:
-            comm.allreduce_sum_(c)          # slot-aligned partials (tests)
-            continue
-        so = tables[i].slot_of[:tables[i].n_hashes]
-        by_hash = c[so]
-        comm.allreduce_sum_(by_hash)
-        c[so] = by_hash
+    for c in counts:
+        comm.allreduce_sum_(c)
     bottom = _bottom_s(np.concatenate(comm.allgather_np(np.asarray(bottom, np.uint64), tag="bottom")), s)
     nk = int(sum(int(x[0]) for x in comm.allgather_np(np.array([nk], dtype=np.int64), tag="n_kmers")))
     return counts, bottom, nk
@@ -162,7 +164,7 @@ def table_stats(gpu, t: ScreenTable, counts):
     sh = gpu.zeros(max(n, 1), torch.int32)
     md = gpu.zeros(max(n, 1), torch.int32)
     if n:
-        gpu.call("hymet_screen_stats", ptr(t.ref_off), n, ptr(t.slot_of), ptr(counts), ptr(sh), ptr(md))
+        gpu.call("hymet_screen_stats", ptr(t.ref_off), n, ptr(t.canon_of), ptr(counts), ptr(sh), ptr(md))
     return sh[:n].cpu().numpy().view(np.uint32).copy(), md[:n].cpu().numpy().view(np.uint32).copy()
 
 

@@ -111,9 +111,14 @@ int hymet_name_hash(hymet_ctx *ctx, const uint8_t *d_raw, const int64_t *d_name_
  * per-reference shared / median-depth statistics. */
 int64_t hymet_screen_table_slots(int64_t n_hashes);
 /* d_keys: n_slots uint64; d_slot_of: n_hashes int64 (slot of each input hash, n_slots for
- * the reserved all-ones key).  Resets d_keys itself. */
+ * the reserved all-ones key); d_canon: n_slots int32, the smallest input index holding each
+ * slot's key (its canonical index); d_canon_of: n_hashes int32, each input hash's canonical
+ * index (n_hashes for the all-ones key).  Hits are counted per canonical index, so counts are
+ * in the DB's own order on every rank whatever slots parallel insertion chose, and the
+ * ranks' partial counts add up as they are.  Resets d_keys and d_canon. */
 int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n_hashes,
-                             uint64_t *d_keys, int64_t n_slots, int64_t *d_slot_of);
+                             uint64_t *d_keys, int64_t n_slots, int64_t *d_slot_of, int32_t *d_canon,
+                             int32_t *d_canon_of);
 /* The library's stable LSD radix sort (8-bit digits) of device (key, value) pairs by key bits
  * [begin_bit, end_bit), in place (the sort behind the mapper's minimizer, group, chain and
  * anchor-segment orders and the LCA row order; no rocPRIM on the mapping path). */
@@ -143,6 +148,10 @@ int hymet_msh_open(const char *path, hymet_msh **out);
 int hymet_msh_info_get(const hymet_msh *m, hymet_msh_info *info);
 int hymet_msh_copy(const hymet_msh *m, int threads, uint64_t *hashes, int64_t *offsets, int64_t *lengths,
                    char *names, char *comments, char *alphabet);
+/* Where each reference's name and comment start in hymet_msh_copy's NUL-separated pools
+ * (n_refs + 1 entries each, the last = the pool size): the host reader indexes the pools
+ * without scanning them for NULs. */
+int hymet_msh_text_offsets(const hymet_msh *m, int64_t *name_start, int64_t *comment_start);
 /* The hashes of every reference (as hymet_msh_copy's `hashes`) gathered into the pinned host
  * array `pinned` in n_chunks chunks of equal hash counts, each chunk's host-to-device DMA into
  * `d_hashes` queued on ctx's stream as soon as it is gathered, so the copy of one chunk
@@ -160,20 +169,23 @@ int hymet_msh_upload_range(hymet_ctx *ctx, const hymet_msh *m, int threads, uint
 void hymet_msh_close(hymet_msh *m);
 /* Hash every valid canonical k-mer of the packed pool (k in 1..32: MurmurHash3_x64_128
  * word 0 with `seed` for k > 16, MurmurHash3_x86_32 widened to 64 bits for k <= 16, as
- * Mash's 64- / 32-bit sketches), probe ndb (<= 4) tables, count hits into d_counts[i] (n_slots[i]+1
- * uint32 each, caller-zeroed), and append every hash < cand_thr to d_cand (bottom-s
+ * Mash's 64- / 32-bit sketches), probe ndb (<= 4) tables, count hits into d_counts[i] at the
+ * hit key's canonical index (h_d_canon[i]; n_hashes[i]+1 uint32 each, caller-zeroed, the last
+ * for the all-ones hash), and append every hash < cand_thr to d_cand (bottom-s
  * candidates; d_cand_n counts appends, may exceed cand_cap).  d_nkmers += valid k-mers.
  * seq_begin/seq_end limit the k-mer START positions processed (for sharding). */
 int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask,
                        int64_t n_bases, int64_t pos_begin, int64_t pos_end, int k, uint32_t seed,
                        int ndb, const uint64_t *const *h_d_keys, const int64_t *h_n_slots,
+                       const int32_t *const *h_d_canon, const int64_t *h_n_hashes,
                        uint32_t *const *h_d_counts, uint64_t cand_thr, uint64_t *d_cand,
                        int64_t cand_cap, unsigned long long *d_cand_n,
                        unsigned long long *d_nkmers);
-/* Per reference r (hashes d_ref_off[r]..d_ref_off[r+1] of the table input):
- * shared[r] = #hashes with count > 0; median[r] = sorted positive counts[shared/2]. */
+/* Per reference r (hashes d_ref_off[r]..d_ref_off[r+1] of the table input, each counted at
+ * d_canon_of[j]): shared[r] = #hashes with count > 0; median[r] = sorted positive
+ * counts[shared/2]. */
 int hymet_screen_stats(hymet_ctx *ctx, const int64_t *d_ref_off, int64_t n_refs,
-                       const int64_t *d_slot_of, const uint32_t *d_counts, uint32_t *d_shared,
+                       const int32_t *d_canon_of, const uint32_t *d_counts, uint32_t *d_shared,
                        uint32_t *d_median);
 
 /* --------------------------------------------------- minimizer index (minimap2 -d)

@@ -85,20 +85,38 @@ def test_screen_partials_reduce_like_one_pool():
 
 
 def _screen_perm_fn(comm):
-    """Each rank's table puts the same hashes in different slots (parallel insertion order):
-    the exchange must line counts up by hash, not by slot."""
-    import types
+    """Each rank's table puts the same hashes in different slots (its own insertion order, as
+    parallel insertion does); hits are counted per canonical index -- the smallest DB index
+    holding the key, kept per slot (csrc/screen.hip table_insert_kernel) -- so the ranks'
+    count arrays line up by hash and add up as they are."""
     import torch
     from hymet_amd.screen import reduce_partials
     rng = np.random.default_rng(21)
     H, S = 300, 1024
-    per_hash = [rng.integers(0, 4, size=H).astype(np.int32) for _ in range(2)]      # [rank] hits per hash
-    slot_of = np.random.default_rng(100 + comm.rank).permutation(S)[:H].astype(np.int64)
-    c = torch.zeros(S + 1, dtype=torch.int32)
-    c[torch.from_numpy(slot_of)] = torch.from_numpy(per_hash[comm.rank])
-    tab = types.SimpleNamespace(slot_of=torch.from_numpy(slot_of), n_hashes=H)
-    out, _, _ = reduce_partials(comm, [c], np.zeros(0, np.uint64), 0, 10, [tab])
-    return out[0][torch.from_numpy(slot_of)].numpy(), per_hash[0] + per_hash[1]
+    keys = rng.integers(0, 200, size=H)            # duplicates: one key in several references
+    hits = [rng.integers(0, 200, size=500) for _ in range(2)]   # [rank] the k-mer keys it sees
+    # this rank's table: insertion in a rank-specific order, linear probing, canon = min index
+    order = np.random.default_rng(100 + comm.rank).permutation(H)
+    slot_key, slot_canon = {}, {}
+    home = (np.random.default_rng(7).permutation(S))          # a fixed home slot per key value
+    slot_of = np.zeros(H, np.int64)
+    for j in order:
+        s = int(home[keys[j] % S])
+        while s in slot_key and slot_key[s] != keys[j]:
+            s = (s + 1) % S
+        slot_key[s] = keys[j]
+        slot_canon[s] = min(slot_canon.get(s, H), int(j))
+        slot_of[j] = s
+    canon_of = np.array([slot_canon[int(slot_of[j])] for j in range(H)])
+    by_key = {v: s for s, v in slot_key.items()}
+    c = torch.zeros(H + 1, dtype=torch.int32)
+    for k in hits[comm.rank]:
+        if k in by_key:
+            c[slot_canon[by_key[k]]] += 1
+    out, _, _ = reduce_partials(comm, [c], np.zeros(0, np.uint64), 0, 10, None)
+    got = out[0][torch.from_numpy(canon_of)].numpy()          # per DB hash, as screen_stats reads
+    exp = np.array([sum(int((h == keys[j]).sum()) for h in hits) for j in range(H)], np.int32)
+    return got, exp
 
 
 def test_screen_counts_reduce_by_hash_not_slot():
