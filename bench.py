@@ -131,6 +131,14 @@ def gpu_scratch_gb(gpu):
     return tot / 1e9
 
 
+def scratch_stats(gpu):
+    """The scratch allocator's (hipMalloc calls, OOM cache drops, frees past the cap) so far."""
+    import numpy as _np
+    v = _np.zeros(3, _np.int64)
+    gpu.lib.hymet_scratch_stats(gpu.ctx, v.ctypes.data)
+    return [int(x) for x in v]
+
+
 def cpu_info():
     model = ""
     try:
@@ -272,6 +280,7 @@ def bench_cami(args, comm, gpu, torch):
     gpu.prof(True)
     torch.cuda.synchronize()
     comm.barrier()
+    ss0 = scratch_stats(gpu)
     t0 = time.perf_counter()
     prof_host = os.environ.get("HYMET_BENCH_PYPROF") and comm.rank == 0
     if prof_host:
@@ -325,6 +334,11 @@ def bench_cami(args, comm, gpu, torch):
                              "every step)"},
         "cold_run_s": cold,
         "scratch_cached_gb": gpu_scratch_gb(gpu),
+        # allocator events inside the timed steps (hipMalloc, OOM drops, over-cap frees): each
+        # can synchronise the device; a steady state has none
+        "scratch_events_timed": [b - a for a, b in zip(ss0, scratch_stats(gpu))],
+        "hbm_free_gb": torch.cuda.mem_get_info(gpu.dev)[0] / 1e9,
+        "torch_reserved_gb": torch.cuda.memory_reserved(gpu.dev) / 1e9,
         "paf_lines": n_lines,
         "kernel_ms_per_step_rank0": kern_ms,
         "stage_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},

@@ -28,6 +28,7 @@ _SIGS = {
     "hymet_prof_names": (_i32, [_vp, _c.c_char_p, _i64]),
     "hymet_scratch_trim": (_i32, [_vp, _c.POINTER(_i64)]),
     "hymet_scratch_cached": (_i32, [_vp, _c.POINTER(_i64)]),
+    "hymet_scratch_stats": (_i32, [_vp, _vp]),
     "hymet_copy_to_host": (_i32, [_vp, _vp, _vp, _i64, _i32]),
     "hymet_copy_to_device": (_i32, [_vp, _vp, _vp, _i64, _i32]),
     "hymet_pack": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
@@ -45,9 +46,9 @@ _SIGS = {
     "hymet_msh_text_offsets": (_i32, [_vp, _vp, _vp]),
     "hymet_msh_close": (None, [_vp]),
     "hymet_screen_table_slots": (_i64, [_i64]),
-    "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _vp]),
     "hymet_screen_count": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _u32, _i32, _c.POINTER(_vp), _c.POINTER(_i64),
-                                  _c.POINTER(_vp), _c.POINTER(_i64), _c.POINTER(_vp), _u64, _vp, _i64, _vp, _vp]),
+                                  _c.POINTER(_i64), _c.POINTER(_vp), _u64, _vp, _i64, _vp, _vp]),
     "hymet_screen_stats": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "hymet_mm_sketch": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i64, _c.POINTER(_i64)]),
     "hymet_mm_index_build": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _c.POINTER(_vp)]),

@@ -35,6 +35,7 @@ struct CacheKey {
 };
 static std::map<CacheKey, std::vector<void *>> g_cache;  // free blocks
 static size_t g_cached = 0;                                // bytes held in g_cache
+static int64_t g_stats[3] = {0, 0, 0};  // hipMalloc calls (cache misses), OOM cache drops, frees over the cap
 
 static size_t cache_cap() {
     static const size_t cap = [] {
@@ -84,10 +85,15 @@ hipError_t scratch_alloc(size_t bytes, hipStream_t stream, void **p, size_t *cls
         }
     }
     e = hipMalloc(p, *cls);
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        g_stats[0]++;
+    }
     if (e == hipErrorOutOfMemory) {  // give the cached blocks of this device back and retry once
         (void)hipGetLastError();
         (void)hipDeviceSynchronize();
         std::lock_guard<std::mutex> lk(g_cache_mu);
+        g_stats[1]++;
         drop_cached(dev);
         e = hipMalloc(p, *cls);
     }
@@ -99,6 +105,7 @@ void scratch_free(void *p, hipStream_t stream, size_t cls) {
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> lk(g_cache_mu);
     if (g_cached + cls > cache_cap()) {  // over the cap: hand it back (hipFree waits for the device)
+        g_stats[2]++;
         (void)hipFree(p);
         return;
     }
@@ -117,6 +124,11 @@ int scratch_trim(int dev, int64_t *freed) {
 int64_t scratch_cached() {
     std::lock_guard<std::mutex> lk(g_cache_mu);
     return (int64_t)g_cached;
+}
+
+void scratch_stats(int64_t *out) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    for (int k = 0; k < 3; k++) out[k] = g_stats[k];
 }
 }  // namespace hymet
 
@@ -245,6 +257,12 @@ int hymet_scratch_trim(hymet_ctx *ctx, int64_t *freed_bytes) {
     HY_HIP(hipSetDevice(ctx->device));
     HY_HIP(hipStreamSynchronize(ctx->stream));
     return hymet::scratch_trim(ctx->device, freed_bytes);
+}
+
+int hymet_scratch_stats(hymet_ctx *ctx, int64_t *counts) {
+    HY_ARG(ctx && counts, "hymet_scratch_stats: null argument");
+    hymet::scratch_stats(counts);
+    return HYMET_OK;
 }
 
 int hymet_scratch_cached(hymet_ctx *ctx, int64_t *bytes) {

@@ -1,10 +1,10 @@
 // Mash `screen` on MI355X (replaces scripts/mash.sh:14).
 //
 // Kernels
-//   table_insert   : distinct sketch hashes -> open-addressing uint64 table in HBM
-//                    (linear probing from a multiplicative-hash home slot), one atomicCAS per hash;
-//                    each slot also keeps the smallest DB hash index holding its key (atomicMin),
-//                    the key's canonical index.  Hit counts are kept per canonical index, in the
+//   table_insert   : distinct sketch hashes -> open-addressing table in HBM (linear probing
+//                    from a multiplicative-hash home slot), one atomicCAS per hash; a 16-byte slot
+//                    holds the key and the smallest DB hash index holding it (atomicMin on the
+//                    line the CAS just brought in), the key's canonical index.  Hit counts are kept per canonical index, in the
 //                    DB's own order: the same on every rank whatever slots the parallel insertion
 //                    gave the keys, so the ranks' counts add up as they are (one all-reduce).
 //   canon_of       : per DB hash, the canonical index of its key (duplicates across references
@@ -113,10 +113,9 @@ struct CountParams {
     int64_t n_bases, pos_begin, pos_end;
     uint32_t seed;
     int ndb;
-    const uint64_t *keys[kMaxDb];
+    const uint64_t *tab[kMaxDb];   // 16-byte slots: key, canonical index
     uint64_t mask[kMaxDb];
     int shift[kMaxDb];
-    const int32_t *canon[kMaxDb];  // slot -> canonical index of its key
     uint32_t *counts[kMaxDb];      // per canonical index, + [nhash] for the all-ones hash
     uint64_t nhash[kMaxDb];
     uint64_t cand_thr;
@@ -177,12 +176,12 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
                     atomicAdd(&P.counts[d][P.nhash[d]], 1u);
                     continue;
                 }
-                const uint64_t *keys = P.keys[d];
+                const uint64_t *tab = P.tab[d];
                 uint64_t s = home_slot(h, P.shift[d]);
                 for (;;) {
-                    const uint64_t key = keys[s];
+                    const uint64_t key = tab[2 * s];
                     if (key == h) {
-                        atomicAdd(&P.counts[d][P.canon[d][s]], 1u);
+                        atomicAdd(&P.counts[d][(uint32_t)tab[2 * s + 1]], 1u);
                         break;
                     }
                     if (key == kEmpty) break;
@@ -199,8 +198,8 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
 }
 
 __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t *__restrict__ hashes, int64_t n,
-                                                           unsigned long long *keys, uint64_t mask, int shift,
-                                                           int64_t nslots, int64_t *slot_of, int32_t *canon) {
+                                                           unsigned long long *tab, uint64_t mask, int shift,
+                                                           int64_t nslots, int64_t *slot_of) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t h = hashes[i];
@@ -210,21 +209,21 @@ __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t *__res
     }
     uint64_t s = home_slot(h, shift);
     for (;;) {
-        unsigned long long prev = atomicCAS(&keys[s], (unsigned long long)kEmpty, (unsigned long long)h);
+        unsigned long long prev = atomicCAS(&tab[2 * s], (unsigned long long)kEmpty, (unsigned long long)h);
         if (prev == kEmpty || prev == h) break;
         s = (s + 1) & mask;
     }
-    atomicMin(&canon[s], (int32_t)i);
+    atomicMin(reinterpret_cast<unsigned int *>(&tab[2 * s + 1]), (unsigned int)i);
     slot_of[i] = (int64_t)s;
 }
 
 // per DB hash: its key's canonical index (n for the all-ones hash: the extra counter)
 __global__ __launch_bounds__(256) void canon_of_kernel(const int64_t *__restrict__ slot_of, int64_t n, int64_t nslots,
-                                                       const int32_t *__restrict__ canon, int32_t *canon_of) {
+                                                       const uint64_t *__restrict__ tab, int32_t *canon_of) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t s = slot_of[i];
-    canon_of[i] = s == nslots ? (int32_t)n : canon[s];
+    canon_of[i] = s == nslots ? (int32_t)n : (int32_t)(uint32_t)tab[2 * s + 1];
 }
 
 template <typename T>
@@ -323,30 +322,30 @@ int64_t hymet_screen_table_slots(int64_t n_hashes) {
     return s;
 }
 
-int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n, uint64_t *d_keys, int64_t n_slots,
-                             int64_t *d_slot_of, int32_t *d_canon, int32_t *d_canon_of) {
-    HY_ARG(ctx && d_keys && d_slot_of && d_canon && d_canon_of, "hymet_screen_table_build: null argument");
+int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n, uint64_t *d_table, int64_t n_slots,
+                             int64_t *d_slot_of, int32_t *d_canon_of) {
+    HY_ARG(ctx && d_table && d_slot_of && d_canon_of, "hymet_screen_table_build: null argument");
     HY_ARG(n_slots >= 1024 && (n_slots & (n_slots - 1)) == 0, "hymet_screen_table_build: n_slots must be a power of two >= 1024");
     HY_ARG(n_slots >= 2 * n, "hymet_screen_table_build: n_slots must be >= 2*n_hashes");
     HY_ARG(n < (1ll << 31) - 1, "hymet_screen_table_build: more than 2^31 - 2 hashes");
     HY_HIP(hipSetDevice(ctx->device));
-    HY_HIP(hipMemsetAsync(d_keys, 0xFF, (size_t)n_slots * 8, ctx->stream));
-    HY_HIP(hipMemsetAsync(d_canon, 0x7F, (size_t)n_slots * 4, ctx->stream));  // INT32_MAX-ish: above any index
+    // empty key ~0 and canonical index 0xFFFFFFFF (above any index: the unsigned atomicMin)
+    HY_HIP(hipMemsetAsync(d_table, 0xFF, (size_t)n_slots * 16, ctx->stream));
     if (n <= 0) return HYMET_OK;
     const int lg = log2_exact(n_slots);
     hymet::ProfScope _ps(ctx, "screen_table_build");
     hipLaunchKernelGGL(table_insert_kernel, dim3((unsigned)hymet::cdiv(n, 256)), dim3(256), 0, ctx->stream, d_hashes, n,
-                       (unsigned long long *)d_keys, (uint64_t)(n_slots - 1), 64 - lg, n_slots, d_slot_of, d_canon);
+                       (unsigned long long *)d_table, (uint64_t)(n_slots - 1), 64 - lg, n_slots, d_slot_of);
     HY_CHECK_LAUNCH("table_insert_kernel");
     hipLaunchKernelGGL(canon_of_kernel, dim3((unsigned)hymet::cdiv(n, 256)), dim3(256), 0, ctx->stream,
-                       (const int64_t *)d_slot_of, n, n_slots, (const int32_t *)d_canon, d_canon_of);
+                       (const int64_t *)d_slot_of, n, n_slots, (const uint64_t *)d_table, d_canon_of);
     HY_CHECK_LAUNCH("canon_of_kernel");
     return HYMET_OK;
 }
 
 int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask, int64_t n_bases, int64_t pos_begin,
-                       int64_t pos_end, int k, uint32_t seed, int ndb, const uint64_t *const *h_d_keys,
-                       const int64_t *h_n_slots, const int32_t *const *h_d_canon, const int64_t *h_n_hashes,
+                       int64_t pos_end, int k, uint32_t seed, int ndb, const uint64_t *const *h_d_tables,
+                       const int64_t *h_n_slots, const int64_t *h_n_hashes,
                        uint32_t *const *h_d_counts, uint64_t cand_thr, uint64_t *d_cand,
                        int64_t cand_cap, unsigned long long *d_cand_n, unsigned long long *d_nkmers) {
     HY_ARG(ctx && d_2b && d_mask && d_cand_n && d_nkmers, "hymet_screen_count: null argument");
@@ -367,11 +366,10 @@ int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_m
     for (int d = 0; d < ndb; d++) {
         const int64_t ns = h_n_slots[d];
         HY_ARG(ns >= 1024 && (ns & (ns - 1)) == 0, "hymet_screen_count: table size must be a power of two");
-        HY_ARG(h_d_keys[d] && h_d_canon[d] && h_d_counts[d] && h_n_hashes[d] >= 0, "hymet_screen_count: null table");
-        P.keys[d] = h_d_keys[d];
+        HY_ARG(h_d_tables[d] && h_d_counts[d] && h_n_hashes[d] >= 0, "hymet_screen_count: null table");
+        P.tab[d] = h_d_tables[d];
         P.mask[d] = (uint64_t)(ns - 1);
         P.shift[d] = 64 - log2_exact(ns);
-        P.canon[d] = h_d_canon[d];
         P.counts[d] = h_d_counts[d];
         P.nhash[d] = (uint64_t)h_n_hashes[d];
     }

@@ -380,7 +380,7 @@ class Pipeline:
 
         def classifier():
             try:
-                self._load_classifier()
+                self._load_classifier(side)
             except BaseException as e:  # noqa: BLE001 -- re-raised below
                 err.append(e)
         th = threading.Thread(target=classifier, name="hymet-taxonomy")
@@ -414,7 +414,7 @@ class Pipeline:
         self.timings["msh_allgather_s"] = time.perf_counter() - t0
         self._build_tables(side)
 
-    def _load_classifier(self):
+    def _load_classifier(self, side=None):
         """C1-C2: detailed_taxonomy.tsv and taxonomy_hierarchy.tsv.  classification_cami.py
         runs as `... || true` (run_hymet_cami.sh:175-180): a classifier that cannot load its
         inputs leaves an empty TSV, and the fallback runs."""
@@ -424,6 +424,17 @@ class Pipeline:
             self.classifier_error = None
         except Exception as e:  # noqa: BLE001 -- any failure of the reference script
             self.classifier, self.classifier_error = None, e
+        if self.classifier is not None and side is not None:
+            # the taxonomy's HBM tables (labels, name ids, hierarchy flags) on this loader
+            # thread, on the idle mapping stream, rather than in the run's classification
+            # step.  No stream of its own: a process's streams share a few hardware queues
+            # (GPU_MAX_HW_QUEUES, 4), and one more stream shifted the round-robin so that the
+            # two mapping streams landed on one queue and ran one after the other (C4 step
+            # 1,298 -> 1,388 ms)
+            torch = self.gpu.torch
+            with torch.cuda.stream(side.stream):
+                self.classifier.device_tables(None)
+            side.stream.synchronize()
         self.timings["classifier_load_s"] = time.perf_counter() - t0
 
     def load_inputs(self):

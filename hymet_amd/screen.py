@@ -39,8 +39,7 @@ class ScreenTable:
         n = int(len(db.hashes))
         self.n_hashes = n
         self.n_slots = int(gpu.lib.hymet_screen_table_slots(n))
-        self.keys = gpu.empty(self.n_slots, torch.int64)
-        self.canon = gpu.empty(self.n_slots, torch.int32)
+        self.table = gpu.empty(2 * self.n_slots, torch.int64)   # 16-byte slots: key, canonical index
         self.canon_of = gpu.empty(max(n, 1), torch.int32)
         slot_of = gpu.empty(max(n, 1), torch.int64)      # build scratch
         dev = getattr(db, "dev_hashes", None)
@@ -53,8 +52,7 @@ class ScreenTable:
             d_h = pinned[:n].to(gpu.dev, non_blocking=True)
         else:
             d_h = torch.from_numpy(np.ascontiguousarray(db.hashes).view(np.int64)).to(gpu.dev)
-        gpu.call("hymet_screen_table_build", ptr(d_h), n, ptr(self.keys), self.n_slots, ptr(slot_of), ptr(self.canon),
-                 ptr(self.canon_of))
+        gpu.call("hymet_screen_table_build", ptr(d_h), n, ptr(self.table), self.n_slots, ptr(slot_of), ptr(self.canon_of))
         self.ref_off = torch.from_numpy(np.ascontiguousarray(db.offsets, dtype=np.int64)).to(gpu.dev)
         del d_h, slot_of
 
@@ -93,13 +91,12 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
     frac = 16.0 * s / span
     top = hash_top(k)              # hashes are 64-bit for k > 16, 32-bit (x86_32) for k <= 16
     thr = U64_MAX if frac >= 1.0 else int(frac * float(top))
-    keys_arr = (ctypes.c_void_p * 4)(*[ptr(t.keys).value for t in tables])
+    keys_arr = (ctypes.c_void_p * 4)(*[ptr(t.table).value for t in tables])
     slots_arr = (ctypes.c_int64 * 4)(*[t.n_slots for t in tables])
-    canon_arr = (ctypes.c_void_p * 4)(*[ptr(t.canon).value for t in tables])
     nh_arr = (ctypes.c_int64 * 4)(*[t.n_hashes for t in tables])
     cnt_arr = (ctypes.c_void_p * 4)(*[ptr(c).value for c in counts])
     gpu.call("hymet_screen_count", ptr(pool.w2b), ptr(pool.wmask), n_bases, pos_begin, pos_end, k, seed,
-             len(tables), keys_arr, slots_arr, canon_arr, nh_arr, cnt_arr, thr, ptr(cand), cap, ptr(cand_n), ptr(nk))
+             len(tables), keys_arr, slots_arr, nh_arr, cnt_arr, thr, ptr(cand), cap, ptr(cand_n), ptr(nk))
     n_kmers = int(nk.item())
     dummy = gpu.zeros(1, torch.int64)
 
@@ -107,7 +104,7 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
         buf = gpu.empty(cap_, torch.int64)
         cand_n.zero_()
         gpu.call("hymet_screen_count", ptr(pool.w2b), ptr(pool.wmask), n_bases, pos_begin, pos_end, k, seed,
-                 0, keys_arr, slots_arr, canon_arr, nh_arr, cnt_arr, thr_, ptr(buf), cap_, ptr(cand_n), ptr(dummy))
+                 0, keys_arr, slots_arr, nh_arr, cnt_arr, thr_, ptr(buf), cap_, ptr(cand_n), ptr(dummy))
         return buf
 
     while True:

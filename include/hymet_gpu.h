@@ -60,6 +60,9 @@ int hymet_prof_names(hymet_ctx *ctx, char *buf, int64_t cap);
  * allocates large tensors); cached reports the bytes held. */
 int hymet_scratch_trim(hymet_ctx *ctx, int64_t *freed_bytes);
 int hymet_scratch_cached(hymet_ctx *ctx, int64_t *bytes);
+/* counts[0..2]: the allocator's hipMalloc calls (cache misses), out-of-memory retries (each
+ * synchronises the device and drops the cache) and frees past the cap (hipFree), since load. */
+int hymet_scratch_stats(hymet_ctx *ctx, int64_t *counts);
 /* n bytes of device memory (written by this context's stream) into pageable host memory,
  * through two pinned 64 MiB staging chunks (PCIe and `threads` host copy threads overlap).
  * Synchronous.
@@ -110,15 +113,14 @@ int hymet_name_hash(hymet_ctx *ctx, const uint8_t *d_raw, const int64_t *d_name_
  * sketch hashes of a DB, counts of every pooled canonical k-mer hash that hits it, and the
  * per-reference shared / median-depth statistics. */
 int64_t hymet_screen_table_slots(int64_t n_hashes);
-/* d_keys: n_slots uint64; d_slot_of: n_hashes int64 (slot of each input hash, n_slots for
- * the reserved all-ones key); d_canon: n_slots int32, the smallest input index holding each
- * slot's key (its canonical index); d_canon_of: n_hashes int32, each input hash's canonical
- * index (n_hashes for the all-ones key).  Hits are counted per canonical index, so counts are
- * in the DB's own order on every rank whatever slots parallel insertion chose, and the
- * ranks' partial counts add up as they are.  Resets d_keys and d_canon. */
+/* d_table: n_slots 16-byte slots (2 * n_slots uint64: key, then the smallest input index
+ * holding it -- its canonical index -- in the low 32 bits); d_slot_of: n_hashes int64 (slot of
+ * each input hash, n_slots for the reserved all-ones key); d_canon_of: n_hashes int32, each
+ * input hash's canonical index (n_hashes for the all-ones key).  Hits are counted per canonical
+ * index, so counts are in the DB's own order on every rank whatever slots parallel insertion
+ * chose, and the ranks' partial counts add up as they are.  Resets d_table. */
 int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n_hashes,
-                             uint64_t *d_keys, int64_t n_slots, int64_t *d_slot_of, int32_t *d_canon,
-                             int32_t *d_canon_of);
+                             uint64_t *d_table, int64_t n_slots, int64_t *d_slot_of, int32_t *d_canon_of);
 /* The library's stable LSD radix sort (8-bit digits) of device (key, value) pairs by key bits
  * [begin_bit, end_bit), in place (the sort behind the mapper's minimizer, group, chain and
  * anchor-segment orders and the LCA row order; no rocPRIM on the mapping path). */
@@ -169,15 +171,15 @@ int hymet_msh_upload_range(hymet_ctx *ctx, const hymet_msh *m, int threads, uint
 void hymet_msh_close(hymet_msh *m);
 /* Hash every valid canonical k-mer of the packed pool (k in 1..32: MurmurHash3_x64_128
  * word 0 with `seed` for k > 16, MurmurHash3_x86_32 widened to 64 bits for k <= 16, as
- * Mash's 64- / 32-bit sketches), probe ndb (<= 4) tables, count hits into d_counts[i] at the
- * hit key's canonical index (h_d_canon[i]; n_hashes[i]+1 uint32 each, caller-zeroed, the last
- * for the all-ones hash), and append every hash < cand_thr to d_cand (bottom-s
+ * Mash's 64- / 32-bit sketches), probe ndb (<= 4) tables (hymet_screen_table_build's), count
+ * hits into d_counts[i] at the hit key's canonical index (n_hashes[i]+1 uint32 each,
+ * caller-zeroed, the last for the all-ones hash), and append every hash < cand_thr to d_cand (bottom-s
  * candidates; d_cand_n counts appends, may exceed cand_cap).  d_nkmers += valid k-mers.
  * seq_begin/seq_end limit the k-mer START positions processed (for sharding). */
 int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask,
                        int64_t n_bases, int64_t pos_begin, int64_t pos_end, int k, uint32_t seed,
-                       int ndb, const uint64_t *const *h_d_keys, const int64_t *h_n_slots,
-                       const int32_t *const *h_d_canon, const int64_t *h_n_hashes,
+                       int ndb, const uint64_t *const *h_d_tables, const int64_t *h_n_slots,
+                       const int64_t *h_n_hashes,
                        uint32_t *const *h_d_counts, uint64_t cand_thr, uint64_t *d_cand,
                        int64_t cand_cap, unsigned long long *d_cand_n,
                        unsigned long long *d_nkmers);
