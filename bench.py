@@ -29,6 +29,13 @@ import time
 
 import numpy as np
 
+# HIP multiplexes a process's streams over GPU_MAX_HW_QUEUES hardware queues (4 by default),
+# assigned as streams are created; two mapping streams that land on one queue run one after
+# the other (profiles/r05_streams/: +90 ms per C4 step).  A rank of a multi-GPU job also
+# holds the RCCL communicators' streams, so give the process enough queues for every stream
+# it creates (before the HIP runtime starts; at N = 1 it measured the same as 4).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 

@@ -23,6 +23,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <memory>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -451,13 +453,36 @@ int hymet_msh_upload_range(hymet_ctx *ctx, const hymet_msh *m, int threads, uint
     threads = std::max(1, std::min(threads, 64));
     n_chunks = std::max(1, std::min(n_chunks, 64));
     const int64_t span = hi_h - lo_h;
+    if (span < (1 << 20)) threads = 1;
+    // equal hash counts per chunk.  One set of threads walks the chunks in order, each taking
+    // its share of every chunk; the caller queues a chunk's DMA as soon as every thread is
+    // past it (threads spawned once: per-chunk spawns cost more than a small slice's copy)
+    std::unique_ptr<std::atomic<int>[]> done(new std::atomic<int>[(size_t)n_chunks]);
+    for (int c = 0; c < n_chunks; c++) done[(size_t)c].store(0);
+    auto chunk = [&](int c, int64_t *lo, int64_t *hi) {
+        *lo = lo_h + span * c / n_chunks;
+        *hi = lo_h + span * (c + 1) / n_chunks;
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++)
+        th.emplace_back([&, t] {
+            for (int c = 0; c < n_chunks; c++) {
+                int64_t lo, hi;
+                chunk(c, &lo, &hi);
+                gather_hashes(m, off, lo + (hi - lo) * t / threads, lo + (hi - lo) * (t + 1) / threads, 1, pinned);
+                done[(size_t)c].fetch_add(1, std::memory_order_release);
+            }
+        });
+    hipError_t err = hipSuccess;
     for (int c = 0; c < n_chunks; c++) {
-        // equal hash counts per chunk; each chunk's DMA is queued as soon as it is gathered
-        const int64_t lo = lo_h + span * c / n_chunks, hi = lo_h + span * (c + 1) / n_chunks;
-        if (hi <= lo) continue;
-        gather_hashes(m, off, lo, hi, threads, pinned);
-        HY_HIP(hipMemcpyAsync(d_hashes + lo, pinned + lo, 8 * (size_t)(hi - lo), hipMemcpyHostToDevice, ctx->stream));
+        while (done[(size_t)c].load(std::memory_order_acquire) < threads) std::this_thread::yield();
+        int64_t lo, hi;
+        chunk(c, &lo, &hi);
+        if (hi > lo && err == hipSuccess)
+            err = hipMemcpyAsync(d_hashes + lo, pinned + lo, 8 * (size_t)(hi - lo), hipMemcpyHostToDevice, ctx->stream);
     }
+    for (auto &x : th) x.join();
+    HY_HIP(err);
     return HYMET_OK;
 }
 

@@ -3,12 +3,12 @@
 // Kernels
 //   table_insert   : distinct sketch hashes -> open-addressing table in HBM (linear probing
 //                    from a multiplicative-hash home slot), one atomicCAS per hash; a 16-byte slot
-//                    holds the key and the smallest DB hash index holding it (atomicMin on the
-//                    line the CAS just brought in), the key's canonical index.  Hit counts are kept per canonical index, in the
+//                    holds the key and the smallest DB hash index holding it, the key's canonical
+//                    index (the claiming thread's own; keys shared by references fixed up after).  Hit counts are kept per canonical index, in the
 //                    DB's own order: the same on every rank whatever slots the parallel insertion
 //                    gave the keys, so the ranks' counts add up as they are (one all-reduce).
 //   canon_of       : per DB hash, the canonical index of its key (duplicates across references
-//                    share one counter).
+//                    share one counter): written by the insert, fixed up for duplicates.
 //   screen_count<K>: one thread = one 64-position tile of the pooled, packed query bases.
 //                    Rolling 2-bit forward / reverse-complement words decide the canonical
 //                    strand by integer compare (== Mash's memcmp on ASCII, since A<C<G<T);
@@ -197,12 +197,21 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(P.nkmers, v);
 }
 
+// insert: the thread whose CAS claims an empty slot owns it and writes the slot's second word
+// (canonical index and owner, both its own index) with a plain store on the line the CAS just
+// brought in, and canon_of[i] = i; a thread finding its key already there (a hash shared by
+// references) is marked in slot_of (kDup) and fixed up by the two passes below.  Keys appear
+// once in most DBs, so the common insert costs one CAS and two plain stores (an atomicMin per
+// insert for the canonical index cost 5 ms of 13 on 1e8 hashes, and a gather pass 2.5 ms).
+constexpr int64_t kDup = 1ll << 62;
+
 __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t *__restrict__ hashes, int64_t n,
                                                            unsigned long long *tab, uint64_t mask, int shift,
-                                                           int64_t nslots, int64_t *slot_of) {
+                                                           int64_t nslots, int64_t *slot_of, int32_t *canon_of) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t h = hashes[i];
+    canon_of[i] = h == kEmpty ? (int32_t)n : (int32_t)i;
     if (h == kEmpty) {
         slot_of[i] = nslots;
         return;
@@ -210,20 +219,40 @@ __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t *__res
     uint64_t s = home_slot(h, shift);
     for (;;) {
         unsigned long long prev = atomicCAS(&tab[2 * s], (unsigned long long)kEmpty, (unsigned long long)h);
-        if (prev == kEmpty || prev == h) break;
+        if (prev == kEmpty) {  // owner
+            tab[2 * s + 1] = (unsigned long long)(uint32_t)i | (unsigned long long)(uint32_t)i << 32;
+            slot_of[i] = (int64_t)s;
+            return;
+        }
+        if (prev == h) {  // a duplicate of an owned key
+            slot_of[i] = (int64_t)s | kDup;
+            return;
+        }
         s = (s + 1) & mask;
     }
-    atomicMin(reinterpret_cast<unsigned int *>(&tab[2 * s + 1]), (unsigned int)i);
-    slot_of[i] = (int64_t)s;
 }
 
-// per DB hash: its key's canonical index (n for the all-ones hash: the extra counter)
-__global__ __launch_bounds__(256) void canon_of_kernel(const int64_t *__restrict__ slot_of, int64_t n, int64_t nslots,
-                                                       const uint64_t *__restrict__ tab, int32_t *canon_of) {
+// duplicates, pass 1 (after every owner's store): the slot's canonical index = the smallest
+// index holding its key
+__global__ __launch_bounds__(256) void dup_min_kernel(const int64_t *__restrict__ slot_of, int64_t n,
+                                                      unsigned long long *tab) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int64_t s = slot_of[i];
-    canon_of[i] = s == nslots ? (int32_t)n : (int32_t)(uint32_t)tab[2 * s + 1];
+    const int64_t v = slot_of[i];
+    if (v & kDup) atomicMin(reinterpret_cast<unsigned int *>(&tab[2 * (v & ~kDup) + 1]), (unsigned int)i);
+}
+
+// duplicates, pass 2: each duplicate and its slot's owner take the final canonical index
+__global__ __launch_bounds__(256) void dup_fix_kernel(const int64_t *__restrict__ slot_of, int64_t n,
+                                                      const unsigned long long *tab, int32_t *canon_of) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t v = slot_of[i];
+    if (!(v & kDup)) return;
+    const unsigned long long w = tab[2 * (v & ~kDup) + 1];
+    const int32_t c = (int32_t)(uint32_t)w;
+    canon_of[i] = c;
+    canon_of[(uint32_t)(w >> 32)] = c;  // the owner (every duplicate of the slot writes the same value)
 }
 
 template <typename T>
@@ -334,12 +363,16 @@ int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n
     if (n <= 0) return HYMET_OK;
     const int lg = log2_exact(n_slots);
     hymet::ProfScope _ps(ctx, "screen_table_build");
-    hipLaunchKernelGGL(table_insert_kernel, dim3((unsigned)hymet::cdiv(n, 256)), dim3(256), 0, ctx->stream, d_hashes, n,
-                       (unsigned long long *)d_table, (uint64_t)(n_slots - 1), 64 - lg, n_slots, d_slot_of);
+    const dim3 grid((unsigned)hymet::cdiv(n, 256));
+    hipLaunchKernelGGL(table_insert_kernel, grid, dim3(256), 0, ctx->stream, d_hashes, n, (unsigned long long *)d_table,
+                       (uint64_t)(n_slots - 1), 64 - lg, n_slots, d_slot_of, d_canon_of);
     HY_CHECK_LAUNCH("table_insert_kernel");
-    hipLaunchKernelGGL(canon_of_kernel, dim3((unsigned)hymet::cdiv(n, 256)), dim3(256), 0, ctx->stream,
-                       (const int64_t *)d_slot_of, n, n_slots, (const uint64_t *)d_table, d_canon_of);
-    HY_CHECK_LAUNCH("canon_of_kernel");
+    hipLaunchKernelGGL(dup_min_kernel, grid, dim3(256), 0, ctx->stream, (const int64_t *)d_slot_of, n,
+                       (unsigned long long *)d_table);
+    HY_CHECK_LAUNCH("dup_min_kernel");
+    hipLaunchKernelGGL(dup_fix_kernel, grid, dim3(256), 0, ctx->stream, (const int64_t *)d_slot_of, n,
+                       (const unsigned long long *)d_table, d_canon_of);
+    HY_CHECK_LAUNCH("dup_fix_kernel");
     return HYMET_OK;
 }
 

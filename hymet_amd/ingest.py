@@ -205,9 +205,10 @@ class QueryShard:
 
     @classmethod
     def from_fasta(cls, gpu, fx: FastaIndex, r0: int = 0, r1: Optional[int] = None, batch_bases: int = 40_000_000,
-                   d_all=None, q_base: Optional[int] = None):
+                   d_all=None, q_base: Optional[int] = None, d_base: int = 0):
         """One H2D copy of the records' contiguous byte range, then device-side compaction.
-        d_all: the whole input already in HBM (uploaded while the records were scanned).
+        d_all: the input's bytes from file offset d_base on, already in HBM (uploaded while the
+        records were scanned: the whole file, or a rank's byte range).
         q_base: index of record r0 in the whole input (default r0: fx indexes the whole file)."""
         torch = gpu.torch
         r1 = fx.n if r1 is None else r1
@@ -220,7 +221,9 @@ class QueryShard:
         lo = int(min(fx.name_off[r0], fx.seq_off[r0]))
         hi = int(fx.seq_end[r1 - 1])
         if d_all is not None:
-            d_raw, lo = d_all, 0
+            if lo < d_base or hi - d_base > d_all.numel():
+                raise ValueError("from_fasta: the records lie outside the uploaded bytes")
+            d_raw, lo = d_all, d_base
         else:
             # one upload through the library's double-buffered pinned staging (a pageable copy
             # staged the gigabyte on one thread)

@@ -218,7 +218,21 @@ class _Struct:
         return [_Struct(self.m, s, t + 1 + j * step, dw, npt) for j in range(cnt)]
 
 
-def read_msh(path, threads: int = 16, alloc=None, upload=None, shard=None) -> SketchDB:
+class _PendingStrings(Sequence):
+    """A DB's names / comments before read_msh(defer_meta=True)'s finish_meta() ran: the
+    right length, no contents."""
+
+    def __init__(self, n: int):
+        self._n = n
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        raise RuntimeError("sketch DB names read before SketchDB.finish_meta()")
+
+
+def read_msh(path, threads: int = 16, alloc=None, upload=None, shard=None, defer_meta: bool = False) -> SketchDB:
     """.msh -> SketchDB through the library's native reader (hymet_msh_*: mmap, pointer walk
     and a threaded hash gather; S1 of SURVEY.md §8a, on the timed path since `mash screen`
     reads its DB on every call).  alloc(n) may supply the uint64 array the hashes are
@@ -230,17 +244,23 @@ def read_msh(path, threads: int = 16, alloc=None, upload=None, shard=None) -> Sk
     hashes, [rank * c, (rank + 1) * c), is gathered and uploaded (hymet_msh_upload_range) into
     a device tensor of world * c entries, for Comm.allgather_slices_ to fill in the others;
     db.dev_slice = (lo, hi, c), and db.hashes holds valid hashes only on [lo, hi).
+    defer_meta (with upload): the file stays open and the names / comments are copied only by
+    db.finish_meta() -- the caller runs it while the GPU builds the table; until then they
+    are placeholders of the right length.
     The library is required, like every product path."""
     import ctypes
+    import time
     from ._lib import check, load
     if shard is not None and upload is None:
         raise ValueError("read_msh: shard needs upload (the slices meet in HBM)")
+    if defer_meta and upload is None:
+        raise ValueError("read_msh: defer_meta needs upload")
     lib = load()
     h = ctypes.c_void_p()
-    import time
     t0 = time.perf_counter()
     check(lib.hymet_msh_open(str(path).encode(), ctypes.byref(h)), "hymet_msh_open")
     t1 = t2 = time.perf_counter()
+    keep_open = False
     try:
         raw = (ctypes.c_int64 * 9)()   # hymet_msh_info: 7 int32 (+4 pad) then 5 int64
         check(lib.hymet_msh_info_get(h, ctypes.byref(raw)), "hymet_msh_info_get")
@@ -275,20 +295,25 @@ def read_msh(path, threads: int = 16, alloc=None, upload=None, shard=None) -> Sk
                                              ctypes.c_void_p(dev.data_ptr()), 8, lo, hi), "hymet_msh_upload_range")
             t2 = time.perf_counter()
             check(lib.hymet_msh_copy(h, int(threads), None, offsets.ctypes.data_as(ctypes.c_void_p),
-                                     lengths.ctypes.data_as(ctypes.c_void_p), names, comments, alpha), "hymet_msh_copy")
+                                     lengths.ctypes.data_as(ctypes.c_void_p), None if defer_meta else names,
+                                     None if defer_meta else comments, alpha), "hymet_msh_copy")
         else:
             check(lib.hymet_msh_copy(h, int(threads), hashes.ctypes.data_as(ctypes.c_void_p),
                                      offsets.ctypes.data_as(ctypes.c_void_p), lengths.ctypes.data_as(ctypes.c_void_p),
                                      names, comments, alpha), "hymet_msh_copy")
+        keep_open = defer_meta
     finally:
-        lib.hymet_msh_close(h)
+        if not keep_open:
+            lib.hymet_msh_close(h)
     t3 = time.perf_counter()
 
     def split(buf, n, st):
         return NulStrings(buf, n, st) if n else []
 
     db = SketchDB(k=k, seed=seed, sketch_size=ss, alphabet=alpha.raw[:al].decode() or "ACGT", preserve_case=bool(pc),
-                  noncanonical=bool(nonc), window_size=win, names=split(names_a, n_refs, name_st), comments=split(comments_a, n_refs, comment_st),
+                  noncanonical=bool(nonc), window_size=win,
+                  names=_PendingStrings(n_refs) if defer_meta else split(names_a, n_refs, name_st),
+                  comments=_PendingStrings(n_refs) if defer_meta else split(comments_a, n_refs, comment_st),
                   lengths=lengths[:n_refs].copy(), offsets=offsets, hashes=hashes[:n_hashes])
     db.dev_hashes = dev
     db.dev_slice = (lo, hi, c) if shard is not None else None
@@ -298,6 +323,19 @@ def read_msh(path, threads: int = 16, alloc=None, upload=None, shard=None) -> Sk
         db.load_s = {"open": t1 - t0, "hashes": t2 - t1, "meta": t3 - t2, "wrap": time.perf_counter() - t3}
     else:
         db.load_s = {"open": t1 - t0, "hashes": t3 - t1, "meta": 0.0, "wrap": time.perf_counter() - t3}
+    db.finish_meta = None
+    if defer_meta:
+        def finish_meta():
+            tm = time.perf_counter()
+            try:
+                check(lib.hymet_msh_copy(h, int(threads), None, None, None, names, comments, None), "hymet_msh_copy")
+            finally:
+                lib.hymet_msh_close(h)
+                db.finish_meta = None
+            db.names = split(names_a, n_refs, name_st)
+            db.comments = split(comments_a, n_refs, comment_st)
+            db.load_s["meta"] += time.perf_counter() - tm
+        db.finish_meta = finish_meta
     return db
 
 

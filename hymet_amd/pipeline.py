@@ -350,7 +350,7 @@ class Pipeline:
             else:
                 with self.gpu.torch.cuda.stream(side.stream):
                     dbs.append(read_msh(p, alloc=pin, upload=(side, lambda n: side.empty(n, side.torch.int64)),
-                                        shard=shard))
+                                        shard=shard, defer_meta=True))
         self.dbs = dbs
         self.timings["msh_read_s"] = time.perf_counter() - t0
         for k in ("open", "meta", "hashes"):    # read_msh's own phases, summed over the DBs
@@ -362,14 +362,22 @@ class Pipeline:
         overlapping the ingest; that thread waits for side's stream before run() joins it)."""
         t1 = time.perf_counter()
         if side is None:
+            self._finish_meta()
             self.tables = [scr.ScreenTable(self.gpu, db, pinned=self._pin[i]) for i, db in enumerate(self.dbs)]
             self.gpu.sync()
         else:
             with self.gpu.torch.cuda.stream(side.stream):
                 self.tables = [scr.ScreenTable(side, db, pinned=self._pin[i]) for i, db in enumerate(self.dbs)]
             self.timings["screen_table_enqueue_s"] = time.perf_counter() - t1
+            self._finish_meta()        # the DBs' names copied while the GPU inserts the hashes
             side.stream.synchronize()
         self.timings["screen_table_s"] = time.perf_counter() - t1
+
+    def _finish_meta(self):
+        """Names / comments of DBs read with defer_meta (closes their files)."""
+        for db in self.dbs:
+            if getattr(db, "finish_meta", None) is not None:
+                db.finish_meta()
 
     def _read_inputs(self, side=None):
         """The run's input loads for a second host thread: .msh parse (+ the HBM tables on
@@ -393,6 +401,7 @@ class Pipeline:
                 elif side is not None:
                     self._build_tables(side)
         finally:
+            self._finish_meta()        # (a no-op unless an error cut the build short)
             th.join()
         if err:
             raise err[0]
@@ -464,34 +473,16 @@ class Pipeline:
                 # this rank scans, uploads and maps only its byte range of the FASTA; the ranks'
                 # record counts give its first query's index in the whole input
                 b0, b1 = shard_bytes(data, self.rank, self.world)
-                fx = FastaIndex(data, byte_range=(b0, b1))
+                d_rng, fx = self._upload_while(data, b0, b1, lambda: FastaIndex(data, byte_range=(b0, b1)))
                 counts = self.comm.allgather_np(np.array([fx.n], np.int64), tag="shard_records")
                 q_base = int(sum(int(c[0]) for c in counts[:self.rank]))
-                sh = QueryShard.from_fasta(self.gpu, fx, 0, fx.n, self.cfg.map_batch_bases, q_base=q_base)
+                sh = QueryShard.from_fasta(self.gpu, fx, 0, fx.n, self.cfg.map_batch_bases, q_base=q_base,
+                                           d_all=d_rng, d_base=b0)
                 sh.fasta, sh.fasta_r0 = fx, 0
                 return sh
             if len(data):
-                # one rank takes every record: the bytes go up on a second thread while the
-                # record table is scanned (the staged copy and the scan both read host memory)
-                import threading
-                torch = self.gpu.torch
-                d_all = self.gpu.empty(len(data), torch.uint8)
-                up_err = []
-
-                def upload():
-                    try:
-                        check(self.gpu.lib.hymet_copy_to_device(self.gpu.ctx, ptr(d_all), data, len(data), 16),
-                              "hymet_copy_to_device")
-                    except BaseException as e:  # noqa: BLE001 -- re-raised below
-                        up_err.append(e)
-                up = threading.Thread(target=upload, name="hymet-upload")
-                up.start()
-                try:
-                    queries = FastaIndex(data)
-                finally:
-                    up.join()
-                if up_err:
-                    raise up_err[0]
+                # one rank takes every record: the bytes go up while the record table is scanned
+                d_all, queries = self._upload_while(data, 0, len(data), lambda: FastaIndex(data))
             else:
                 queries = FastaIndex(data)
         if isinstance(queries, FastaIndex):
@@ -507,6 +498,33 @@ class Pipeline:
         raise TypeError(f"unsupported query input {type(queries)!r}")
 
     prepare = ingest
+
+    def _upload_while(self, data: bytes, b0: int, b1: int, scan):
+        """Bytes [b0, b1) of data uploaded to HBM on a second thread (the library's staged,
+        threaded copy) while scan() runs on this one (the record scan: both read host memory,
+        neither holds the GIL).  Returns (device bytes, scan())."""
+        import threading
+        torch = self.gpu.torch
+        d = self.gpu.empty(max(b1 - b0, 1), torch.uint8)
+        up_err = []
+
+        def upload():
+            try:
+                if b1 > b0:
+                    src = ctypes.cast(ctypes.c_char_p(data), ctypes.c_void_p).value + b0
+                    check(self.gpu.lib.hymet_copy_to_device(self.gpu.ctx, ptr(d), ctypes.c_void_p(src), b1 - b0, 16),
+                          "hymet_copy_to_device")
+            except BaseException as e:  # noqa: BLE001 -- re-raised below
+                up_err.append(e)
+        up = threading.Thread(target=upload, name="hymet-upload")
+        up.start()
+        try:
+            out = scan()
+        finally:
+            up.join()
+        if up_err:
+            raise up_err[0]
+        return d, out
 
     def screen_select(self, pool):
         t0 = time.perf_counter()

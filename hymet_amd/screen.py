@@ -52,8 +52,10 @@ class ScreenTable:
             d_h = pinned[:n].to(gpu.dev, non_blocking=True)
         else:
             d_h = torch.from_numpy(np.ascontiguousarray(db.hashes).view(np.int64)).to(gpu.dev)
-        gpu.call("hymet_screen_table_build", ptr(d_h), n, ptr(self.table), self.n_slots, ptr(slot_of), ptr(self.canon_of))
+        # the offsets first: a pageable upload waits for the stream's earlier work, and queued
+        # behind the insert it would hold the host for the whole build
         self.ref_off = torch.from_numpy(np.ascontiguousarray(db.offsets, dtype=np.int64)).to(gpu.dev)
+        gpu.call("hymet_screen_table_build", ptr(d_h), n, ptr(self.table), self.n_slots, ptr(slot_of), ptr(self.canon_of))
         del d_h, slot_of
 
 

@@ -137,3 +137,35 @@ def test_gpu_hash_kat_x86_32(gpu):
     pool = DevicePool(gpu, from_records([(f"q{i}", "", v["s"].encode()) for i, v in enumerate(vecs)]), DevicePool.ALPHA_MASH)
     r = scr.screen(gpu, pool, [db])[0]
     assert (r.shared == 1).all()
+
+
+@pytest.mark.parametrize("dup_frac", [0.0, 0.3, 0.9])
+def test_table_canonical_index_is_the_first_holder(gpu, dup_frac):
+    """hymet_screen_table_build: every DB hash's canonical index is the smallest index holding
+    its key (hashes shared by references, the insert's duplicate fix-up), the all-ones key maps
+    to the extra counter n, and each slot's second word carries its key's canonical index."""
+    from hymet_amd import screen as scr
+    from hymet_amd.msh import SketchDB
+    rng = np.random.default_rng(int(dup_frac * 10) + 3)
+    n = 400_000
+    pool = rng.integers(0, 2**63, size=max(1, int(n * (1 - dup_frac))), dtype=np.int64).astype(np.uint64)
+    h = np.concatenate([pool, rng.choice(pool, n - len(pool))]) if dup_frac else pool[:n]
+    h = h[rng.permutation(len(h))]
+    h[rng.choice(len(h), 3, replace=False)] = np.uint64(2**64 - 1)     # the reserved all-ones key
+    per = 100
+    db = SketchDB(names=[""] * (len(h) // per), comments=[""] * (len(h) // per), lengths=np.ones(len(h) // per, np.int64),
+                  offsets=np.arange(len(h) // per + 1, dtype=np.int64) * per, hashes=h)
+    t = scr.ScreenTable(gpu, db)
+    gpu.sync()
+    got = t.canon_of[:len(h)].cpu().numpy()
+    _, first = np.unique(h, return_index=True)
+    inv = np.unique(h, return_inverse=True)[1]
+    want = first[inv].astype(np.int64)
+    want[h == np.uint64(2**64 - 1)] = len(h)
+    np.testing.assert_array_equal(got, want)
+    tab = t.table.cpu().numpy().view(np.uint64).reshape(-1, 2)
+    used = tab[:, 0] != np.uint64(2**64 - 1)
+    keys, canon = tab[used, 0], (tab[used, 1] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    assert len(keys) == len(np.unique(h[h != np.uint64(2**64 - 1)]))
+    pos = np.searchsorted(np.unique(h), keys)
+    np.testing.assert_array_equal(canon, first[pos])

@@ -1,13 +1,16 @@
 """Screen-table build in isolation (run under rocprofv3 --kernel-trace --stats): 1e8 random
 hashes in 1e5 sorted lists, built 5 times; prints the host-timed build."""
+import os
+import sys
 import time
 
 import numpy as np
 import torch
 
-from hymet_amd._lib import Gpu
-from hymet_amd import screen as scr
-from hymet_amd.msh import SketchDB
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from hymet_amd._lib import Gpu  # noqa: E402
+from hymet_amd import screen as scr  # noqa: E402
+from hymet_amd.msh import SketchDB  # noqa: E402
 
 gpu = Gpu(0)
 n_ref, per = 100_000, 1000
