@@ -2,13 +2,18 @@
 //
 // Kernels
 //   table_insert   : distinct sketch hashes -> open-addressing table in HBM (linear probing
-//                    from a multiplicative-hash home slot), one atomicCAS per hash; a 16-byte slot
-//                    holds the key and the smallest DB hash index holding it, the key's canonical
-//                    index (the claiming thread's own; keys shared by references fixed up after).  Hit counts are kept per canonical index, in the
+//                    from a multiplicative-hash home slot), one atomicCAS per hash.  An 8-byte
+//                    slot holds the key's high 32 bits and the smallest DB index holding the key
+//                    (its canonical index); a probe that matches the high word checks the full key
+//                    against the DB's hash array at that index.  Device-scope atomics are done
+//                    past the L2 on this part, so any second store per insert (a canonical-index
+//                    word beside the key) is another random line write: +4.3 ms on 1e8 hashes
+//                    (tools/insert_bench.hip); here the CAS writes both at once.  Hit counts are kept per canonical index, in the
 //                    DB's own order: the same on every rank whatever slots the parallel insertion
 //                    gave the keys, so the ranks' counts add up as they are (one all-reduce).
 //   canon_of       : per DB hash, the canonical index of its key (duplicates across references
-//                    share one counter): written by the insert, fixed up for duplicates.
+//                    share one counter): written by the insert, fixed up for duplicates (a key
+//                    held by several references: rare, listed by the insert).
 //   screen_count<K>: one thread = one 64-position tile of the pooled, packed query bases.
 //                    Rolling 2-bit forward / reverse-complement words decide the canonical
 //                    strand by integer compare (== Mash's memcmp on ASCII, since A<C<G<T);
@@ -113,7 +118,8 @@ struct CountParams {
     int64_t n_bases, pos_begin, pos_end;
     uint32_t seed;
     int ndb;
-    const uint64_t *tab[kMaxDb];   // 16-byte slots: key, canonical index
+    const uint64_t *tab[kMaxDb];   // slots: key's high 32 bits, canonical index
+    const uint64_t *hashes[kMaxDb];  // the DB's hashes (full-key check of a high-word match)
     uint64_t mask[kMaxDb];
     int shift[kMaxDb];
     uint32_t *counts[kMaxDb];      // per canonical index, + [nhash] for the all-ones hash
@@ -179,12 +185,12 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
                 const uint64_t *tab = P.tab[d];
                 uint64_t s = home_slot(h, P.shift[d]);
                 for (;;) {
-                    const uint64_t key = tab[2 * s];
-                    if (key == h) {
-                        atomicAdd(&P.counts[d][(uint32_t)tab[2 * s + 1]], 1u);
+                    const uint64_t w = tab[s];
+                    if (w == kEmpty) break;
+                    if ((w >> 32) == (h >> 32) && P.hashes[d][(uint32_t)w] == h) {
+                        atomicAdd(&P.counts[d][(uint32_t)w], 1u);
                         break;
                     }
-                    if (key == kEmpty) break;
                     s = (s + 1) & P.mask[d];
                 }
             }
@@ -197,62 +203,53 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(P.nkmers, v);
 }
 
-// insert: the thread whose CAS claims an empty slot owns it and writes the slot's second word
-// (canonical index and owner, both its own index) with a plain store on the line the CAS just
-// brought in, and canon_of[i] = i; a thread finding its key already there (a hash shared by
-// references) is marked in slot_of (kDup) and fixed up by the two passes below.  Keys appear
-// once in most DBs, so the common insert costs one CAS and two plain stores (an atomicMin per
-// insert for the canonical index cost 5 ms of 13 on 1e8 hashes, and a gather pass 2.5 ms).
-constexpr int64_t kDup = 1ll << 62;
-
+// insert: one CAS of (key's high word, own index) into the first slot that is empty or holds
+// the key.  Finding the key already there (a hash shared by references: the high word matches
+// and the full key at the holder's index), the thread lowers the slot's index to its own if
+// smaller (a 64-bit atomicMin: the high words are equal) and lists itself with the index it
+// saw; canon_of[i] = i is written for every hash and fixed for the listed ones after.
 __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t *__restrict__ hashes, int64_t n,
                                                            unsigned long long *tab, uint64_t mask, int shift,
-                                                           int64_t nslots, int64_t *slot_of, int32_t *canon_of) {
+                                                           int64_t *dups, int32_t *canon_of) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t h = hashes[i];
     canon_of[i] = h == kEmpty ? (int32_t)n : (int32_t)i;
-    if (h == kEmpty) {
-        slot_of[i] = nslots;
-        return;
-    }
+    if (h == kEmpty) return;
+    const unsigned long long want = (h & 0xFFFFFFFF00000000ull) | (uint32_t)i;
     uint64_t s = home_slot(h, shift);
     for (;;) {
-        unsigned long long prev = atomicCAS(&tab[2 * s], (unsigned long long)kEmpty, (unsigned long long)h);
-        if (prev == kEmpty) {  // owner
-            tab[2 * s + 1] = (unsigned long long)(uint32_t)i | (unsigned long long)(uint32_t)i << 32;
-            slot_of[i] = (int64_t)s;
-            return;
-        }
-        if (prev == h) {  // a duplicate of an owned key
-            slot_of[i] = (int64_t)s | kDup;
+        const unsigned long long prev = atomicCAS(&tab[s], (unsigned long long)kEmpty, want);
+        if (prev == kEmpty) return;  // claimed
+        if ((prev >> 32) == (h >> 32) && hashes[(uint32_t)prev] == h) {  // the key is there already
+            atomicMin(&tab[s], want);
+            const unsigned long long k = atomicAdd(reinterpret_cast<unsigned long long *>(dups), 1ull);
+            dups[1 + k] = (int64_t)((uint64_t)i << 32 | (uint32_t)prev);
             return;
         }
         s = (s + 1) & mask;
     }
 }
 
-// duplicates, pass 1 (after every owner's store): the slot's canonical index = the smallest
-// index holding its key
-__global__ __launch_bounds__(256) void dup_min_kernel(const int64_t *__restrict__ slot_of, int64_t n,
-                                                      unsigned long long *tab) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t v = slot_of[i];
-    if (v & kDup) atomicMin(reinterpret_cast<unsigned int *>(&tab[2 * (v & ~kDup) + 1]), (unsigned int)i);
-}
-
-// duplicates, pass 2: each duplicate and its slot's owner take the final canonical index
-__global__ __launch_bounds__(256) void dup_fix_kernel(const int64_t *__restrict__ slot_of, int64_t n,
-                                                      const unsigned long long *tab, int32_t *canon_of) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t v = slot_of[i];
-    if (!(v & kDup)) return;
-    const unsigned long long w = tab[2 * (v & ~kDup) + 1];
-    const int32_t c = (int32_t)(uint32_t)w;
-    canon_of[i] = c;
-    canon_of[(uint32_t)(w >> 32)] = c;  // the owner (every duplicate of the slot writes the same value)
+// listed duplicates (after every insert and atomicMin): each, and the index it found holding
+// the key (the owner is found by the first duplicate to arrive), take the slot's final index
+__global__ __launch_bounds__(256) void dup_fix_kernel(const uint64_t *__restrict__ hashes, const int64_t *dups,
+                                                      const unsigned long long *tab, uint64_t mask, int shift,
+                                                      int32_t *canon_of) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= dups[0]) return;
+    const uint64_t e = (uint64_t)dups[1 + k];
+    const uint32_t j = (uint32_t)(e >> 32), p = (uint32_t)e;
+    const uint64_t h = hashes[j];
+    uint64_t s = home_slot(h, shift);
+    unsigned long long w;
+    for (;;) {  // the key's slot (it is in the table: j's CAS found it)
+        w = tab[s];
+        if ((w >> 32) == (h >> 32) && hashes[(uint32_t)w] == h) break;
+        s = (s + 1) & mask;
+    }
+    canon_of[j] = (int32_t)(uint32_t)w;
+    canon_of[p] = (int32_t)(uint32_t)w;
 }
 
 template <typename T>
@@ -352,33 +349,30 @@ int64_t hymet_screen_table_slots(int64_t n_hashes) {
 }
 
 int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n, uint64_t *d_table, int64_t n_slots,
-                             int64_t *d_slot_of, int32_t *d_canon_of) {
-    HY_ARG(ctx && d_table && d_slot_of && d_canon_of, "hymet_screen_table_build: null argument");
+                             int64_t *d_scratch, int32_t *d_canon_of) {
+    HY_ARG(ctx && d_table && d_scratch && d_canon_of, "hymet_screen_table_build: null argument");
     HY_ARG(n_slots >= 1024 && (n_slots & (n_slots - 1)) == 0, "hymet_screen_table_build: n_slots must be a power of two >= 1024");
     HY_ARG(n_slots >= 2 * n, "hymet_screen_table_build: n_slots must be >= 2*n_hashes");
     HY_ARG(n < (1ll << 31) - 1, "hymet_screen_table_build: more than 2^31 - 2 hashes");
     HY_HIP(hipSetDevice(ctx->device));
-    // empty key ~0 and canonical index 0xFFFFFFFF (above any index: the unsigned atomicMin)
-    HY_HIP(hipMemsetAsync(d_table, 0xFF, (size_t)n_slots * 16, ctx->stream));
+    HY_HIP(hipMemsetAsync(d_table, 0xFF, (size_t)n_slots * 8, ctx->stream));  // empty: all ones (no index is 2^32 - 1)
     if (n <= 0) return HYMET_OK;
+    HY_HIP(hipMemsetAsync(d_scratch, 0, 8, ctx->stream));                    // the duplicate count
     const int lg = log2_exact(n_slots);
     hymet::ProfScope _ps(ctx, "screen_table_build");
     const dim3 grid((unsigned)hymet::cdiv(n, 256));
     hipLaunchKernelGGL(table_insert_kernel, grid, dim3(256), 0, ctx->stream, d_hashes, n, (unsigned long long *)d_table,
-                       (uint64_t)(n_slots - 1), 64 - lg, n_slots, d_slot_of, d_canon_of);
+                       (uint64_t)(n_slots - 1), 64 - lg, d_scratch, d_canon_of);
     HY_CHECK_LAUNCH("table_insert_kernel");
-    hipLaunchKernelGGL(dup_min_kernel, grid, dim3(256), 0, ctx->stream, (const int64_t *)d_slot_of, n,
-                       (unsigned long long *)d_table);
-    HY_CHECK_LAUNCH("dup_min_kernel");
-    hipLaunchKernelGGL(dup_fix_kernel, grid, dim3(256), 0, ctx->stream, (const int64_t *)d_slot_of, n,
-                       (const unsigned long long *)d_table, d_canon_of);
+    hipLaunchKernelGGL(dup_fix_kernel, grid, dim3(256), 0, ctx->stream, d_hashes, (const int64_t *)d_scratch,
+                       (const unsigned long long *)d_table, (uint64_t)(n_slots - 1), 64 - lg, d_canon_of);
     HY_CHECK_LAUNCH("dup_fix_kernel");
     return HYMET_OK;
 }
 
 int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask, int64_t n_bases, int64_t pos_begin,
                        int64_t pos_end, int k, uint32_t seed, int ndb, const uint64_t *const *h_d_tables,
-                       const int64_t *h_n_slots, const int64_t *h_n_hashes,
+                       const int64_t *h_n_slots, const uint64_t *const *h_d_hashes, const int64_t *h_n_hashes,
                        uint32_t *const *h_d_counts, uint64_t cand_thr, uint64_t *d_cand,
                        int64_t cand_cap, unsigned long long *d_cand_n, unsigned long long *d_nkmers) {
     HY_ARG(ctx && d_2b && d_mask && d_cand_n && d_nkmers, "hymet_screen_count: null argument");
@@ -399,8 +393,9 @@ int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_m
     for (int d = 0; d < ndb; d++) {
         const int64_t ns = h_n_slots[d];
         HY_ARG(ns >= 1024 && (ns & (ns - 1)) == 0, "hymet_screen_count: table size must be a power of two");
-        HY_ARG(h_d_tables[d] && h_d_counts[d] && h_n_hashes[d] >= 0, "hymet_screen_count: null table");
+        HY_ARG(h_d_tables[d] && h_d_hashes[d] && h_d_counts[d] && h_n_hashes[d] >= 0, "hymet_screen_count: null table");
         P.tab[d] = h_d_tables[d];
+        P.hashes[d] = h_d_hashes[d];
         P.mask[d] = (uint64_t)(ns - 1);
         P.shift[d] = 64 - log2_exact(ns);
         P.counts[d] = h_d_counts[d];

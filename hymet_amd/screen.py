@@ -39,9 +39,9 @@ class ScreenTable:
         n = int(len(db.hashes))
         self.n_hashes = n
         self.n_slots = int(gpu.lib.hymet_screen_table_slots(n))
-        self.table = gpu.empty(2 * self.n_slots, torch.int64)   # 16-byte slots: key, canonical index
+        self.table = gpu.empty(self.n_slots, torch.int64)   # slots: key's high word, canonical index
         self.canon_of = gpu.empty(max(n, 1), torch.int32)
-        slot_of = gpu.empty(max(n, 1), torch.int64)      # build scratch
+        scratch = gpu.empty(max(n, 1) + 1, torch.int64)     # build scratch: duplicate keys
         dev = getattr(db, "dev_hashes", None)
         if not n:
             d_h = gpu.empty(1, torch.int64)
@@ -55,8 +55,9 @@ class ScreenTable:
         # the offsets first: a pageable upload waits for the stream's earlier work, and queued
         # behind the insert it would hold the host for the whole build
         self.ref_off = torch.from_numpy(np.ascontiguousarray(db.offsets, dtype=np.int64)).to(gpu.dev)
-        gpu.call("hymet_screen_table_build", ptr(d_h), n, ptr(self.table), self.n_slots, ptr(slot_of), ptr(self.canon_of))
-        del d_h, slot_of
+        gpu.call("hymet_screen_table_build", ptr(d_h), n, ptr(self.table), self.n_slots, ptr(scratch), ptr(self.canon_of))
+        self.hashes = d_h          # probes check full keys here: it lives as long as the table
+        del scratch
 
 
 @dataclass
@@ -95,10 +96,11 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
     thr = U64_MAX if frac >= 1.0 else int(frac * float(top))
     keys_arr = (ctypes.c_void_p * 4)(*[ptr(t.table).value for t in tables])
     slots_arr = (ctypes.c_int64 * 4)(*[t.n_slots for t in tables])
+    hash_arr = (ctypes.c_void_p * 4)(*[ptr(t.hashes).value for t in tables])
     nh_arr = (ctypes.c_int64 * 4)(*[t.n_hashes for t in tables])
     cnt_arr = (ctypes.c_void_p * 4)(*[ptr(c).value for c in counts])
     gpu.call("hymet_screen_count", ptr(pool.w2b), ptr(pool.wmask), n_bases, pos_begin, pos_end, k, seed,
-             len(tables), keys_arr, slots_arr, nh_arr, cnt_arr, thr, ptr(cand), cap, ptr(cand_n), ptr(nk))
+             len(tables), keys_arr, slots_arr, hash_arr, nh_arr, cnt_arr, thr, ptr(cand), cap, ptr(cand_n), ptr(nk))
     n_kmers = int(nk.item())
     dummy = gpu.zeros(1, torch.int64)
 
@@ -106,7 +108,7 @@ def count_pool(gpu, pool, tables: Sequence[ScreenTable], k: int, seed: int, s: i
         buf = gpu.empty(cap_, torch.int64)
         cand_n.zero_()
         gpu.call("hymet_screen_count", ptr(pool.w2b), ptr(pool.wmask), n_bases, pos_begin, pos_end, k, seed,
-                 0, keys_arr, slots_arr, nh_arr, cnt_arr, thr_, ptr(buf), cap_, ptr(cand_n), ptr(dummy))
+                 0, keys_arr, slots_arr, hash_arr, nh_arr, cnt_arr, thr_, ptr(buf), cap_, ptr(cand_n), ptr(dummy))
         return buf
 
     while True:

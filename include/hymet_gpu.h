@@ -113,14 +113,16 @@ int hymet_name_hash(hymet_ctx *ctx, const uint8_t *d_raw, const int64_t *d_name_
  * sketch hashes of a DB, counts of every pooled canonical k-mer hash that hits it, and the
  * per-reference shared / median-depth statistics. */
 int64_t hymet_screen_table_slots(int64_t n_hashes);
-/* d_table: n_slots 16-byte slots (2 * n_slots uint64: key, then the smallest input index
- * holding it -- its canonical index -- in the low 32 bits); d_slot_of: n_hashes int64 (slot of
- * each input hash, n_slots for the reserved all-ones key); d_canon_of: n_hashes int32, each
- * input hash's canonical index (n_hashes for the all-ones key).  Hits are counted per canonical
- * index, so counts are in the DB's own order on every rank whatever slots parallel insertion
- * chose, and the ranks' partial counts add up as they are.  Resets d_table. */
+/* d_table: n_slots uint64 slots, each (key >> 32) << 32 | the smallest input index holding
+ * the key (its canonical index), all ones when empty -- a probe matching the high word checks
+ * the full key at d_hashes[index], so d_hashes must stay allocated while the table is used;
+ * d_scratch: n_hashes + 1 int64 (the duplicate keys' list); d_canon_of: n_hashes int32, each
+ * input hash's canonical index (n_hashes for the reserved all-ones key).  Hits are counted per
+ * canonical index, so counts are in the DB's own order on every rank whatever slots parallel
+ * insertion chose, and the ranks' partial counts add up as they are.  Resets
+ * d_table. */
 int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n_hashes,
-                             uint64_t *d_table, int64_t n_slots, int64_t *d_slot_of, int32_t *d_canon_of);
+                             uint64_t *d_table, int64_t n_slots, int64_t *d_scratch, int32_t *d_canon_of);
 /* The library's stable LSD radix sort (8-bit digits) of device (key, value) pairs by key bits
  * [begin_bit, end_bit), in place (the sort behind the mapper's minimizer, group, chain and
  * anchor-segment orders and the LCA row order; no rocPRIM on the mapping path). */
@@ -179,7 +181,7 @@ void hymet_msh_close(hymet_msh *m);
 int hymet_screen_count(hymet_ctx *ctx, const uint32_t *d_2b, const uint32_t *d_mask,
                        int64_t n_bases, int64_t pos_begin, int64_t pos_end, int k, uint32_t seed,
                        int ndb, const uint64_t *const *h_d_tables, const int64_t *h_n_slots,
-                       const int64_t *h_n_hashes,
+                       const uint64_t *const *h_d_hashes, const int64_t *h_n_hashes,
                        uint32_t *const *h_d_counts, uint64_t cand_thr, uint64_t *d_cand,
                        int64_t cand_cap, unsigned long long *d_cand_n,
                        unsigned long long *d_nkmers);

@@ -143,7 +143,7 @@ def test_gpu_hash_kat_x86_32(gpu):
 def test_table_canonical_index_is_the_first_holder(gpu, dup_frac):
     """hymet_screen_table_build: every DB hash's canonical index is the smallest index holding
     its key (hashes shared by references, the insert's duplicate fix-up), the all-ones key maps
-    to the extra counter n, and each slot's second word carries its key's canonical index."""
+    to the extra counter n, and each slot holds its key's high word and canonical index."""
     from hymet_amd import screen as scr
     from hymet_amd.msh import SketchDB
     rng = np.random.default_rng(int(dup_frac * 10) + 3)
@@ -163,9 +163,10 @@ def test_table_canonical_index_is_the_first_holder(gpu, dup_frac):
     want = first[inv].astype(np.int64)
     want[h == np.uint64(2**64 - 1)] = len(h)
     np.testing.assert_array_equal(got, want)
-    tab = t.table.cpu().numpy().view(np.uint64).reshape(-1, 2)
-    used = tab[:, 0] != np.uint64(2**64 - 1)
-    keys, canon = tab[used, 0], (tab[used, 1] & np.uint64(0xFFFFFFFF)).astype(np.int64)
-    assert len(keys) == len(np.unique(h[h != np.uint64(2**64 - 1)]))
-    pos = np.searchsorted(np.unique(h), keys)
-    np.testing.assert_array_equal(canon, first[pos])
+    tab = t.table.cpu().numpy().view(np.uint64)
+    used = tab != np.uint64(2**64 - 1)
+    canon = (tab[used] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    assert len(canon) == len(np.unique(h[h != np.uint64(2**64 - 1)]))     # one slot per distinct key
+    np.testing.assert_array_equal(tab[used] >> np.uint64(32), h[canon] >> np.uint64(32))   # high word = key's
+    keys = h[canon]
+    np.testing.assert_array_equal(canon, first[np.searchsorted(np.unique(h), keys)])
