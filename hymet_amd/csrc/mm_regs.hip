@@ -166,7 +166,10 @@ __device__ __forceinline__ int32_t mini_idx_at(const AnchorStatParams &P, int64_
 // block), their loads issued row after row before any is used -- one position per thread
 // left every thread waiting on a chain of ~6 dependent loads (chain, query, chain slot,
 // anchor, minimizer index) with nothing else in flight
-constexpr int kStatItems = 4;
+#ifndef HYMET_STAT_ITEMS
+#define HYMET_STAT_ITEMS 4
+#endif
+constexpr int kStatItems = HYMET_STAT_ITEMS;
 constexpr int kStatSpan = 256 * kStatItems;  // chain-order positions per block
 
 // the chain holding chain-order position kStatSpan b, for every block b of
