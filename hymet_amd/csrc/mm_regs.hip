@@ -165,9 +165,11 @@ __device__ __forceinline__ int32_t mini_idx_at(const AnchorStatParams &P, int64_
 // chain_stats_flat_kernel: kStatItems chain-order positions per thread (rows of 256 in a
 // block), their loads issued row after row before any is used -- one position per thread
 // left every thread waiting on a chain of ~6 dependent loads (chain, query, chain slot,
-// anchor, minimizer index) with nothing else in flight
+// anchor, minimizer index) with nothing else in flight.  Two per thread: C4 one-stream
+// 108.6 ms per step at four, 86.6 at two, 196.5 at eight (the register-held rows cost
+// occupancy; profiles/r05_chain_stats/)
 #ifndef HYMET_STAT_ITEMS
-#define HYMET_STAT_ITEMS 4
+#define HYMET_STAT_ITEMS 2
 #endif
 constexpr int kStatItems = HYMET_STAT_ITEMS;
 constexpr int kStatSpan = 256 * kStatItems;  // chain-order positions per block
@@ -382,8 +384,11 @@ __global__ __launch_bounds__(64) void query_sumk_kernel(const uint64_t *mini_pos
 // kernel leaves them.  Real genomes make such queries common: a contig that carries a
 // repeat (an IS element, an rRNA operon) hits every copy in every strain, hundreds to
 // thousands of chains, and one thread walking them through global memory took ~0.9 s per
-// step on the Zymo-backbone workload.
-constexpr int kRegWave = 48;
+// step on the Zymo-backbone workload.  From 17 chains on: at C5 (5,000 candidates, ~350 PAF
+// lines per contig) the thread kernel's divergent 17-48-chain queries held the regions scope
+// at 1.52 s per step, 0.40 s with them on the wave kernel; C4 unchanged (1,258 vs 1,255 ms)
+// (profiles/r05_chain_stats/, profiles/r05_c5_pmc/).
+constexpr int kRegWave = 16;
 constexpr int kRegSmall = 256;  // the wave kernel holds a query's regions in LDS up to this many
 constexpr int kRegEntryBytes = 16 + 16 + 4 * 3 + 8;  // slot, aux, wl, psub, pns, covb per entry
 // global scratch of the wave kernel per chain: a query of n > kRegSmall chains takes m < 2n
