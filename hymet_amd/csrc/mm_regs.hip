@@ -2,7 +2,7 @@
 // mm_gen_regs (score + hash order), mm_reg_set_coor / mm_cal_fuzzy_len, mm_set_parent,
 // mm_select_sub (+ mm_sync_regs), mm_est_err, mm_filter_strand_retained, mm_set_mapq.
 // Everything that walks a chain's anchors is anchor-parallel and runs first:
-//   chain_stats_flat_kernel four chained anchors per thread: mlen/blen terms (mm_reg_set_coor),
+//   chain_stats_flat_kernel two chained anchors per thread: mlen/blen terms (mm_reg_set_coor),
 //                           its minimizer index (mm_est_err's get_mini_idx, by table lookup)
 //                           and the first anchor, in est_err's walking order, whose index does
 //                           not increase -- est_err's sequential two-pointer walk matches

@@ -37,7 +37,10 @@ constexpr uint64_t kEmpty = ~0ull;
 // alone would crowd every real sketch into the bottom of the table: a bottom-s MinHash sketch
 // holds the s SMALLEST hashes of its genome, so their top bits are all zero.
 __device__ __forceinline__ uint64_t home_slot(uint64_t h, int shift) { return (h * 0x9E3779B97F4A7C15ull) >> shift; }
-constexpr int kTile = 64;  // k-mer start positions per thread (multiple of 32: lanes stay in phase)
+#ifndef HYMET_SCREEN_TILE
+#define HYMET_SCREEN_TILE 64
+#endif
+constexpr int kTile = HYMET_SCREEN_TILE;  // k-mer start positions per thread (multiple of 32: lanes stay in phase)
 constexpr int kMaxDb = 4;
 
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
