@@ -614,10 +614,23 @@ int sort_segments(hymet_ctx *ctx, const Seg *lists, int64_t cap, const int32_t *
     }
     HY_SEG_LAUNCH(kB256, (block_seg_sort_kernel<64, 4>), 64)
     HY_SEG_LAUNCH(kB512, (block_seg_sort_kernel<64, 8>), 64)
-    HY_SEG_LAUNCH(kB1K, (block_seg_sort_kernel<64, 16>), 64)
-    HY_SEG_LAUNCH(kB2K, (block_seg_sort_kernel<128, 16>), 128)
-    HY_SEG_LAUNCH(kB4K, (block_seg_sort_kernel<256, 16>), 256)
-    HY_SEG_LAUNCH(kB8K, (block_seg_sort_kernel<512, 16>), 512)
+    // (A/B knobs: threads per block of the 1K / 2K / 4K / 8K classes; items = class size / threads)
+#ifndef HYMET_SORT_T1K
+#define HYMET_SORT_T1K 64
+#endif
+#ifndef HYMET_SORT_T2K
+#define HYMET_SORT_T2K 128
+#endif
+#ifndef HYMET_SORT_T4K
+#define HYMET_SORT_T4K 256
+#endif
+#ifndef HYMET_SORT_T8K
+#define HYMET_SORT_T8K 512
+#endif
+    HY_SEG_LAUNCH(kB1K, (block_seg_sort_kernel<HYMET_SORT_T1K, 1024 / HYMET_SORT_T1K>), HYMET_SORT_T1K)
+    HY_SEG_LAUNCH(kB2K, (block_seg_sort_kernel<HYMET_SORT_T2K, 2048 / HYMET_SORT_T2K>), HYMET_SORT_T2K)
+    HY_SEG_LAUNCH(kB4K, (block_seg_sort_kernel<HYMET_SORT_T4K, 4096 / HYMET_SORT_T4K>), HYMET_SORT_T4K)
+    HY_SEG_LAUNCH(kB8K, (block_seg_sort_kernel<HYMET_SORT_T8K, 8192 / HYMET_SORT_T8K>), HYMET_SORT_T8K)
     HY_SEG_LAUNCH(kB16K, (block_seg_sort_kernel<1024, 16>), 1024)
 #undef HY_SEG_LAUNCH
     return HYMET_OK;
