@@ -397,7 +397,8 @@ class Pipeline:
             if self.db_paths:
                 self._read_dbs(side)
                 if side is not None and self._sliced():
-                    self._join_slices(side)
+                    if not self._db_gather_main():
+                        self._join_slices(side)
                 elif side is not None:
                     self._build_tables(side)
         finally:
@@ -409,9 +410,18 @@ class Pipeline:
     def _sliced(self):
         return any(getattr(db, "dev_slice", None) is not None for db in self.dbs)
 
+    @staticmethod
+    def _db_gather_main() -> bool:
+        """HYMET_DB_GATHER=main: all-gather the DB slices and build the tables on the calling
+        thread after the ingest (one thread issuing every collective) instead of on the loader
+        thread beside it -- the fallback if concurrent collectives on two communicators ever
+        misbehave on a multi-GPU node (about 8 ms more per rank step at N = 8)."""
+        return os.environ.get("HYMET_DB_GATHER", "loader") == "main"
+
     def _join_slices(self, side):
         """The DBs' hash slices all-gathered on side's stream (behind this rank's DMAs), then
-        the tables built there -- on the loader thread, overlapping the contigs' ingest.  The
+        the tables built there -- on the loader thread, overlapping the contigs' ingest (or,
+        with HYMET_DB_GATHER=main, on the calling thread after it).  The
         all-gathers go over the communicator Comm keeps for the DB load alone (Comm.db_group),
         so they cannot interleave with the main thread's collectives: every rank issues the
         DB all-gathers in DB order on one communicator, the rest in run order on the other."""
@@ -715,6 +725,9 @@ class Pipeline:
         lap("input_wait_s")                   # the loader thread's remainder after the ingest
         if reader is not None and self.db_paths and side is None:
             self._build_tables()
+        elif reader is not None and side is not None and not self.tables and self._sliced():
+            self._join_slices(side)           # HYMET_DB_GATHER=main
+            lap("db_join_s")
         selected, rows, thr = self.screen_select(sh.mash)
         if not selected:
             raise RuntimeError("candidate list empty after applying limit")  # run_hymet_cami.sh:126

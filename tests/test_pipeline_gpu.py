@@ -167,10 +167,11 @@ def test_emit_tsv_confidence_rounding(gpu):
     assert got == buf.getvalue().encode()
 
 
-def _world2_worker(rank, port, data_path, msh_path, tax, hier, q):
+def _world2_worker(rank, port, data_path, msh_path, tax, hier, q, db_gather="loader"):
     import os
     import traceback
     try:
+        os.environ["HYMET_DB_GATHER"] = db_gather
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         from hymet_amd import pipeline
@@ -204,7 +205,8 @@ def _w2_setup(gpu):
 
 
 @pytest.mark.timeout(300)
-def test_world2_pipeline_equals_world1(gpu, tmp_path):
+@pytest.mark.parametrize("db_gather", ["loader", "main"])
+def test_world2_pipeline_equals_world1(gpu, tmp_path, db_gather):
     """Two ranks (two processes on this GPU, gloo staging the collectives through the host):
     each takes a contiguous half of the same FASTA; rank 0's TSV equals the one-rank TSV and
     the ranks' PAF texts concatenate to the one-rank PAF (one index part).  The ranks read the
@@ -229,7 +231,7 @@ def test_world2_pipeline_equals_world1(gpu, tmp_path):
         port = s.getsockname()[1]
     ctx = mpc.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_world2_worker, args=(r, port, str(dp), str(mp_), str(tax), str(hier), q)) for r in range(2)]
+    ps = [ctx.Process(target=_world2_worker, args=(r, port, str(dp), str(mp_), str(tax), str(hier), q, db_gather)) for r in range(2)]
     for x in ps:
         x.start()
     got = {}
