@@ -663,6 +663,8 @@ def bench_emulate(args, gpu, torch):
         x_db = EmulatedComm.model_ms(db_step, N)
         ing, wait, rd = phe.get("ingest_s", 0.0), phe.get("input_wait_s", 0.0), phe.get("reader_s", 0.0)
         x_db_exposed = max(0.0, rd + x_db - ing) - wait
+        if os.environ.get("HYMET_DB_GATHER", "loader") == "main":
+            x_db_exposed = x_db                # on the calling thread: in series with the step
         model = x_main + max(0.0, x_db_exposed)
         out_ranks[str(R)] = {
             "shard_records": [int(r0), int(r1)], "shard_mbp": float(fx.nbases[r0:r1].sum()) / 1e6,
