@@ -25,7 +25,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from ._lib import HymetError, check, load, ptr
+from ._lib import check, load, ptr
 from .seqio import SeqSet
 
 _c = ctypes
