@@ -1859,8 +1859,9 @@ constexpr int kBtWin = 8;
 // reads each step's node from it with readlane.  A fence after each walk and L2 loads of t
 // make the walk's marks visible to the next probes.
 // (C4: threshold 1024 -> 128 took mm_backtrack 623 -> 301 ms per step once the wave kernel
-// stopped issuing agent-scope fences)
-constexpr int64_t kBtLong = 128;
+// stopped issuing agent-scope fences; round 5, 128 -> 64: 1,247 -> 1,239 ms per step, 256:
+// 1,277 -- profiles/r05_bt_long/)
+constexpr int64_t kBtLong = 64;
 // The wave kernel's work counters (backtrack_long_kernel): kBtStripes of them, kBtCtrPad
 // ints apart, each atomic taking kBtGrab positions of its stripe
 #ifndef HYMET_BT_GRAB
