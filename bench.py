@@ -335,7 +335,8 @@ def bench_cami(args, comm, gpu, torch):
                    "global_contigs": n_contigs, "parallelism": f"contig-shard x{comm.world}",
                    "backend": (("nccl (RCCL over xGMI)" if comm.dist.get_backend() == "nccl" else comm.dist.get_backend())
                                if comm.dist is not None else "none (1 rank)"),
-                   "window": "sketch{1..3}.msh + detailed_taxonomy.tsv + taxonomy_hierarchy.tsv read, FASTA bytes in host "
+                   "window": " + ".join(os.path.basename(q) for q in (pipe.db_paths or [])) +
+                             " + detailed_taxonomy.tsv + taxonomy_hierarchy.tsv read, FASTA bytes in host "
                              "memory -> classified_sequences.tsv written + resultados.paf text in host memory (DB parse + "
                              "table build, taxonomy load, ingest, H2D, screen, select, limit, map, LCA, text emit inside "
                              "every step)"},

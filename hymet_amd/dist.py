@@ -7,13 +7,22 @@ PAF-line counts (all-reduce, int32 sum) and the per-contig results (gather to ra
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import threading
 from typing import List, Sequence
 
 import numpy as np
 
 
 class Comm:
+    """Collectives of one rank.  Invariant: at any moment ONE host thread issues collectives.
+    The per-run DB load (Pipeline's loader thread) takes the communicator with `owned()` for
+    the whole of its all-gathers and the table build behind them, and the calling thread
+    issues no collective until it has joined the loader; `_check_owner` turns any breach of
+    that order into an error instead of an RCCL deadlock (NCCL/RCCL guarantee progress only
+    when every rank issues its collectives in one order)."""
+
     def __init__(self, rank: int = 0, world: int = 1, replicated_pool: bool = False):
         """replicated_pool: every rank holds the same contig pool (the screen then splits
         k-mer positions); otherwise (default) each rank's pool is its own contig shard."""
@@ -22,6 +31,27 @@ class Comm:
         self.dist = None
         self.device = None
         self.db_group = None
+        self._owner = None          # thread ident holding the communicator (owned()), else None
+
+    @contextlib.contextmanager
+    def owned(self):
+        """This thread alone may issue collectives until the block ends (the loader thread's
+        DB all-gathers: the block also covers the stream synchronisation behind them, so no
+        collective of theirs is still running on the GPU when another thread's is issued)."""
+        me = threading.get_ident()
+        if self._owner is not None and self._owner != me:
+            raise RuntimeError("Comm.owned: another thread holds the communicator")
+        prev, self._owner = self._owner, me
+        try:
+            yield self
+        finally:
+            self._owner = prev
+
+    def _check_owner(self):
+        o = self._owner
+        if o is not None and o != threading.get_ident():
+            raise RuntimeError("collective issued while another thread holds the communicator "
+                               "(two threads' collectives could interleave differently per rank)")
 
     @classmethod
     def from_env(cls) -> "Comm":
@@ -41,12 +71,20 @@ class Comm:
             if backend == "nccl" and gpu is not None:
                 kw["device_id"] = gpu.dev
             dist.init_process_group(backend, rank=self.rank, world_size=self.world, **kw)
-        # a second communicator over the same ranks for the per-run DB load: its all-gathers
-        # run on the loader thread while the main thread's collectives go over the default one
+        # a second communicator over the same ranks for the per-run DB load (the loader
+        # thread's all-gathers, while it holds the communicator: owned())
         self.db_group = dist.new_group(list(range(self.world)))
         self.dist = dist
         self.device = gpu.dev if gpu is not None else torch.device("cpu")
         self.torch = torch
+        # both communicators created now, on this thread and in this order on every rank (RCCL
+        # would otherwise create db_group's lazily, on the loader thread, at its first use)
+        on_dev = dist.get_backend() == "nccl"
+        for g in (None, self.db_group):
+            t = torch.zeros(1, dtype=torch.int32, device=self.device if on_dev else "cpu")
+            dist.all_reduce(t, group=g)
+        if on_dev:
+            torch.cuda.synchronize(self.device)
         return self
 
     # ------------------------------------------------------------- partitioning
@@ -78,6 +116,7 @@ class Comm:
 
     def allreduce_sum_(self, t):
         if self.world > 1:
+            self._check_owner()
             if self._staged(t):
                 h = t.cpu()
                 self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM)
@@ -90,6 +129,7 @@ class Comm:
         """All-gather the first n rows of t (n may differ per rank): rows padded to the
         largest n; returns the list of every rank's first-n slices."""
         torch = self.torch
+        self._check_owner()
         ns = [int(x[0]) for x in self.allgather_np(np.array([n], np.int64))]
         m = max(ns) if ns else 0
         pad = torch.zeros((max(m, 1),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
@@ -109,6 +149,7 @@ class Comm:
         (db_group: called from the loader thread).  key names the DB for EmulatedComm."""
         if self.world <= 1:
             return t
+        self._check_owner()
         mine = t[self.rank * c:(self.rank + 1) * c]
         if self._staged(t):
             parts = [self.torch.empty(c, dtype=t.dtype) for _ in range(self.world)]
@@ -174,6 +215,7 @@ class Comm:
         """All-gather of a small host array (tag names the exchange for EmulatedComm)."""
         if self.world <= 1:
             return [arr]
+        self._check_owner()
         objs = [None] * self.world
         self.dist.all_gather_object(objs, np.ascontiguousarray(arr))
         return objs
@@ -181,6 +223,7 @@ class Comm:
     def gather_obj(self, obj, dst: int = 0):
         if self.world <= 1:
             return [obj]
+        self._check_owner()
         out = [None] * self.world if self.rank == dst else None
         self.dist.gather_object(obj, out, dst=dst)
         return out
@@ -188,17 +231,20 @@ class Comm:
     def broadcast_obj(self, obj, src: int = 0):
         if self.world <= 1:
             return obj
+        self._check_owner()
         lst = [obj]
         self.dist.broadcast_object_list(lst, src=src)
         return lst[0]
 
     def barrier(self):
         if self.world > 1:
+            self._check_owner()
             self.dist.barrier()
 
     def max_float(self, v: float) -> float:
         if self.world <= 1:
             return v
+        self._check_owner()
         t = self.torch.tensor([v], dtype=self.torch.float64, device=self.device)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())

@@ -12,9 +12,11 @@ INPUT_FASTA into input/; mash.sh:14 and minimap2.sh:23 read it).  Here:
     PAF / TSV writers read, and the mapping batches (contiguous record ranges sized for the
     anchor working set).
 
-Multi-GPU: every rank indexes the same FASTA bytes and takes the contiguous
-record range `FastaIndex.shard(rank, world)` balanced by bases, so the ranks' query indices
-are consecutive slices of the input order.
+Multi-GPU: every rank holds the same FASTA bytes and indexes, uploads and
+maps only its own contiguous byte range (`shard_bytes`: the cuts k * len / world moved to the
+next record start), so the ranks' query indices are consecutive slices of the input order.
+`FastaIndex.shard` (record ranges balanced by bases) serves inputs given as a whole-file
+record table.
 """
 from __future__ import annotations
 
@@ -185,7 +187,7 @@ def _batches(lengths: np.ndarray, max_bases: int):
 class QueryShard:
     """Queries resident in HBM (both packed alphabets, names, lengths, mapping batches)."""
     n: int
-    q_base: int                 # index of the first query in the whole input
+    q_base: Optional[int]       # index of the first query in the whole input (None: pending, Pipeline.shard_base)
     lengths: np.ndarray         # int64 per query
     starts: np.ndarray          # int64 pool offset per query
     mash: PackedPool
@@ -198,6 +200,7 @@ class QueryShard:
     names_host: Optional[List[str]] = None   # SeqSet input: names on the host
     fasta: Optional[FastaIndex] = None       # FASTA input: the record table the shard was cut from
     fasta_r0: int = 0                        # index in `fasta` of the shard's first record
+    byte_sharded: bool = False               # a rank's byte range of a multi-rank run (Pipeline.ingest)
 
     @property
     def total_bases(self) -> int:

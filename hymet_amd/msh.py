@@ -98,7 +98,14 @@ class SketchDB:
         return len(self.names)
 
     def ref_hashes(self, i):
-        return self.hashes[self.offsets[i]:self.offsets[i + 1]]
+        a, b = int(self.offsets[i]), int(self.offsets[i + 1])
+        sl = getattr(self, "dev_slice", None)
+        if sl is not None and b > a and (a < sl[0] or b > sl[1]):
+            # read_msh(shard=...): the host array holds this rank's slice only; the whole DB
+            # exists only in HBM after the ranks' all-gather
+            raise RuntimeError(f"SketchDB.ref_hashes({i}): hashes [{a}, {b}) lie outside this rank's "
+                               f"host slice [{sl[0]}, {sl[1]})")
+        return self.hashes[a:b]
 
 
 # ------------------------------------------------------------------ capnp reader
@@ -243,7 +250,8 @@ def read_msh(path, threads: int = 16, alloc=None, upload=None, shard=None, defer
     shard = (rank, world), with upload: only this rank's slice of c = ceil(n_hashes / world)
     hashes, [rank * c, (rank + 1) * c), is gathered and uploaded (hymet_msh_upload_range) into
     a device tensor of world * c entries, for Comm.allgather_slices_ to fill in the others;
-    db.dev_slice = (lo, hi, c), and db.hashes holds valid hashes only on [lo, hi).
+    db.dev_slice = (lo, hi, c), and db.hashes holds valid hashes only on [lo, hi) (ref_hashes
+    raises for a reference outside it).
     defer_meta (with upload): the file stays open and the names / comments are copied only by
     db.finish_meta() -- the caller runs it while the GPU builds the table; until then they
     are placeholders of the right length.

@@ -9,9 +9,10 @@
 
 Host work per run is the short text logic of selection and a few dozen library calls; no
 per-contig or per-line Python.  Multi-GPU: every rank takes a contiguous
-record range of the same FASTA (balanced by bases); the screen hit counts and the
-per-target PAF line counts are all-reduced; fixed-size LCA row records are all-gathered and
-rank 0 writes the TSV in the reference's query order.
+byte range of the same FASTA (ingest.shard_bytes); the DB hash slices are all-gathered, the
+screen hit counts (by canonical DB index) and the per-target PAF line counts all-reduced;
+fixed-size LCA row records and the name pools are all-gathered and rank 0 writes the TSV in
+the reference's query order.  One host thread issues collectives at a time (dist.Comm).
 """
 from __future__ import annotations
 
@@ -284,6 +285,33 @@ def emit_paf_bytes(gpu, ix: IndexSet, sh: QueryShard, acc: PafAcc, bufs) -> byte
     return _to_host(gpu, bufs, "paf_h", out, nb.value)
 
 
+def run_beside(loader, main):
+    """main() on this thread while loader() (or nothing, when None) runs on a second host
+    thread; the loader is joined before main's result is returned, and an exception of either
+    is re-raised here (main's first).  Pipeline.run's placement of the per-run input loads:
+    the loader may issue collectives (holding the communicator, Comm.owned); main may not --
+    the caller issues its collectives after this returns."""
+    if loader is None:
+        return main()
+    import threading
+    err = []
+
+    def body():
+        try:
+            loader()
+        except BaseException as e:  # noqa: BLE001 -- re-raised on the calling thread
+            err.append(e)
+    th = threading.Thread(target=body, name="hymet-inputs")
+    th.start()
+    try:
+        out = main()
+    finally:
+        th.join()
+    if err:
+        raise err[0]
+    return out
+
+
 class Pipeline:
     def __init__(self, gpu, dbs: Sequence[SketchDB], ref_lookup, taxonomy, hierarchy, cfg: Config = None, comm=None,
                  variant: int = cls.CAMI):
@@ -421,17 +449,19 @@ class Pipeline:
     def _join_slices(self, side):
         """The DBs' hash slices all-gathered on side's stream (behind this rank's DMAs), then
         the tables built there -- on the loader thread, overlapping the contigs' ingest (or,
-        with HYMET_DB_GATHER=main, on the calling thread after it).  The
-        all-gathers go over the communicator Comm keeps for the DB load alone (Comm.db_group),
-        so they cannot interleave with the main thread's collectives: every rank issues the
-        DB all-gathers in DB order on one communicator, the rest in run order on the other."""
+        with HYMET_DB_GATHER=main, on the calling thread after it).  The all-gathers go over
+        the communicator Comm keeps for the DB load alone (Comm.db_group), and this thread holds
+        the communicator (Comm.owned) until they have completed on the GPU: run() issues no
+        collective before it has joined the loader thread (ingest() defers its record-count
+        all-gather), so every rank's collectives form one sequence."""
         t0 = time.perf_counter()
-        with self.gpu.torch.cuda.stream(side.stream):
-            for i, db in enumerate(self.dbs):
-                if db.dev_slice is not None and db.dev_hashes is not None:
-                    self.comm.allgather_slices_(db.dev_hashes, db.dev_slice[2], key=i)
-        self.timings["msh_allgather_s"] = time.perf_counter() - t0
-        self._build_tables(side)
+        with self.comm.owned():
+            with self.gpu.torch.cuda.stream(side.stream):
+                for i, db in enumerate(self.dbs):
+                    if db.dev_slice is not None and db.dev_hashes is not None:
+                        self.comm.allgather_slices_(db.dev_hashes, db.dev_slice[2], key=i)
+            self.timings["msh_allgather_s"] = time.perf_counter() - t0
+            self._build_tables(side)          # ends in side.stream.synchronize(): the gathers are done
 
     def _load_classifier(self, side=None):
         """C1-C2: detailed_taxonomy.tsv and taxonomy_hierarchy.tsv.  classification_cami.py
@@ -471,9 +501,11 @@ class Pipeline:
         return self.comm.rank if self.comm is not None else 0
 
     # ------------------------------------------------------------------ stages
-    def ingest(self, queries) -> QueryShard:
+    def ingest(self, queries, defer_base: bool = False) -> QueryShard:
         """FASTA bytes / FastaIndex (this rank's contiguous record range) or a SeqSet (one
-        rank) -> QueryShard resident in HBM."""
+        rank) -> QueryShard resident in HBM.  defer_base (run(), while the loader thread may
+        hold the communicator): a byte-range shard's first query index is left pending
+        (q_base None) for shard_base() to all-gather once the loader has been joined."""
         if isinstance(queries, QueryShard):
             return queries
         d_all = None
@@ -484,11 +516,16 @@ class Pipeline:
                 # record counts give its first query's index in the whole input
                 b0, b1 = shard_bytes(data, self.rank, self.world)
                 d_rng, fx = self._upload_while(data, b0, b1, lambda: FastaIndex(data, byte_range=(b0, b1)))
-                counts = self.comm.allgather_np(np.array([fx.n], np.int64), tag="shard_records")
-                q_base = int(sum(int(c[0]) for c in counts[:self.rank]))
-                sh = QueryShard.from_fasta(self.gpu, fx, 0, fx.n, self.cfg.map_batch_bases, q_base=q_base,
+                sh = QueryShard.from_fasta(self.gpu, fx, 0, fx.n, self.cfg.map_batch_bases, q_base=0,
                                            d_all=d_rng, d_base=b0)
                 sh.fasta, sh.fasta_r0 = fx, 0
+                # every rank of a byte-sharded run takes this branch, whatever its range holds
+                # (one rank may get the whole file, another nothing): the name-pool gather of
+                # _global_names keys on this flag, never on the range, so all ranks join it
+                sh.byte_sharded = True
+                sh.q_base = None
+                if not defer_base:
+                    self.shard_base(sh)
                 return sh
             if len(data):
                 # one rank takes every record: the bytes go up while the record table is scanned
@@ -508,6 +545,14 @@ class Pipeline:
         raise TypeError(f"unsupported query input {type(queries)!r}")
 
     prepare = ingest
+
+    def shard_base(self, sh: QueryShard) -> int:
+        """A byte-range shard's first query index in the whole input: the ranks' record counts
+        all-gathered (a collective; every rank of a byte-sharded run calls it once)."""
+        if sh.q_base is None:
+            counts = self.comm.allgather_np(np.array([sh.n], np.int64), tag="shard_records")
+            sh.q_base = int(sum(int(c[0]) for c in counts[:self.rank]))
+        return sh.q_base
 
     def _upload_while(self, data: bytes, b0: int, b1: int, scan):
         """Bytes [b0, b1) of data uploaded to HBM on a second thread (the library's staged,
@@ -690,22 +735,8 @@ class Pipeline:
     def run(self, queries, with_paf=False) -> RunResult:
         """queries: FASTA bytes, a FastaIndex, a SeqSet, or a QueryShard already resident.
         Rank 0's RunResult.tsv is the whole classified_sequences.tsv."""
-        reader, err = None, []
         side = self.map_gpus[0] if self.map_gpus else None
-        if self.cfg.reload_inputs and self._ran:
-            # the input loads (.msh parse into pinned memory and, with a mapping context to
-            # spare, the HBM tables on its stream; taxonomy tables) overlap the contigs' ingest
-            import threading
-
-            def read():
-                t0 = time.perf_counter()
-                try:
-                    self._read_inputs(side)
-                except BaseException as e:  # noqa: BLE001 -- re-raised on the calling thread
-                    err.append(e)
-                self.timings["reader_s"] = time.perf_counter() - t0
-            reader = threading.Thread(target=read, name="hymet-inputs")
-            reader.start()
+        reader = self.cfg.reload_inputs and self._ran
         self._ran = True
         ph = self.phases = {}   # host wall seconds of the run's phases (bench.py --emulate-rank)
         tp = [time.perf_counter()]
@@ -714,18 +745,28 @@ class Pipeline:
             t = time.perf_counter()
             ph[name] = ph.get(name, 0.0) + t - tp[0]
             tp[0] = t
-        try:
-            sh = self.ingest(queries)
+
+        def read():
+            t0 = time.perf_counter()
+            try:
+                self._read_inputs(side)
+            finally:
+                self.timings["reader_s"] = time.perf_counter() - t0
+
+        def ingest():
+            sh_ = self.ingest(queries, defer_base=True)
             lap("ingest_s")
-        finally:
-            if reader is not None:
-                reader.join()
-        if err:
-            raise err[0]
+            return sh_
+        # the input loads (.msh parse into pinned memory and, with a mapping context to spare,
+        # the DB all-gathers and HBM tables on its stream; taxonomy tables) overlap the
+        # contigs' ingest, which issues no collective meanwhile
+        sh = run_beside(read if reader else None, ingest)
         lap("input_wait_s")                   # the loader thread's remainder after the ingest
-        if reader is not None and self.db_paths and side is None:
+        if getattr(sh, "byte_sharded", False):
+            self.shard_base(sh)               # the record-count all-gather, now that the loader is done
+        if reader and self.db_paths and side is None:
             self._build_tables()
-        elif reader is not None and side is not None and not self.tables and self._sliced():
+        elif reader and side is not None and not self.tables and self._sliced():
             self._join_slices(side)           # HYMET_DB_GATHER=main
             lap("db_join_s")
         selected, rows, thr = self.screen_select(sh.mash)
@@ -767,7 +808,7 @@ class Pipeline:
         ranks' pools gathered (a byte-range shard indexes only its own records), or the
         whole-file record table's names.  A collective: every rank calls it."""
         fx = sh.fasta
-        if fx is not None and fx.byte_range != (0, len(fx.data)):
+        if getattr(sh, "byte_sharded", False):
             return self.comm.gather_name_pools(sh.qname, sh.qname_off, sh.n)
         if self._bufs.get("names_of") is not fx:
             torch = self.gpu.torch

@@ -202,3 +202,96 @@ def test_partition_and_shard_range():
     assert max(loads) - min(loads) <= max(lengths)
     spans = [Comm(r, 3).shard_range(10) for r in range(3)]
     assert spans == [(0, 3), (3, 6), (6, 10)]
+
+
+# ------------------------------------------------- loader-thread placement of the DB load
+def _loader_placement_fn(comm):
+    """Pipeline.run's placement, with CPU tensors: the loader thread (pipeline.run_beside)
+    holds the communicator (Comm.owned) and all-gathers two DBs' hash slices in place --
+    Comm.allgather_slices_'s un-staged branch, all_gather_into_tensor on db_group, the RCCL
+    path's call -- while the calling thread ingests; a collective the calling thread tries
+    meanwhile is refused before it reaches the backend; after the join the calling thread runs
+    the deferred record-count all-gather (Pipeline.shard_base's tag) on the default group."""
+    import threading
+    import time
+    import torch
+    from hymet_amd.pipeline import run_beside
+    sizes = (1001, 64)                       # hashes per DB: ragged last slice, and c * world == H
+    held, tried = threading.Event(), threading.Event()
+    refused = []
+
+    def loader():
+        with comm.owned():
+            held.set()
+            tried.wait(60)
+            out = []
+            for d, h in enumerate(sizes):
+                c = -(-h // comm.world)
+                t = torch.full((comm.world * c,), -1, dtype=torch.int64)
+                lo, hi = comm.rank * c, min(h, (comm.rank + 1) * c)
+                t[lo:hi] = torch.arange(lo, hi, dtype=torch.int64) * 7 + d
+                comm.allgather_slices_(t, c, key=d)
+                out.append(t[:h].clone())
+            time.sleep(0.2)                  # stands in for the table build behind the gathers
+        return out
+
+    got = []
+
+    def ingest():
+        held.wait(60)
+        try:
+            comm.allgather_np(np.array([1], np.int64), tag="shard_records")
+        except RuntimeError as e:
+            refused.append(str(e))
+        tried.set()
+        return 100 + comm.rank               # this rank's record count
+
+    n = run_beside(lambda: got.extend(loader()), ingest)
+    counts = comm.allgather_np(np.array([n], np.int64), tag="shard_records")
+    q_base = int(sum(int(c[0]) for c in counts[:comm.rank]))
+    return [g.numpy() for g in got], refused, q_base
+
+
+def test_loader_thread_allgather_slices_and_deferred_record_counts():
+    res = _run_ranks("_loader_placement_fn")
+    for r in (0, 1):
+        got, refused, q_base = res[r]
+        for d, h in enumerate((1001, 64)):
+            np.testing.assert_array_equal(got[d], np.arange(h, dtype=np.int64) * 7 + d)
+        assert len(refused) == 1 and "holds the communicator" in refused[0]
+        assert q_base == (0 if r == 0 else 100)
+
+
+def test_comm_owner_guard_single_process():
+    """The guard refuses another thread's collective while one thread holds the communicator,
+    and lets the holder's own (and everyone's after release) through -- checked before any
+    backend call, with a stand-in backend."""
+    import threading
+    from hymet_amd.dist import Comm
+
+    class FakeDist:
+        calls = 0
+
+        def barrier(self):
+            FakeDist.calls += 1
+    c = Comm(0, 2)
+    c.dist = FakeDist()
+    errs = []
+
+    def other():
+        try:
+            c.barrier()
+        except RuntimeError as e:
+            errs.append(e)
+    with c.owned():
+        c.barrier()                          # the holder's own
+        th = threading.Thread(target=other)
+        th.start()
+        th.join()
+        with c.owned():                      # re-entrant on the holding thread
+            c.barrier()
+    c.barrier()
+    th = threading.Thread(target=other)
+    th.start()
+    th.join()
+    assert len(errs) == 1 and FakeDist.calls == 4

@@ -61,3 +61,20 @@ def test_writer_round_trip_native(tmp_path):
     got = msh.read_msh(tmp_path / "w.msh")
     assert got.names == db.names and got.comments == db.comments
     assert (got.offsets == db.offsets).all() and (got.hashes == db.hashes).all() and (got.lengths == db.lengths).all()
+
+
+def test_sliced_host_hashes_fail_loudly():
+    """read_msh(shard=...) leaves only this rank's slice valid in the host array; reading a
+    reference outside it raises instead of returning stale pinned memory."""
+    import numpy as np
+    import pytest
+    from hymet_amd.msh import SketchDB
+    db = SketchDB(names=["a", "b", "c"], comments=["", "", ""], lengths=np.ones(3, np.int64),
+                  offsets=np.array([0, 4, 8, 12], np.int64), hashes=np.arange(12, dtype=np.uint64))
+    db.dev_slice = (4, 8, 4)                    # rank 1 of 3: hashes [4, 8)
+    assert db.ref_hashes(1).tolist() == [4, 5, 6, 7]
+    for i in (0, 2):
+        with pytest.raises(RuntimeError, match="outside this rank's host slice"):
+            db.ref_hashes(i)
+    db.dev_slice = None
+    assert db.ref_hashes(2).tolist() == [8, 9, 10, 11]

@@ -204,21 +204,45 @@ def _w2_setup(gpu):
     return w, db, by_name
 
 
+def _world2_input(w, shape):
+    """FASTA bytes for the world-2 test.  halves: the 60 contigs (the byte cut lands mid-file,
+    both ranks get records).  one_record: a single contig (rank 0's byte range is the whole
+    file, rank 1's is empty).  big_last: the contigs and then one record longer than all of
+    them together -- two candidate genomes joined -- so the cut at len/2 falls inside it and
+    rank 0 again takes every record.  The last two are the shapes where a rank-local test of
+    the byte range would send the ranks down different collective paths."""
+    if shape == "halves":
+        return _fasta_text(w, quote_name=False)
+    if shape == "one_record":
+        i = int(np.argmax([len(s) for s in w.contigs]))
+        return b">" + w.contig_names[i].encode() + b" len=" + str(len(w.contigs[i])).encode() + b"\n" + w.contigs[i] + b"\n"
+    if shape == "big_last":
+        big = w.refs[0] + w.refs[1]
+        assert len(big) > sum(len(s) for s in w.contigs)
+        return _fasta_text(w, quote_name=False) + b">chimera_0_1\n" + big + b"\n"
+    raise ValueError(shape)
+
+
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("db_gather", ["loader", "main"])
-def test_world2_pipeline_equals_world1(gpu, tmp_path, db_gather):
+@pytest.mark.parametrize("db_gather,shape", [("loader", "halves"), ("main", "halves"), ("loader", "one_record"),
+                                             ("loader", "big_last")])
+def test_world2_pipeline_equals_world1(gpu, tmp_path, db_gather, shape):
     """Two ranks (two processes on this GPU, gloo staging the collectives through the host):
-    each takes a contiguous half of the same FASTA; rank 0's TSV equals the one-rank TSV and
+    each takes its byte range of the same FASTA; rank 0's TSV equals the one-rank TSV and
     the ranks' PAF texts concatenate to the one-rank PAF (one index part).  The ranks read the
     DB from its .msh path on every run; the second run loads it as per-rank hash slices
-    all-gathered between the ranks, and must give the same bytes."""
+    all-gathered between the ranks (the loader thread holding the communicator), and must give
+    the same bytes.  One-record and big-last-record inputs leave rank 1 with no records."""
     from hymet_amd.msh import write_msh
     import multiprocessing as mpc
     import socket
     from hymet_amd import pipeline
+    from hymet_amd.ingest import shard_bytes
     from hymet_amd.seqio import from_records
     w, db, by_name, tax, hier = _setup(gpu, tmp_path)
-    data = _fasta_text(w, quote_name=False)
+    data = _world2_input(w, shape)
+    if shape != "halves":
+        assert shard_bytes(data, 0, 2) == (0, len(data)) and shard_bytes(data, 1, 2) == (len(data), len(data))
     dp = tmp_path / "pool.fna"
     dp.write_bytes(data)
     mp_ = tmp_path / "sketch.msh"
@@ -248,6 +272,7 @@ def test_world2_pipeline_equals_world1(gpu, tmp_path, db_gather):
         assert r0[0] == one.tsv
         assert r1[0] == b""
         assert r0[1] + r1[1] == one.paf_bytes
+    assert one.n_queries >= 1
 
 
 def test_map_streams_one_and_two_identical(gpu, tmp_path):
