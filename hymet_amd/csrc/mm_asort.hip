@@ -60,16 +60,25 @@ __device__ __forceinline__ int seg_class_group(int64_t n) {
     return n <= kTile ? seg_class(n) : n <= 8192 ? kB8K : n <= 16384 ? kB16K : kLarge;
 }
 
-// the anchor set written for sorted position i: x, y (groups are read from x and the query
-// offsets, so the sorted key itself is not written)
+// the anchor set written for sorted position i: x, y (the sorted key itself is not written),
+// and the set's chaining-group heads: bit i of hb is set where the key above rpos -- (query,
+// strand, target) -- differs from position i-1's, so chain_set numbers the groups from this
+// bitmap instead of re-reading x (hb zeroed by grouped_anchor_sort; a word may straddle two
+// writers' segments, hence the atomic)
 struct AnchorOut {
     uint64_t *ax, *ay;
     int rb, pb;
     uint64_t yhi;
+    uint32_t *hb;
     __device__ __forceinline__ void put(int64_t i, uint64_t k, uint32_t y) const {
         const uint64_t rev = k >> (rb + pb) & 1, rid = k >> pb & ((1ull << rb) - 1), rpos = k & ((1ull << pb) - 1);
         ax[i] = rev << 63 | rid << 32 | rpos;
         ay[i] = yhi << 32 | y;
+    }
+    // k written at i, kp at i - 1 (first: i starts a writer's segment -- a query or a bin, a
+    // head either way)
+    __device__ __forceinline__ void head(int64_t i, uint64_t k, uint64_t kp, bool first) const {
+        if (first || (k >> pb) != (kp >> pb)) atomicOr(hb + (i >> 5), 1u << (i & 31));
     }
 };
 
@@ -366,7 +375,11 @@ __global__ __launch_bounds__(256) void group_class_kernel(const Seg *groups, int
     for (int j = 0; j < 4; j++) {
         const int64_t g = (int64_t)blockIdx.x * 1024 + j * 256 + threadIdx.x;
         sg[j] = g < G ? groups[g] : Seg{0, 0, 0};
-        if (sg[j].n == 1) out.put(sg[j].s, key[sg[j].s], val[sg[j].s]);
+        if (sg[j].n == 1) {
+            const uint64_t k = key[sg[j].s];
+            out.put(sg[j].s, k, val[sg[j].s]);
+            out.head(sg[j].s, k, k, true);
+        }
         cls[j] = sg[j].n > 1 ? seg_class_group(sg[j].n) : -1;
     }
     block_append<4>(sg, cls, lists, cap, cnt);
@@ -408,7 +421,10 @@ __global__ __launch_bounds__(256) void thread_seg_sort_kernel(const Seg *list, i
             }
 #pragma unroll
     for (int j = 0; j < 8; j++)
-        if (j < S.n) out.put(S.s + j, k[j], v[j]);
+        if (j < S.n) {
+            out.put(S.s + j, k[j], v[j]);
+            out.head(S.s + j, k[j], k[j > 0 ? j - 1 : 0], j == 0);
+        }
 }
 
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
@@ -438,7 +454,12 @@ __global__ __launch_bounds__(64) void wave_seg_sort_kernel(const Seg *list, cons
                 v = ov;
             }
         }
-    if (lane < S.n) out.put(S.s + lane, k, v);
+    const uint64_t kp = (uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(k >> 32), 1, 64) << 32 |
+                        (uint32_t)__shfl_up((int)(uint32_t)k, 1, 64);  // lane - 1's word
+    if (lane < S.n) {
+        out.put(S.s + lane, k, v);
+        out.head(S.s + lane, k, kp, lane == 0);
+    }
 }
 
 __device__ __forceinline__ int lds_ix(int e) { return e + (e >> 4); }  // one pad word per 16: blocked access without bank conflicts
@@ -532,8 +553,9 @@ __global__ __launch_bounds__(BLOCK) void block_seg_sort_kernel(const Seg *list, 
     for (int j = 0; j < ITEMS; j++) sm[lds_ix(tid * ITEMS + j)] = k[j];
     __syncthreads();
     for (int e = tid; e < S.n; e += BLOCK) {  // coalesced write
-        const uint64_t w = sm[lds_ix(e)];
+        const uint64_t w = sm[lds_ix(e)], wp = sm[lds_ix(e > 0 ? e - 1 : 0)];
         out.put(S.s + e, hi_bits | w >> ybits, (uint32_t)(w & ym));
+        out.head(S.s + e, hi_bits | w >> ybits, hi_bits | wp >> ybits, e == 0);
     }
 }
 
@@ -561,6 +583,7 @@ __global__ __launch_bounds__(256) void big_put_kernel(const Seg *list, const int
         const uint64_t k = tk[d + e];
         const bool prev_eq = e > 0 && tk[d + e - 1] == k;
         if (prev_eq) continue;
+        out.head(S.s + e, hi_bits | (k & pm), hi_bits | (tk[d + (e > 0 ? e - 1 : 0)] & pm), e == 0);
         int f = e;
         while (f + 1 < S.n && tk[d + f + 1] == k) f++;
         if (f == e) {
@@ -640,7 +663,7 @@ int sort_segments(hymet_ctx *ctx, const Seg *lists, int64_t cap, const int32_t *
 
 int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val, int64_t n, const int64_t *d_qoff, int n_q,
                         int rb, int pb, uint64_t yhi, int64_t max_qlen, uint64_t *okey, uint32_t *oval, uint64_t *ax,
-                        uint64_t *ay) {
+                        uint64_t *ay, uint32_t *hb) {
     // bins = (strand, target) -- or, for parts of more than 2047 targets, (strand, target >> cs):
     // coarse bins of 2^cs consecutive targets, sorted inside by (low target bits, rpos, y)
     const int cs = std::max(0, 1 + rb - 12);
@@ -649,7 +672,8 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     const int ybits = bits_of(max_qlen);
     if (n <= 0 || n_q <= 0 || 1 + rb + pb + ybits > 63) return 1;
     hipStream_t st = ctx->stream;
-    const AnchorOut out{ax, ay, rb, pb, yhi};
+    const AnchorOut out{ax, ay, rb, pb, yhi, hb};
+    HY_HIP(hipMemsetAsync(hb, 0, head_bits_bytes(n), st));
     // 1 queries by size
     DevBuf qlists, nt;
     HY_HIP(qlists.alloc(sizeof(Seg) * kClasses * (size_t)n_q, st));

@@ -153,9 +153,13 @@ int inclusive_max_scan_i32(hymet_ctx *ctx, const int32_t *in, int32_t *out, int6
 // Per-query grouped sort of anchor keys (mm_asort.hip): key/val (n, query-major, query offsets
 // d_qoff[n_q + 1]) into the sorted anchor set okey (k1) / ax / ay (oval: scratch).  Returns 1
 // with nothing written where it does not apply (the caller's device sort then runs).
+// hb: the set's group-head bitmap (head_bits_bytes(n); AnchorOut::head).
 int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val, int64_t n, const int64_t *d_qoff, int n_q,
                         int rb, int pb, uint64_t yhi, int64_t max_qlen, uint64_t *okey, uint32_t *oval, uint64_t *ax,
-                        uint64_t *ay);
+                        uint64_t *ay, uint32_t *hb);
+// bytes of an anchor set's group-head bitmap: one bit per anchor, in whole 64-bit words (the
+// group kernels read two words per thread)
+inline size_t head_bits_bytes(int64_t n) { return 8 * (size_t)((n + 63) / 64 + 1); }
 
 // Minimizers of a packed set of sequences: host-side chunk bookkeeping + both passes.
 // On success d_x / d_y hold *n_out minimizers in sequence order (sequence-major); if

@@ -490,32 +490,24 @@ __global__ void group_flag_x_kernel(const uint64_t *x, int64_t n, uint32_t *flag
     if (i < n) flag[i] = (i == 0 || (x[i] >> 32) != (x[i - 1] >> 32)) ? 1u : 0u;
 }
 
-// Groups of an anchor set sorted by (query, x, y) in two passes over tiles of 4096 anchors
-// (instead of flag, scan and start passes over per-anchor flags): a group starts at every
-// query's first anchor and wherever x >> 32 (strand, target) changes.  Pass 1 counts the
-// starts per tile; after a scan of the tile counts, pass 2 recomputes them and writes g_start
-// and every anchor's group id.  A tile's query starts come from the query offsets into an LDS
-// bitmap.
-constexpr int kGTile = 4096;
+// Groups of an anchor set sorted by (query, x, y): a group starts at every non-empty query's
+// first anchor and wherever x >> 32 (strand, target) changes.  The x changes come as a bitmap
+// from whoever wrote the set -- the grouped sort's writers (AnchorOut::head), the long join's
+// compaction, or head_bits_x_kernel for the other paths -- so numbering the groups reads one bit
+// per anchor instead of x twice: pass 1 counts the heads per tile of kGTile anchors (64 per
+// thread: two bitmap words), a scan of the tile counts, pass 2 writes g_start and each group's
+// query-first flag.  A tile's query starts come from the query offsets into an LDS bitmap.
+constexpr int kGTile = 16384;
 
-__device__ __forceinline__ void group_tile_heads(const uint64_t *x, int64_t n, const int64_t *qoff, int n_q, int64_t t0,
-                                                 uint32_t *qs, uint32_t *rc, bool (&h)[16]) {
+__device__ __forceinline__ uint64_t group_tile_bits(const uint32_t *hb, int64_t n, const int64_t *qoff, int n_q, int64_t t0,
+                                                    uint64_t *qs) {
     __shared__ int s_q0;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int tid = threadIdx.x;
     const int64_t t1 = min(t0 + kGTile, n);
-    // the (strand, target) words of the tile's anchors and of their predecessors, loaded before
-    // the query search at clamped positions (straight-line: 32 loads in flight per lane, where
-    // a load inside the head test's short-circuit was one round trip per row)
-    const uint32_t *xh = reinterpret_cast<const uint32_t *>(x) + 1;
-    uint32_t xv[16], xp[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const int64_t i = min(t0 + j * 256 + (int64_t)threadIdx.x, n - 1);
-        xv[j] = xh[2 * i];
-        xp[j] = xh[2 * max(i - 1, (int64_t)0)];
-    }
-    for (int k = threadIdx.x; k < kGTile / 32; k += 256) qs[k] = 0;
-    if (threadIdx.x == 0) {  // first query whose range ends after t0
+    const int64_t a0 = t0 + 64 * (int64_t)tid;
+    const uint64_t hw = a0 < n ? reinterpret_cast<const uint64_t *>(hb)[a0 >> 6] : 0;
+    qs[tid] = 0;
+    if (tid == 0) {  // first query whose range ends after t0
         int lo = 0, hi = n_q;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
@@ -525,73 +517,68 @@ __device__ __forceinline__ void group_tile_heads(const uint64_t *x, int64_t n, c
         s_q0 = lo;
     }
     __syncthreads();
-    for (int q = s_q0 + (int)threadIdx.x; q < n_q; q += 256) {
+    for (int q = s_q0 + tid; q < n_q; q += 256) {
         const int64_t a = qoff[q];
         if (a >= t1) break;
-        if (a >= t0 && a < qoff[q + 1]) atomicOr(&qs[(a - t0) >> 5], 1u << ((a - t0) & 31));
+        if (a >= t0 && a < qoff[q + 1]) atomicOr((unsigned long long *)&qs[(a - t0) >> 6], 1ull << ((a - t0) & 63));
     }
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const int64_t i = t0 + j * 256 + threadIdx.x;
-        const int64_t l = i - t0;
-        h[j] = i < n && (i == 0 || (qs[l >> 5] >> (l & 31) & 1) || xv[j] != xp[j]);
-        const uint64_t b = __ballot(h[j]);
-        if (lane == 0) rc[j * 4 + w] = (uint32_t)__popcll(b);
-    }
-    __syncthreads();
+    const int64_t m = n - a0;  // anchors of this thread's 64 that exist
+    const uint64_t live = m >= 64 ? ~0ull : m > 0 ? (1ull << m) - 1 : 0ull;
+    return (hw | qs[tid]) & live;
 }
 
-__global__ __launch_bounds__(256) void group_count_kernel(const uint64_t *x, int64_t n, const int64_t *qoff, int n_q,
+__global__ __launch_bounds__(256) void group_count_kernel(const uint32_t *hb, int64_t n, const int64_t *qoff, int n_q,
                                                           uint32_t *tile_cnt) {
-    __shared__ uint32_t qs[kGTile / 32], rc[64];
-    bool h[16];
-    group_tile_heads(x, n, qoff, n_q, (int64_t)blockIdx.x * kGTile, qs, rc, h);
-    if (threadIdx.x < 64) {
-        uint32_t v = rc[threadIdx.x];
-        for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
-        if (threadIdx.x == 0) tile_cnt[blockIdx.x] = v;
-    }
+    __shared__ uint64_t qs[kGTile / 64];
+    __shared__ uint32_t ws[4];
+    const uint64_t h = group_tile_bits(hb, n, qoff, n_q, (int64_t)blockIdx.x * kGTile, qs);
+    uint32_t c = (uint32_t)__popcll(h);
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// also: t[i] = 0 for every anchor (the backtrack's initial marks; the chaining kernels'
-// overflow path stamps iterations as i + 1) and the g_start[G] = n sentinel
-// (g_start and each group's query-first flag -- lchain.c's krmq index-0 quirk -- at its head;
-// t zeroed for the chaining and backtrack kernels)
-__global__ __launch_bounds__(256) void group_write_kernel(const uint64_t *x, int64_t n, const int64_t *qoff, int n_q,
+// g_start of every group, its query-first flag (lchain.c's krmq index-0 quirk) and the
+// g_start[G] = n sentinel
+__global__ __launch_bounds__(256) void group_write_kernel(const uint32_t *hb, int64_t n, const int64_t *qoff, int n_q,
                                                           const int64_t *tile_off, int64_t *g_start, uint8_t *qfirst,
-                                                          int32_t *t, int64_t G) {
-    __shared__ uint32_t qs[kGTile / 32], rc[64];
-    bool h[16];
+                                                          int64_t G) {
+    __shared__ uint64_t qs[kGTile / 64];
+    __shared__ uint32_t ws[4];
     const int64_t t0 = (int64_t)blockIdx.x * kGTile;
-    group_tile_heads(x, n, qoff, n_q, t0, qs, rc, h);
+    uint64_t h = group_tile_bits(hb, n, qoff, n_q, t0, qs);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (w == 0) {  // exclusive scan of the 64 (row, wave) counts in anchor order
-        const uint32_t v = rc[lane];
-        uint32_t inc = v;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
-            if (lane >= d) inc += o;
-        }
-        rc[lane] = inc - v;
+    const uint32_t c = (uint32_t)__popcll(h);
+    uint32_t inc = c;  // exclusive scan of the threads' counts in anchor order
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+        if (lane >= d) inc += o;
     }
+    if (lane == 63) ws[w] = inc;
     __syncthreads();
-    const int64_t base = tile_off[blockIdx.x];
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const int64_t i = t0 + j * 256 + threadIdx.x;
-        const uint64_t b = __ballot(h[j]);
-        const int64_t g = base + rc[j * 4 + w] + __popcll(b & ((2ull << lane) - 1)) - 1;  // inclusive - 1
-        if (i < n) {
-            t[i] = 0;
-            if (h[j]) {
-                const int64_t l = i - t0;
-                g_start[g] = i;
-                qfirst[g] = (uint8_t)(qs[l >> 5] >> (l & 31) & 1);
-            }
-        }
+    int64_t g = tile_off[blockIdx.x] + inc - c;
+    for (int k = 0; k < w; k++) g += ws[k];
+    const uint64_t qw = qs[threadIdx.x];
+    const int64_t a0 = t0 + 64 * (int64_t)threadIdx.x;
+    while (h) {
+        const int b = __ffsll((unsigned long long)h) - 1;
+        h &= h - 1;
+        g_start[g] = a0 + b;
+        qfirst[g] = (uint8_t)(qw >> b & 1);
+        ++g;
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) g_start[G] = n;
+}
+
+// the head bitmap of an anchor set written without one (the two-key and re-sort paths):
+// x >> 32 differs from the previous anchor's, a wave's 64 anchors per 64-bit word
+__global__ __launch_bounds__(256) void head_bits_x_kernel(const uint64_t *x, int64_t n, uint64_t *hb) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool hd = i < n && (i == 0 || (x[i] >> 32) != (x[i - 1] >> 32));
+    const uint64_t b = __ballot(hd);
+    if ((threadIdx.x & 63) == 0 && i < n) hb[i >> 6] = b;
 }
 
 __global__ void group_start_kernel(const uint32_t *flag, const int64_t *gpos, int64_t n, int64_t *g_start, int32_t *gid) {
@@ -617,12 +604,14 @@ __global__ void max_group_kernel(const int64_t *g_start, const int32_t *order, i
     *out = best;
 }
 
-__global__ void nonwork_fp_kernel(const int64_t *g_start, int32_t G, int min_cnt, int32_t *f, int64_t *p) {
+// groups of fewer than min_cnt anchors: f = 0, p = -1, t = 0 (the chaining kernels write all
+// three for the anchors of every work group, so t needs no pass over the set)
+__global__ void nonwork_fp_kernel(const int64_t *g_start, int32_t G, int min_cnt, int32_t *f, int64_t *p, int32_t *t) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
     const int64_t a0 = g_start[g], a1 = g_start[g + 1];
     if (a1 - a0 >= min_cnt) return;
-    for (int64_t a = a0; a < a1; a++) f[a] = 0, p[a] = -1;
+    for (int64_t a = a0; a < a1; a++) f[a] = 0, p[a] = -1, t[a] = 0;
 }
 
 // also clears the per-group query-first flags and the z-order list counters
@@ -1083,26 +1072,43 @@ __device__ __forceinline__ uint32_t keep_bits16(const int32_t *t, int64_t n, con
     return bits;
 }
 
+// (also each tile's last kept anchor, or -1: the compaction's group heads compare a tile's
+// first kept anchor with the one before it)
 __global__ __launch_bounds__(256) void mark_count_kernel(const int32_t *t, int64_t n, const uint32_t *qflag,
-                                                         const int64_t *qoff, int n_q, uint32_t *cnt) {
+                                                         const int64_t *qoff, int n_q, uint32_t *cnt, int64_t *last_kept) {
     __shared__ uint32_t ws[4];
+    __shared__ int64_t wl[4];
     const int64_t e0 = (int64_t)blockIdx.x * 4096 + threadIdx.x * 16;
-    uint32_t c = __popc(keep_bits16(t, n, qflag, qoff, n_q, e0));
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor((int)c, o, 64);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    const uint32_t kb = keep_bits16(t, n, qflag, qoff, n_q, e0);
+    uint32_t c = __popc(kb);
+    long long l = kb ? e0 + 31 - __clz((int)kb) : -1;
+    for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_xor((int)c, o, 64);
+        l = max(l, __shfl_xor(l, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c, wl[threadIdx.x >> 6] = l;
     __syncthreads();
-    if (threadIdx.x == 0) cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+    if (threadIdx.x == 0) {
+        cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+        last_kept[blockIdx.x] = max(max(wl[0], wl[1]), max(wl[2], wl[3]));
+    }
 }
 
 // stable compaction of the kept anchors (x, y): the first-pass set is sorted by (query, x,
 // y), so its kept subsequence is the long join's sorted anchor set -- no re-sort.  The keep
 // bits are decided per 16 consecutive anchors (as in the count) into LDS; rows of 256
 // anchors are then written lanes striped (coalesced), positions by ballot counts.
+// The output's group heads (x >> 32 differs from the previous kept anchor's) go into its
+// bitmap ohb (zeroed): the previous kept anchor is a lower lane of the same 64-anchor chunk
+// (shuffle), else the last kept one of an earlier chunk of the tile (LDS), else the last kept
+// anchor of an earlier tile (last_kept, from the count).
 __global__ __launch_bounds__(256) void mark_compact_kernel(const int32_t *t, int64_t n, const uint32_t *qflag,
                                                            const int64_t *qoff, int n_q, const int64_t *tile_off,
-                                                           const uint64_t *ax, const uint64_t *ay, uint64_t *ox,
-                                                           uint64_t *oy) {
+                                                           const int64_t *last_kept, const uint64_t *ax, const uint64_t *ay,
+                                                           uint64_t *ox, uint64_t *oy, uint32_t *ohb) {
     __shared__ uint32_t rc[64];       // kept per (row, wave), row-major
+    __shared__ uint32_t nk[64];       // the same counts (rc becomes their exclusive scan)
+    __shared__ uint32_t lx[64];       // x >> 32 of each (row, wave) chunk's last kept anchor
     __shared__ uint16_t kb[256];      // keep bits of anchors [16 l, 16 l + 16) of the tile
     const int64_t t0 = (int64_t)blockIdx.x * 4096;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1118,6 +1124,7 @@ __global__ __launch_bounds__(256) void mark_compact_kernel(const int32_t *t, int
     }
     __syncthreads();
     uint32_t v = 0, inc = 0;
+    if (w == 0) nk[lane] = rc[lane];
     if (w == 0) {  // wave 0: exclusive scan of the 64 counts in element order
         v = rc[lane];
         inc = v;
@@ -1130,14 +1137,47 @@ __global__ __launch_bounds__(256) void mark_compact_kernel(const int32_t *t, int
     if (w == 0) rc[lane] = inc - v;
     __syncthreads();
     const int64_t base = tile_off[blockIdx.x];
+    uint32_t xh[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
         const uint64_t b = __ballot(m[j]);
+        xh[j] = 0;
         if (m[j]) {
             const int64_t e = t0 + j * 256 + threadIdx.x;
             const int64_t o = base + rc[j * 4 + w] + __popcll(b & ((1ull << lane) - 1));
-            ox[o] = ax[e];
+            const uint64_t xv = ax[e];
+            xh[j] = (uint32_t)(xv >> 32);
+            ox[o] = xv;
             oy[o] = ay[e];
+        }
+        if (b && lane == 63 - __clzll((long long)b)) lx[j * 4 + w] = xh[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint64_t b = __ballot(m[j]);
+        const uint64_t below = b & ((1ull << lane) - 1);
+        const int src = below ? 63 - __clzll((long long)below) : lane;
+        const uint32_t xp = (uint32_t)__shfl((int)xh[j], src, 64);
+        if (m[j]) {
+            bool hd;
+            if (below) {
+                hd = xp != xh[j];
+            } else {  // the chunk's first kept anchor
+                int c = j * 4 + w - 1;
+                while (c >= 0 && nk[c] == 0) --c;
+                if (c >= 0) {
+                    hd = lx[c] != xh[j];
+                } else {  // the tile's first: the last kept anchor of an earlier tile
+                    int64_t tt = (int64_t)blockIdx.x - 1;
+                    while (tt >= 0 && last_kept[tt] < 0) --tt;
+                    hd = tt < 0 || (uint32_t)(ax[last_kept[tt]] >> 32) != xh[j];
+                }
+            }
+            if (hd) {
+                const int64_t o = base + rc[j * 4 + w] + __popcll(below);
+                atomicOr(ohb + (o >> 5), 1u << (o & 31));
+            }
         }
     }
 }
@@ -1214,6 +1254,8 @@ struct AnchorSet {
     DevBuf ax, ay;
     int64_t n = 0;
     DevBuf d_off;
+    DevBuf hb;            // group-head bitmap (head_bits_bytes(n)): bit i where x >> 32 changes
+    bool has_hb = false;  // hb written by whoever built the set; else chain_set derives it from x
 };
 
 // Chains of an anchor set: compacted anchors (chain by chain, chains ordered by first
@@ -1284,9 +1326,13 @@ static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n,
         return !(e && e[0] == '0');
     }();
     if (gsort) {
+        HY_HIP(out.hb.alloc(head_bits_bytes(n), ctx->stream));
         const int rc = grouped_anchor_sort(ctx, kk, vv, n, d_qoff, n_q, rb, pb, (uint64_t)yhi, max_qlen, kka, vva,
-                                           out.ax.as<uint64_t>(), out.ay.as<uint64_t>());
-        if (rc == HYMET_OK) return HYMET_OK;
+                                           out.ax.as<uint64_t>(), out.ay.as<uint64_t>(), out.hb.as<uint32_t>());
+        if (rc == HYMET_OK) {
+            out.has_hb = true;
+            return HYMET_OK;
+        }
         if (rc != 1) return rc;
     }
     int rc = sort_pairs<uint64_t, uint32_t>(ctx, kk, kka, vv, vva, n, 0, end_bit, "radix_sort_anchors");
@@ -1310,12 +1356,18 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(hipMemsetAsync(C.d_qb.p, 0, 8 * (size_t)(n_q + 1), ctx->stream));
         return HYMET_OK;
     }
-    // groups: (query, strand, target) runs, by tiles (count, scan of the tile counts, write)
+    // groups: (query, strand, target) runs, from the set's head bitmap by tiles (count, scan of
+    // the tile counts, write)
+    if (!A.has_hb) {
+        HY_HIP(A.hb.alloc(head_bits_bytes(n), ctx->stream));
+        LAUNCH1(head_bits_x_kernel, n, A.ax.as<uint64_t>(), n, A.hb.as<uint64_t>());
+        A.has_hb = true;
+    }
     DevBuf tcnt, toff;
     const int64_t ntile = cdiv(n, kGTile);
     HY_HIP(tcnt.alloc(4 * (size_t)(ntile + 1), ctx->stream));
     HY_HIP(toff.alloc(8 * (size_t)(ntile + 1), ctx->stream));
-    hipLaunchKernelGGL(group_count_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.ax.as<uint64_t>(), n,
+    hipLaunchKernelGGL(group_count_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.hb.as<uint32_t>(), n,
                        A.d_off.as<int64_t>(), n_q, tcnt.as<uint32_t>());
     HY_CHECK_LAUNCH("group_count_kernel");
     int64_t G = 0;
@@ -1324,10 +1376,9 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
     DevBuf g_start, t, qfirst;
     HY_HIP(g_start.alloc(8 * (size_t)(G + 1), ctx->stream));
     HY_HIP(qfirst.alloc((size_t)G, ctx->stream));
-    HY_HIP(t.alloc(4 * (size_t)n, ctx->stream));
-    hipLaunchKernelGGL(group_write_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.ax.as<uint64_t>(), n,
-                       A.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
-                       t.as<int32_t>(), G);
+    HY_HIP(t.alloc(4 * (size_t)n, ctx->stream));  // zeroed by the chaining kernels (and nonwork_fp_kernel) as they go
+    hipLaunchKernelGGL(group_write_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.hb.as<uint32_t>(), n,
+                       A.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(), G);
     HY_CHECK_LAUNCH("group_write_kernel");
     // work list: groups with >= min_cnt anchors, biggest first
     DevBuf skey, sidx, swork, skey2, sidx2, zlists;
@@ -1360,9 +1411,11 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         DevBuf f, p;
         HY_HIP(f.alloc(4 * (size_t)n, ctx->stream));
         HY_HIP(p.alloc(8 * (size_t)n, ctx->stream));
-        // the chaining kernels write f/p of every anchor of a work group; the rest (groups of
-        // fewer than min_cnt anchors) get f = 0, p = -1 here instead of memsets of all n
-        LAUNCH1(nonwork_fp_kernel, G, g_start.as<int64_t>(), (int32_t)G, opt->min_cnt, f.as<int32_t>(), p.as<int64_t>());
+        // the chaining kernels write f/p (and t = 0) of every anchor of a work group; the rest
+        // (groups of fewer than min_cnt anchors) get f = 0, p = -1, t = 0 here instead of
+        // memsets of all n
+        LAUNCH1(nonwork_fp_kernel, G, g_start.as<int64_t>(), (int32_t)G, opt->min_cnt, f.as<int32_t>(), p.as<int64_t>(),
+                t.as<int32_t>());
         rc = launch_chain(ctx, A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
                           (const int32_t *)vp,
                           (int32_t)n_work, f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(), opt->max_gap,
@@ -2063,11 +2116,12 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                 // the first-pass set in its (key, y) order -- already the long join's sorted set
                 const int64_t n1 = S1.n, nt = cdiv(n1, 4096);
                 DevBuf &mark = lj.mark;
-                DevBuf tcnt, toff;
+                DevBuf tcnt, toff, tlast;
                 HY_HIP(tcnt.alloc(4 * (size_t)(nt + 1), st));
                 HY_HIP(toff.alloc(8 * (size_t)(nt + 1), st));
+                HY_HIP(tlast.alloc(8 * (size_t)(nt + 1), st));
                 hipLaunchKernelGGL(mark_count_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<int32_t>(), n1,
-                                   flag.as<uint32_t>(), S1.d_off.as<int64_t>(), n_q, tcnt.as<uint32_t>());
+                                   flag.as<uint32_t>(), S1.d_off.as<int64_t>(), n_q, tcnt.as<uint32_t>(), tlast.as<int64_t>());
                 HY_CHECK_LAUNCH("mark_count_kernel");
                 int64_t got = 0;
                 rc = exclusive_scan_u32_i64(ctx, tcnt.as<uint32_t>(), toff.as<int64_t>(), nt, &got);
@@ -2097,11 +2151,15 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                 }
                 HY_HIP(S2.ax.alloc(8 * (size_t)(A2 + 1), st));
                 HY_HIP(S2.ay.alloc(8 * (size_t)(A2 + 1), st));
+                HY_HIP(S2.hb.alloc(head_bits_bytes(A2), st));
+                HY_HIP(hipMemsetAsync(S2.hb.p, 0, head_bits_bytes(A2), st));
                 hipLaunchKernelGGL(mark_compact_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<int32_t>(), n1,
-                                   flag.as<uint32_t>(), S1.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), S1.ax.as<uint64_t>(),
-                                   S1.ay.as<uint64_t>(), S2.ax.as<uint64_t>(), S2.ay.as<uint64_t>());
+                                   flag.as<uint32_t>(), S1.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), tlast.as<int64_t>(),
+                                   S1.ax.as<uint64_t>(), S1.ay.as<uint64_t>(), S2.ax.as<uint64_t>(), S2.ay.as<uint64_t>(),
+                                   S2.hb.as<uint32_t>());
                 HY_CHECK_LAUNCH("mark_compact_kernel");
                 S2.n = A2;
+                S2.has_hb = true;
                 rc = dump_anchors(getenv("HYMET_DUMP_ANCHORS2"), S2, dumped2);
                 if (rc) return rc;
             } else if (key_path) {

@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 6: chaining work-prefetch A/B on the C4 dump + one-stream kernel trace of the bench
+set -eo pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+NOTEST=1 LONG=1 AB_OUT=r6_ab1 bash tools/chain_ab.sh chain_prof chain_prof_wpf0 chain_prof_gt chain_prof_gt0
+OUT=gpurun_out/r6_ab1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace1 -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu --map-streams 1 > $OUT/trace1_bench.json 2> $OUT/trace1_bench.err
+python3 tools/lastrun.py $OUT/trace1 60 > $OUT/onestream_laststep.txt
+find $OUT -name '*.csv' -size +20M -delete
