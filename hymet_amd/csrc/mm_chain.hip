@@ -146,13 +146,6 @@ namespace {
 #ifndef HYMET_CHAIN_UNI
 #define HYMET_CHAIN_UNI 1
 #endif
-// Work items fetched one group ahead: while a wave chains a group, the next item's record (group
-// start, size, query-first flag, in one 16-byte word per work-list position) is already loading
-// and the grab of the one after is in flight -- instead of an atomic, the list entry and the
-// group bounds as dependent round trips between every two groups.
-#ifndef HYMET_CHAIN_WPF
-#define HYMET_CHAIN_WPF 1
-#endif
 #ifndef HYMET_CHAIN_WPE  // waves per SIMD the register allocation targets (0: compiler's choice)
 #define HYMET_CHAIN_WPE 4
 #endif
@@ -248,7 +241,6 @@ struct ChainParams {
     int max_dist, max_dist_inner, bw, max_chn_skip, cap_rmq_size;
     float pen_gap, pen_skip;
     const int32_t *work_end;  // device: the wave kernel takes work items [0, *work_end) (null: n_work)
-    const int4 *wrec;         // per work item: (g_start lo, g_start hi, anchors, group | qfirst << 31)
 };
 
 __device__ __forceinline__ float mg_log2(float x) {
@@ -620,7 +612,7 @@ __device__ __forceinline__ void chain_mid_group(const ChainParams &P, int64_t g0
     if (act) {
         P.f[g0 + lane] = F;
         P.p[g0 + lane] = PJ < 0 ? -1 : g0 + PJ;
-        P.t_global[g0 + lane] = 0;  // the backtrack's marks start cleared
+        if (HYMET_CHAIN_TZERO) P.t_global[g0 + lane] = 0;  // the backtrack's marks start cleared
     }
     __builtin_amdgcn_wave_barrier();
 }
@@ -660,50 +652,6 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
     // s + kChainStripes t), as in backtrack_long_kernel: one returning atomic per group on a
     // single address serialises at its L2 channel
     int stripe = (int)(blockIdx.x % kChainStripes), exhausted = 0;
-#if HYMET_CHAIN_WPF
-    // blocking grab: this stripe's next item, moving on when the stripe runs dry; -1: all dry
-    auto grab = [&]() -> int {
-        for (;;) {
-            int w = 0;
-            if (lane == 0) w = atomicAdd(P.work_counter + stripe * kChainCtrPad, 1);
-            w = stripe + kChainStripes * __builtin_amdgcn_readfirstlane(w);
-            if (w < n_work) return w;
-            if (++exhausted == kChainStripes) return -1;
-            stripe = stripe + 1 == kChainStripes ? 0 : stripe + 1;  // this stripe is done: help the next
-        }
-    };
-    int w_nx = grab();
-    int4 rec_nx = make_int4(0, 0, 0, 0);
-    int pq = 0, ps = stripe;  // the grab in flight (lane 0's counter value) and its stripe
-    if (w_nx >= 0) {
-        rec_nx = P.wrec[w_nx];
-        if (lane == 0) pq = atomicAdd(P.work_counter + stripe * kChainCtrPad, 1);
-    }
-    while (w_nx >= 0) {
-        const int4 rec = rec_nx;
-        {  // the next item: the grab issued a group ago, else (its stripe ran dry) the next stripes'
-            int w2 = ps + kChainStripes * __builtin_amdgcn_readfirstlane(pq);
-            if (w2 >= n_work) {
-                if (++exhausted == kChainStripes) {
-                    w2 = -1;
-                } else {
-                    stripe = stripe + 1 == kChainStripes ? 0 : stripe + 1;
-                    w2 = grab();
-                }
-            }
-            w_nx = w2;
-            if (w_nx >= 0) {
-                rec_nx = P.wrec[w_nx];
-                ps = stripe;
-                if (lane == 0) pq = atomicAdd(P.work_counter + stripe * kChainCtrPad, 1);
-            }
-        }
-        const int g = U(rec.w & 0x7fffffff);
-        GTIME_START
-        const int64_t g0 = (int64_t)((uint64_t)(uint32_t)U(rec.y) << 32 | (uint32_t)U(rec.x));
-        const int32_t n = U(rec.z);
-        const bool qfirst = rec.w < 0;
-#else
     for (;;) {
         int w = 0;
         if (lane == 0) w = atomicAdd(P.work_counter + stripe * kChainCtrPad, 1);
@@ -719,7 +667,6 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         const int64_t g0 = P.g_start[g];
         const int32_t n = (int32_t)(P.g_start[g + 1] - g0);
         const bool qfirst = P.g_qfirst[g] != 0;
-#endif
         if constexpr (kMidMax > 0 && !kLongPass) {
             if (n <= kMidMax && P.cap_rmq_size >= 64) {
                 chain_mid_group(P, g0, n, qfirst, c, reinterpret_cast<int32_t *>(smem + kRing * sizeof(int4)));
@@ -1608,7 +1555,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
 #if !HYMET_CHAIN_LATE_FP
                             P.f[g0 + k] = fk;
                             P.p[g0 + k] = pk_local < 0 ? -1 : g0 + pk_local;
-                            P.t_global[g0 + k] = 0;
+                            if (HYMET_CHAIN_TZERO) P.t_global[g0 + k] = 0;
 #endif
                             ring[k & kRingMask] = make_int4(kx, ky, fk, pw);
                             xring[k & (kXRing - 1)] = kx;
@@ -1708,7 +1655,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                         if (lane < acc) {
                             P.f[g0 + k] = fk;
                             P.p[g0 + k] = pk_local < 0 ? -1 : g0 + pk_local;
-                            P.t_global[g0 + k] = 0;
+                            if (HYMET_CHAIN_TZERO) P.t_global[g0 + k] = 0;
                         }
 #endif
                         prev.x = rl(kx, l), prev.y = rl(ky, l), prev.f = rl(fk, l), prev.pw = rl(pw, l);
@@ -1860,7 +1807,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             // stamps only ever land on earlier anchors, and are cleared at the group's end)
             P.f[g0 + i] = max_f;
             P.p[g0 + i] = max_j < 0 ? -1 : g0 + max_j;
-            P.t_global[g0 + i] = 0;
+            if (HYMET_CHAIN_TZERO) P.t_global[g0 + i] = 0;
             prev.x = xi, prev.y = yi, prev.f = max_f, prev.pw = (int32_t)((uint32_t)(max_j + 1) | (uint32_t)span_i << 24);
             if (lane == 0) {
                 ring[i & kRingMask] = make_int4(prev.x, prev.y, prev.f, prev.pw);
@@ -2463,29 +2410,14 @@ __global__ __launch_bounds__(64) void chain_small_kernel(ChainParams P, const in
         F[i] = max_f, PJ[i] = max_j;
         P.f[g0 + i] = max_f;
         P.p[g0 + i] = max_j < 0 ? -1 : g0 + max_j;
-        P.t_global[g0 + i] = 0;
+        if (HYMET_CHAIN_TZERO) P.t_global[g0 + i] = 0;
     }
 }
 
-// the wave kernel's work records: work-list position -> (group start, size, group | qfirst << 31)
-__global__ void chain_wrec_kernel(const int64_t *g_start, const uint8_t *g_qfirst, const int32_t *order, int32_t n_work,
-                                  int4 *wrec) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= n_work) return;
-    const int g = order[w];
-    const int64_t g0 = g_start[g];
-    wrec[w] = make_int4((int32_t)(uint32_t)g0, (int32_t)(g0 >> 32), (int32_t)(g_start[g + 1] - g0),
-                        (int32_t)((uint32_t)g | (g_qfirst[g] ? 0x80000000u : 0u)));
-}
-
 // The chaining launches for a work list: the small-group split, the wave kernel on the
-// groups above kSmall anchors, the lane kernel on the rest.  `split` is device scratch, and
-// P0.wrec n_work records of device scratch.
+// groups above kSmall anchors, the lane kernel on the rest.  `split` is device scratch.
 int launch_chain_raw(hipStream_t st, const ChainParams &P0, int64_t blocks, int32_t *split) {
     ChainParams P = P0;
-    hipLaunchKernelGGL(chain_wrec_kernel, dim3((unsigned)std::max(1, (P.n_work + 255) / 256)), dim3(256), 0, st, P.g_start, P.g_qfirst,
-                       P.order, P.n_work, const_cast<int4 *>(P.wrec));
-    HY_CHECK_LAUNCH("chain_wrec_kernel");
     hipLaunchKernelGGL(chain_small_split_kernel, dim3(1), dim3(64), 0, st, P.g_start, P.order, P.n_work, split,
                        P.work_counter, P.max_dist > 10000 ? kSmallLong : kSmall);
     HY_CHECK_LAUNCH("chain_small_split_kernel");
@@ -2504,15 +2436,14 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
                  int max_dist_inner, int bw, int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip,
                  int64_t n_anchors, int64_t n_groups) {
     if (n_work <= 0) return HYMET_OK;
-    DevBuf cnt, sum, split, wrec;
+    DevBuf cnt, sum, split;
     const size_t n_sum = (size_t)(n_anchors >> 6) + (size_t)n_groups + 2;
     HY_HIP(sum.alloc(16 * kGSumInts * n_sum, ctx->stream));
-    HY_HIP(wrec.alloc(16 * (size_t)n_work, ctx->stream));
     HY_HIP(cnt.alloc(4 * (size_t)kChainCtrPad * kChainStripes, ctx->stream));  // the wave kernel's striped work counters
     HY_HIP(split.alloc(4, ctx->stream));
     if (max_dist < bw) max_dist = bw;
     if (max_dist_inner <= 0 || max_dist_inner >= max_dist) max_dist_inner = 0;
-    ChainParams P{ax, ay, g_start, g_qfirst, order, n_work, cnt.as<int32_t>(), f, p, t_global, sum.as<int4>(), max_dist, max_dist_inner, bw, max_chn_skip, cap_rmq_size, pen_gap, pen_skip, nullptr, wrec.as<int4>()};
+    ChainParams P{ax, ay, g_start, g_qfirst, order, n_work, cnt.as<int32_t>(), f, p, t_global, sum.as<int4>(), max_dist, max_dist_inner, bw, max_chn_skip, cap_rmq_size, pen_gap, pen_skip, nullptr};
     // one wave per block, as many resident per CU as registers and LDS allow
     int64_t blocks = n_work;
     int per_cu = 0;
@@ -2530,9 +2461,6 @@ int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const i
     // anchor it chains (x, y read; f, p written), counted on the device from the work list
     const int slot = long_pass ? 2 : 0;
     hipStream_t st = ctx->stream;
-    hipLaunchKernelGGL(chain_wrec_kernel, dim3((unsigned)((n_work + 255) / 256)), dim3(256), 0, st, g_start, g_qfirst, order,
-                       n_work, wrec.as<int4>());
-    HY_CHECK_LAUNCH("chain_wrec_kernel");
     {
         ProfScope _ps(ctx, long_pass ? "mm_chain_long" : "mm_chain", slot, 28.0);
         hipLaunchKernelGGL(chain_small_split_kernel, dim3(1), dim3(64), 0, st, P.g_start, P.order, P.n_work,

@@ -153,6 +153,14 @@ int inclusive_max_scan_i32(hymet_ctx *ctx, const int32_t *in, int32_t *out, int6
 // Per-query grouped sort of anchor keys (mm_asort.hip): key/val (n, query-major, query offsets
 // d_qoff[n_q + 1]) into the sorted anchor set okey (k1) / ax / ay (oval: scratch).  Returns 1
 // with nothing written where it does not apply (the caller's device sort then runs).
+// t (the backtrack's marks, zero before it runs) cleared by a fill of every anchor in chain_set
+// (0), or by the chaining kernels as each anchor is decided (1: the extra store per anchor made
+// the first-pass wave kernel ~3 % slower on the C4 dump, 6.65-6.81 vs 6.84-7.11 ms, while the
+// fill overlaps the other mapping stream's kernels; profiles/r06_tzero/)
+#ifndef HYMET_CHAIN_TZERO
+#define HYMET_CHAIN_TZERO 0
+#endif
+
 // hb: the set's group-head bitmap (head_bits_bytes(n); AnchorOut::head).
 int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val, int64_t n, const int64_t *d_qoff, int n_q,
                         int rb, int pb, uint64_t yhi, int64_t max_qlen, uint64_t *okey, uint32_t *oval, uint64_t *ax,

@@ -1377,6 +1377,7 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
     HY_HIP(g_start.alloc(8 * (size_t)(G + 1), ctx->stream));
     HY_HIP(qfirst.alloc((size_t)G, ctx->stream));
     HY_HIP(t.alloc(4 * (size_t)n, ctx->stream));  // zeroed by the chaining kernels (and nonwork_fp_kernel) as they go
+    if (!HYMET_CHAIN_TZERO) HY_HIP(hipMemsetAsync(t.p, 0, 4 * (size_t)n, ctx->stream));
     hipLaunchKernelGGL(group_write_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.hb.as<uint32_t>(), n,
                        A.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(), G);
     HY_CHECK_LAUNCH("group_write_kernel");

@@ -114,9 +114,7 @@ int main(int argc, char **argv) {
         CK(hipMemset(df, 0, 4 * n));
         CK(hipMemset(dp, 0xFF, 8 * n));
         CK(hipMemset(dt, 0, 4 * n));  // t arrives zeroed (overflow stamps are i + 1)
-        int4 *wrec;
-        CK(hipMalloc(&wrec, 16 * (size_t)std::max(nwork, 1)));
-        ChainParams P{dx, dy, gs, qf, order, nwork, cnt, df, dp, dt, sum, max_dist, 1000, bw, 25, 100000, 0.12f, 0.0f, nullptr, wrec};
+        ChainParams P{dx, dy, gs, qf, order, nwork, cnt, df, dp, dt, sum, max_dist, 1000, bw, 25, 100000, 0.12f, 0.0f, nullptr};
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
@@ -132,7 +130,6 @@ int main(int argc, char **argv) {
 #endif
         CK(hipEventRecord(e0, 0));
         if (getenv("HYMET_CHAIN_PROF_WAVE_ONLY")) {
-            hipLaunchKernelGGL(chain_wrec_kernel, dim3((unsigned)((nwork + 255) / 256)), dim3(256), 0, 0, gs, qf, order, nwork, wrec);
             hipLaunchKernelGGL(chain_groups_kernel<0>, dim3(nblk), dim3(64), kChainLds, 0, P);
             CK(hipGetLastError());
         } else if (launch_chain_raw(0, P, nblk, split) != 0) {
