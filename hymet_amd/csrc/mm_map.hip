@@ -829,8 +829,39 @@ __global__ __launch_bounds__(256) void zorder_lane_kernel(ZParams P) {
 }
 
 // groups of 2..max_runs ascending runs: merge by ranks, one block per listed group (grid-stride
-// over the list; a flat pass over every anchor position read each one's group first)
+// over the list; a flat pass over every anchor position read each one's group first).  An
+// entry's position is its offset in its own run plus, per other run, the count of smaller keys
+// there (a binary search); a group of up to kZmLds entries is staged in LDS first, so the
+// searches' dependent reads are LDS round trips instead of L2 ones (real repeats: groups of
+// many runs and thousands of entries)
+constexpr int kZmLds = 6144;  // 48 KB: three blocks per CU
+
+template <bool LDS>
+__device__ __forceinline__ void zmerge_group(const uint64_t *zk, const int32_t *rs, int K, int m, int32_t *out) {
+    for (int q = threadIdx.x; q < m; q += blockDim.x) {
+        const uint64_t key = zk[q];
+        int pos = 0;
+        for (int k = 0; k < K; k++) {
+            const int s0 = rs[k], s1 = rs[k + 1];
+            if (q >= s0 && q < s1) {  // own run
+                pos += q - s0;
+                continue;
+            }
+            int lo = s0, hi = s1;  // first entry >= key
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (zk[mid] < key) lo = mid + 1;
+                else hi = mid;
+            }
+            pos += lo - s0;
+        }
+        out[pos] = (int32_t)(uint32_t)key;
+    }
+}
+
 __global__ __launch_bounds__(256) void zmerge_kernel(ZParams P) {
+    __shared__ uint64_t sk[kZmLds];
+    __shared__ int32_t srs[kZRuns + 1];
     const int n_list = P.lists[3];
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // the lists are final (zorder_wave_kernel ran)
         P.mail[0] = P.lists[2];
@@ -843,25 +874,13 @@ __global__ __launch_bounds__(256) void zmerge_kernel(ZParams P) {
         const int m = P.z_cnt[g];
         const int32_t *rs = P.run_start + (int64_t)g * kZRuns;
         const uint64_t *zk = P.zkey + z0;
-        for (int q = threadIdx.x; q < m; q += blockDim.x) {
-            const uint64_t key = zk[q];
-            int pos = 0;
-            for (int k = 0; k < K; k++) {
-                const int s0 = rs[k], s1 = k + 1 < K ? rs[k + 1] : m;
-                if (q >= s0 && q < s1) {  // own run
-                    pos += q - s0;
-                    continue;
-                }
-                int lo = s0, hi = s1;  // first entry >= key
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (zk[mid] < key) lo = mid + 1;
-                    else hi = mid;
-                }
-                pos += lo - s0;
-            }
-            P.z_idx[z0 + pos] = (int32_t)(uint32_t)key;
-        }
+        __syncthreads();  // the previous group's readers are done with sk / srs
+        if (threadIdx.x <= K) srs[threadIdx.x] = threadIdx.x < K ? rs[threadIdx.x] : m;
+        if (m <= kZmLds)
+            for (int q = threadIdx.x; q < m; q += blockDim.x) sk[q] = zk[q];
+        __syncthreads();
+        if (m <= kZmLds) zmerge_group<true>(sk, srs, K, m, P.z_idx + z0);
+        else zmerge_group<false>(zk, srs, K, m, P.z_idx + z0);
     }
 }
 
