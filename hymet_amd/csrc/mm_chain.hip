@@ -510,6 +510,10 @@ __device__ __forceinline__ double st_pr(const int4 &v) { return __hiloint2double
 #ifndef HYMET_CHAIN_MID
 #define HYMET_CHAIN_MID 64
 #endif
+// chain_mid_group skips the inner walk when no inner-tree entry's f + span exceeds max_f
+#ifndef HYMET_CHAIN_MIDSKIP
+#define HYMET_CHAIN_MIDSKIP 1
+#endif
 constexpr int kMidMax = HYMET_CHAIN_MID;
 
 // mg_lchain_rmq on one group of n <= 64 anchors, lane l = anchor l (lchain.c; the same
@@ -575,7 +579,17 @@ __device__ __forceinline__ void chain_mid_group(const ChainParams &P, int64_t g0
             const int32_t sc = fb + comput_sc(xi, yi, __builtin_amdgcn_readlane(X, bj), __builtin_amdgcn_readlane(Y, bj),
                                               __builtin_amdgcn_readlane(SP, bj), P.pen_gap, P.pen_skip, &exact, &width);
             if (width <= P.bw && sc > max_f) max_f = sc, max_j = bj;
-            if (!exact && in_in != 0 && yi > 0) {
+            bool walk = !exact && in_in != 0 && yi > 0;
+#if HYMET_CHAIN_MIDSKIP
+            // a candidate scores at most f_j + span_j (comput_sc <= the candidate's span), so
+            // when no inner-tree entry reaches past max_f the walk changes nothing (its t[]
+            // stamps only matter within this iteration) -- the wave kernel's max-deque test
+            if (walk) {
+                const int ub = __builtin_amdgcn_readlane(scan_max((in_in >> lane & 1) ? F + SP : INT32_MIN), 63);
+                if (ub <= max_f) walk = false;
+            }
+#endif
+            if (walk) {
                 // inner walk: tree entries with y <= yi - 1 by (y, idx) descending, down to
                 // yi - max_dist_inner -- in walk lanes, a prefix scan of the sequential loop
                 const int32_t wF = __shfl(F, wa, 64), wPJ = __shfl(PJ, wa, 64);

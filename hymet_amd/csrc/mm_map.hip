@@ -528,7 +528,7 @@ __device__ __forceinline__ uint64_t group_tile_bits(const uint32_t *hb, int64_t 
     return (hw | qs[tid]) & live;
 }
 
-__global__ __launch_bounds__(256) void group_count_kernel(const uint32_t *hb, int64_t n, const int64_t *qoff, int n_q,
+__global__ __launch_bounds__(256) void group_heads_count_kernel(const uint32_t *hb, int64_t n, const int64_t *qoff, int n_q,
                                                           uint32_t *tile_cnt) {
     __shared__ uint64_t qs[kGTile / 64];
     __shared__ uint32_t ws[4];
@@ -542,7 +542,7 @@ __global__ __launch_bounds__(256) void group_count_kernel(const uint32_t *hb, in
 
 // g_start of every group, its query-first flag (lchain.c's krmq index-0 quirk) and the
 // g_start[G] = n sentinel
-__global__ __launch_bounds__(256) void group_write_kernel(const uint32_t *hb, int64_t n, const int64_t *qoff, int n_q,
+__global__ __launch_bounds__(256) void group_heads_write_kernel(const uint32_t *hb, int64_t n, const int64_t *qoff, int n_q,
                                                           const int64_t *tile_off, int64_t *g_start, uint8_t *qfirst,
                                                           int64_t G) {
     __shared__ uint64_t qs[kGTile / 64];
@@ -1386,9 +1386,9 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
     const int64_t ntile = cdiv(n, kGTile);
     HY_HIP(tcnt.alloc(4 * (size_t)(ntile + 1), ctx->stream));
     HY_HIP(toff.alloc(8 * (size_t)(ntile + 1), ctx->stream));
-    hipLaunchKernelGGL(group_count_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.hb.as<uint32_t>(), n,
+    hipLaunchKernelGGL(group_heads_count_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.hb.as<uint32_t>(), n,
                        A.d_off.as<int64_t>(), n_q, tcnt.as<uint32_t>());
-    HY_CHECK_LAUNCH("group_count_kernel");
+    HY_CHECK_LAUNCH("group_heads_count_kernel");
     int64_t G = 0;
     int rc = exclusive_scan_u32_i64(ctx, tcnt.as<uint32_t>(), toff.as<int64_t>(), ntile, &G);
     if (rc) return rc;
@@ -1397,9 +1397,9 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
     HY_HIP(qfirst.alloc((size_t)G, ctx->stream));
     HY_HIP(t.alloc(4 * (size_t)n, ctx->stream));  // zeroed by the chaining kernels (and nonwork_fp_kernel) as they go
     if (!HYMET_CHAIN_TZERO) HY_HIP(hipMemsetAsync(t.p, 0, 4 * (size_t)n, ctx->stream));
-    hipLaunchKernelGGL(group_write_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.hb.as<uint32_t>(), n,
+    hipLaunchKernelGGL(group_heads_write_kernel, dim3((unsigned)ntile), dim3(256), 0, ctx->stream, A.hb.as<uint32_t>(), n,
                        A.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(), G);
-    HY_CHECK_LAUNCH("group_write_kernel");
+    HY_CHECK_LAUNCH("group_heads_write_kernel");
     // work list: groups with >= min_cnt anchors, biggest first
     DevBuf skey, sidx, swork, skey2, sidx2, zlists;
     HY_HIP(skey.alloc(4 * (size_t)G, ctx->stream));
