@@ -70,10 +70,12 @@ struct AnchorOut {
     int rb, pb;
     uint64_t yhi;
     uint32_t *hb;
+    uint32_t *ax32;  // x's low word (rpos) alone: the chaining kernels' reads, 4 B per anchor instead of 8
     __device__ __forceinline__ void put(int64_t i, uint64_t k, uint32_t y) const {
         const uint64_t rev = k >> (rb + pb) & 1, rid = k >> pb & ((1ull << rb) - 1), rpos = k & ((1ull << pb) - 1);
         ax[i] = rev << 63 | rid << 32 | rpos;
         ay[i] = yhi << 32 | y;
+        ax32[i] = (uint32_t)rpos;
     }
     // k written at i, kp at i - 1 (first: i starts a writer's segment -- a query or a bin, a
     // head either way)
@@ -663,7 +665,7 @@ int sort_segments(hymet_ctx *ctx, const Seg *lists, int64_t cap, const int32_t *
 
 int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val, int64_t n, const int64_t *d_qoff, int n_q,
                         int rb, int pb, uint64_t yhi, int64_t max_qlen, uint64_t *okey, uint32_t *oval, uint64_t *ax,
-                        uint64_t *ay, uint32_t *hb) {
+                        uint64_t *ay, uint32_t *hb, uint32_t *ax32) {
     // bins = (strand, target) -- or, for parts of more than 2047 targets, (strand, target >> cs):
     // coarse bins of 2^cs consecutive targets, sorted inside by (low target bits, rpos, y)
     const int cs = std::max(0, 1 + rb - 12);
@@ -672,7 +674,7 @@ int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val
     const int ybits = bits_of(max_qlen);
     if (n <= 0 || n_q <= 0 || 1 + rb + pb + ybits > 63) return 1;
     hipStream_t st = ctx->stream;
-    const AnchorOut out{ax, ay, rb, pb, yhi, hb};
+    const AnchorOut out{ax, ay, rb, pb, yhi, hb, ax32};
     HY_HIP(hipMemsetAsync(hb, 0, head_bits_bytes(n), st));
     // 1 queries by size
     DevBuf qlists, nt;

@@ -227,7 +227,7 @@ __device__ int4 *g_chain_gcnt;  // per group: loop iterations, batch attempts, b
 constexpr int kChainStripes = HYMET_CHAIN_STRIPES, kChainCtrPad = 64;
 
 struct ChainParams {
-    const uint64_t *ax;
+    const int32_t *ax;        // x's low word (target position) per anchor: x >> 32 is the group's constant
     const uint64_t *ay;
     const int64_t *g_start;   // group g = anchors [g_start[g], g_start[g+1])
     const uint8_t *g_qfirst;  // group g starts its query's anchor array (the krmq index-0 quirk)
@@ -523,8 +523,8 @@ __device__ __forceinline__ void chain_mid_group(const ChainParams &P, int64_t g0
     const int lane = threadIdx.x;
     const bool act = lane < n;
     const int jl = act ? lane : n - 1;
-    const uint64_t xv = P.ax[g0 + jl], yv = P.ay[g0 + jl];
-    const int32_t X = (int32_t)xv, Y = (int32_t)yv, SP = (int32_t)(yv >> 32 & 0xff);
+    const uint64_t yv = P.ay[g0 + jl];
+    const int32_t X = P.ax[g0 + jl], Y = (int32_t)yv, SP = (int32_t)(yv >> 32 & 0xff);
     // walk order: the anchors by (y, idx) descending; lane w of the walk holds anchor wa
     int rank = 0;
     for (int m = 0; m < n; ++m) {
@@ -705,12 +705,13 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 v = hc[jl & 63];
             } else {
                 CCOUNT(0);
-                const uint64_t x = P.ax[g0 + jl], y = P.ay[g0 + jl];
+                const int32_t x = P.ax[g0 + jl];
+                const uint64_t y = P.ay[g0 + jl];
 #if HYMET_CHAIN_HNOP
-                v = make_int4((int32_t)x, (int32_t)y, ld_l2(P.f + g0 + jl), (int32_t)((uint32_t)(y >> 32 & 0xff) << 24));
+                v = make_int4(x, (int32_t)y, ld_l2(P.f + g0 + jl), (int32_t)((uint32_t)(y >> 32 & 0xff) << 24));
 #else
                 const int64_t pp = ld_l2(P.p + g0 + jl);
-                v = make_int4((int32_t)x, (int32_t)y, ld_l2(P.f + g0 + jl),
+                v = make_int4(x, (int32_t)y, ld_l2(P.f + g0 + jl),
                               (int32_t)((pp < 0 ? 0u : (uint32_t)(pp - g0 + 1)) | (uint32_t)(y >> 32 & 0xff) << 24));
 #endif
             }
@@ -725,9 +726,10 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
             if (i - jl <= kRing) {
                 v = ring[jl & kRingMask];
             } else {
-                const uint64_t x = P.ax[g0 + jl], y = P.ay[g0 + jl];
+                const int32_t x = P.ax[g0 + jl];
+                const uint64_t y = P.ay[g0 + jl];
                 const int64_t pp = ld_l2(P.p + g0 + jl);
-                v = make_int4((int32_t)x, (int32_t)y, ld_l2(P.f + g0 + jl),
+                v = make_int4(x, (int32_t)y, ld_l2(P.f + g0 + jl),
                               (int32_t)((pp < 0 ? 0u : (uint32_t)(pp - g0 + 1)) | (uint32_t)(y >> 32 & 0xff) << 24));
             }
             e.x = v.x, e.y = v.y, e.f = v.z, e.pw = v.w;
@@ -741,7 +743,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         auto fetch_x = [&](int32_t jl) -> int32_t {
             if (i - jl <= kXRing) return xring[jl & (kXRing - 1)];
             if ((jl >> 6) == hb) return hc[jl & 63].x;
-            return (int32_t)P.ax[g0 + jl];
+            return P.ax[g0 + jl];
         };
         auto fetch_y = [&](int32_t jl) -> int32_t {
             if (i - jl <= kRing) return ring[jl & kRingMask].y;
@@ -769,9 +771,8 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
                 }
                 const int32_t jn = ((b + 1) << 6) + lane;
                 if (((b + 1) << 6) + 63 < i0) {
-                    const int32_t *ax32 = reinterpret_cast<const int32_t *>(P.ax + g0 + jn);
                     const int32_t *ay32 = reinterpret_cast<const int32_t *>(P.ay + g0 + jn);
-                    pf_x = ax32[0], pf_ylo = ay32[0], pf_yhi = ay32[1];
+                    pf_x = P.ax[g0 + jn], pf_ylo = ay32[0], pf_yhi = ay32[1];
                     pf_f = ld_l2(P.f + g0 + jn);
                     pfb = b + 1;
                 }
@@ -879,7 +880,7 @@ __global__ __launch_bounds__(64) HYMET_CHAIN_ATTR void chain_groups_kernel(Chain
         // the compiler land each prefetch in a temporary and wait for it (vmcnt) to copy it
         // into place, so the prefetch was synchronous.  Lanes past the group end hold copies of
         // its last anchor, which nothing reads (batches stop at the group end).
-        auto ldx = [&](int32_t b) -> int32_t { return reinterpret_cast<const int32_t *>(P.ax + g0 + min(b, n - 1))[0]; };
+        auto ldx = [&](int32_t b) -> int32_t { return P.ax[g0 + min(b, n - 1)]; };
         auto ldy = [&](int32_t b) -> uint64_t { return P.ay[g0 + min(b, n - 1)]; };
         Ent prev{0, 0, 0, 0};  // anchor i-1
         // block b complete: staircase summary -- S1 = argmin, S(k+1) = argmin over y < y(Sk),
@@ -2350,8 +2351,8 @@ __global__ __launch_bounds__(64) void chain_small_kernel(ChainParams P, const in
     int32_t X[kSmall], Y[kSmall], SP[kSmall], F[kSmall], PJ[kSmall], T[kSmall];
     int8_t ord[kSmall];  // local indices by (y, idx) ascending
     for (int j = 0; j < n; ++j) {
-        const uint64_t x = P.ax[g0 + j], y = P.ay[g0 + j];
-        X[j] = (int32_t)x, Y[j] = (int32_t)y, SP[j] = (int32_t)(y >> 32 & 0xff);
+        const uint64_t y = P.ay[g0 + j];
+        X[j] = P.ax[g0 + j], Y[j] = (int32_t)y, SP[j] = (int32_t)(y >> 32 & 0xff);
         F[j] = 0, PJ[j] = -1, T[j] = -1;
         int k = j;  // insertion by (y, idx): later j is the larger idx, so ties stay behind
         while (k > 0 && Y[ord[k - 1]] > Y[j]) {
@@ -2445,7 +2446,7 @@ int launch_chain_raw(hipStream_t st, const ChainParams &P0, int64_t blocks, int3
     return HYMET_OK;
 }
 
-int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *g_start, const uint8_t *g_qfirst,
+int launch_chain(hymet_ctx *ctx, const int32_t *ax, const uint64_t *ay, const int64_t *g_start, const uint8_t *g_qfirst,
                  const int32_t *order, int32_t n_work, int32_t *f, int64_t *p, int32_t *t_global, int max_dist,
                  int max_dist_inner, int bw, int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip,
                  int64_t n_anchors, int64_t n_groups) {

@@ -161,10 +161,10 @@ int inclusive_max_scan_i32(hymet_ctx *ctx, const int32_t *in, int32_t *out, int6
 #define HYMET_CHAIN_TZERO 0
 #endif
 
-// hb: the set's group-head bitmap (head_bits_bytes(n); AnchorOut::head).
+// hb: the set's group-head bitmap (head_bits_bytes(n); AnchorOut::head); ax32: x's low words.
 int grouped_anchor_sort(hymet_ctx *ctx, const uint64_t *key, const uint32_t *val, int64_t n, const int64_t *d_qoff, int n_q,
                         int rb, int pb, uint64_t yhi, int64_t max_qlen, uint64_t *okey, uint32_t *oval, uint64_t *ax,
-                        uint64_t *ay, uint32_t *hb);
+                        uint64_t *ay, uint32_t *hb, uint32_t *ax32);
 // bytes of an anchor set's group-head bitmap: one bit per anchor, in whole 64-bit words (the
 // group kernels read two words per thread)
 inline size_t head_bits_bytes(int64_t n) { return 8 * (size_t)((n + 63) / 64 + 1); }

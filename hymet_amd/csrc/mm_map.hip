@@ -39,7 +39,7 @@ struct hymet_mm_result {
 namespace hymet {
 namespace mm {
 
-int launch_chain(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const int64_t *g_start, const uint8_t *g_qfirst,
+int launch_chain(hymet_ctx *ctx, const int32_t *ax, const uint64_t *ay, const int64_t *g_start, const uint8_t *g_qfirst,
                  const int32_t *order, int32_t n_work, int32_t *f, int64_t *p, int32_t *t_global, int max_dist,
                  int max_dist_inner, int bw, int max_chn_skip, int cap_rmq_size, float pen_gap, float pen_skip,
                  int64_t n_anchors, int64_t n_groups);
@@ -570,6 +570,12 @@ __global__ __launch_bounds__(256) void group_heads_write_kernel(const uint32_t *
         ++g;
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) g_start[G] = n;
+}
+
+// x's low words of an anchor set written without them (the two-key, re-sort and test paths)
+__global__ void x_low_kernel(const uint64_t *x, int64_t n, uint32_t *x32) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) x32[i] = (uint32_t)x[i];
 }
 
 // the head bitmap of an anchor set written without one (the two-key and re-sort paths):
@@ -1124,7 +1130,7 @@ __global__ __launch_bounds__(256) void mark_count_kernel(const int32_t *t, int64
 __global__ __launch_bounds__(256) void mark_compact_kernel(const int32_t *t, int64_t n, const uint32_t *qflag,
                                                            const int64_t *qoff, int n_q, const int64_t *tile_off,
                                                            const int64_t *last_kept, const uint64_t *ax, const uint64_t *ay,
-                                                           uint64_t *ox, uint64_t *oy, uint32_t *ohb) {
+                                                           uint64_t *ox, uint64_t *oy, uint32_t *ohb, uint32_t *ox32) {
     __shared__ uint32_t rc[64];       // kept per (row, wave), row-major
     __shared__ uint32_t nk[64];       // the same counts (rc becomes their exclusive scan)
     __shared__ uint32_t lx[64];       // x >> 32 of each (row, wave) chunk's last kept anchor
@@ -1167,6 +1173,7 @@ __global__ __launch_bounds__(256) void mark_compact_kernel(const int32_t *t, int
             const uint64_t xv = ax[e];
             xh[j] = (uint32_t)(xv >> 32);
             ox[o] = xv;
+            ox32[o] = (uint32_t)xv;
             oy[o] = ay[e];
         }
         if (b && lane == 63 - __clzll((long long)b)) lx[j * 4 + w] = xh[j];
@@ -1275,6 +1282,8 @@ struct AnchorSet {
     DevBuf d_off;
     DevBuf hb;            // group-head bitmap (head_bits_bytes(n)): bit i where x >> 32 changes
     bool has_hb = false;  // hb written by whoever built the set; else chain_set derives it from x
+    DevBuf ax32;          // x's low words (the chaining kernels read 4 B of x per anchor, not 8)
+    bool has_x32 = false;
 };
 
 // Chains of an anchor set: compacted anchors (chain by chain, chains ordered by first
@@ -1346,10 +1355,12 @@ static int sort_anchor_keys(hymet_ctx *ctx, DevBuf &key, DevBuf &val, int64_t n,
     }();
     if (gsort) {
         HY_HIP(out.hb.alloc(head_bits_bytes(n), ctx->stream));
+        HY_HIP(out.ax32.alloc(4 * (size_t)n, ctx->stream));
         const int rc = grouped_anchor_sort(ctx, kk, vv, n, d_qoff, n_q, rb, pb, (uint64_t)yhi, max_qlen, kka, vva,
-                                           out.ax.as<uint64_t>(), out.ay.as<uint64_t>(), out.hb.as<uint32_t>());
+                                           out.ax.as<uint64_t>(), out.ay.as<uint64_t>(), out.hb.as<uint32_t>(),
+                                           out.ax32.as<uint32_t>());
         if (rc == HYMET_OK) {
-            out.has_hb = true;
+            out.has_hb = out.has_x32 = true;
             return HYMET_OK;
         }
         if (rc != 1) return rc;
@@ -1381,6 +1392,11 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         HY_HIP(A.hb.alloc(head_bits_bytes(n), ctx->stream));
         LAUNCH1(head_bits_x_kernel, n, A.ax.as<uint64_t>(), n, A.hb.as<uint64_t>());
         A.has_hb = true;
+    }
+    if (!A.has_x32) {
+        HY_HIP(A.ax32.alloc(4 * (size_t)n, ctx->stream));
+        LAUNCH1(x_low_kernel, n, A.ax.as<uint64_t>(), n, A.ax32.as<uint32_t>());
+        A.has_x32 = true;
     }
     DevBuf tcnt, toff;
     const int64_t ntile = cdiv(n, kGTile);
@@ -1436,7 +1452,7 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
         // memsets of all n
         LAUNCH1(nonwork_fp_kernel, G, g_start.as<int64_t>(), (int32_t)G, opt->min_cnt, f.as<int32_t>(), p.as<int64_t>(),
                 t.as<int32_t>());
-        rc = launch_chain(ctx, A.ax.as<uint64_t>(), A.ay.as<uint64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
+        rc = launch_chain(ctx, A.ax32.as<int32_t>(), A.ay.as<uint64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
                           (const int32_t *)vp,
                           (int32_t)n_work, f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(), opt->max_gap,
                           opt->rmq_inner_dist, bw, opt->max_chain_skip, opt->rmq_size_cap, pen_gap, pen_skip, n, G);
@@ -2172,14 +2188,15 @@ static int mm_map_impl(hymet_ctx *ctx, const hymet_mm_index *idx, const hymet_mm
                 HY_HIP(S2.ax.alloc(8 * (size_t)(A2 + 1), st));
                 HY_HIP(S2.ay.alloc(8 * (size_t)(A2 + 1), st));
                 HY_HIP(S2.hb.alloc(head_bits_bytes(A2), st));
+                HY_HIP(S2.ax32.alloc(4 * (size_t)(A2 + 1), st));
                 HY_HIP(hipMemsetAsync(S2.hb.p, 0, head_bits_bytes(A2), st));
                 hipLaunchKernelGGL(mark_compact_kernel, dim3((unsigned)nt), dim3(256), 0, st, mark.as<int32_t>(), n1,
                                    flag.as<uint32_t>(), S1.d_off.as<int64_t>(), n_q, toff.as<int64_t>(), tlast.as<int64_t>(),
                                    S1.ax.as<uint64_t>(), S1.ay.as<uint64_t>(), S2.ax.as<uint64_t>(), S2.ay.as<uint64_t>(),
-                                   S2.hb.as<uint32_t>());
+                                   S2.hb.as<uint32_t>(), S2.ax32.as<uint32_t>());
                 HY_CHECK_LAUNCH("mark_compact_kernel");
                 S2.n = A2;
-                S2.has_hb = true;
+                S2.has_hb = S2.has_x32 = true;
                 rc = dump_anchors(getenv("HYMET_DUMP_ANCHORS2"), S2, dumped2);
                 if (rc) return rc;
             } else if (key_path) {
@@ -2434,7 +2451,10 @@ int hymet_mm_chain_dp(hymet_ctx *ctx, const uint64_t *h_x, const uint64_t *h_y, 
     HY_HIP(hipMemsetAsync(f.p, 0, 4 * (size_t)n, st));
     HY_HIP(hipMemsetAsync(p.p, 0xFF, 8 * (size_t)n, st));
     HY_HIP(hipMemsetAsync(t.p, 0, 4 * (size_t)n, st));
-    rc = launch_chain(ctx, x.as<uint64_t>(), y.as<uint64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
+    DevBuf x32;
+    HY_HIP(x32.alloc(4 * (size_t)n, st));
+    LAUNCH1(x_low_kernel, n, x.as<uint64_t>(), n, x32.as<uint32_t>());
+    rc = launch_chain(ctx, x32.as<int32_t>(), y.as<uint64_t>(), g_start.as<int64_t>(), qfirst.as<uint8_t>(),
                       (const int32_t *)vp, (int32_t)G, f.as<int32_t>(), p.as<int64_t>(), t.as<int32_t>(), max_dist,
                       max_dist_inner, bw, max_chn_skip, cap_rmq_size, pen_gap, pen_skip, n, G);
     if (rc) return rc;

@@ -55,6 +55,13 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&qf, 1));
     CK(hipMalloc(&sum, 16 * kGSumInts * ns));
     CK(hipMemcpy(dx, hx.data(), 8 * n, hipMemcpyHostToDevice));
+    int32_t *dx32;  // the chaining kernels read x's low words
+    {
+        std::vector<int32_t> h32(n);
+        for (int64_t i = 0; i < n; i++) h32[i] = (int32_t)hx[i];
+        CK(hipMalloc(&dx32, 4 * n));
+        CK(hipMemcpy(dx32, h32.data(), 4 * n, hipMemcpyHostToDevice));
+    }
     CK(hipMemcpy(dy, hy.data(), 8 * n, hipMemcpyHostToDevice));
     // groups = runs of equal x >> 32, work list by size descending, group 0 holds anchor 0
     std::vector<int64_t> h_gs;
@@ -114,7 +121,7 @@ int main(int argc, char **argv) {
         CK(hipMemset(df, 0, 4 * n));
         CK(hipMemset(dp, 0xFF, 8 * n));
         CK(hipMemset(dt, 0, 4 * n));  // t arrives zeroed (overflow stamps are i + 1)
-        ChainParams P{dx, dy, gs, qf, order, nwork, cnt, df, dp, dt, sum, max_dist, 1000, bw, 25, 100000, 0.12f, 0.0f, nullptr};
+        ChainParams P{dx32, dy, gs, qf, order, nwork, cnt, df, dp, dt, sum, max_dist, 1000, bw, 25, 100000, 0.12f, 0.0f, nullptr};
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
