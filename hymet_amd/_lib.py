@@ -46,7 +46,7 @@ _SIGS = {
     "hymet_msh_text_offsets": (_i32, [_vp, _vp, _vp]),
     "hymet_msh_close": (None, [_vp]),
     "hymet_screen_table_slots": (_i64, [_i64]),
-    "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _vp]),
+    "hymet_screen_table_build": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i32]),
     "hymet_screen_count": (_i32, [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _u32, _i32, _c.POINTER(_vp), _c.POINTER(_i64),
                                   _c.POINTER(_vp), _c.POINTER(_i64), _c.POINTER(_vp), _u64, _vp, _i64, _vp, _vp]),
     "hymet_screen_stats": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),

@@ -33,6 +33,11 @@ namespace {
 
 constexpr uint64_t kEmpty = ~0ull;
 
+// A slot's key word: the key's high 32 bits for 64-bit sketches (a match is then checked against
+// the full key in the DB's hash array), the whole key for Mash's 32-bit sketches (k <= 16: the
+// hashes are MurmurHash3_x86_32 values, so the word is the key and no check is needed)
+__device__ __forceinline__ uint32_t key_word(uint64_t h, bool lo) { return lo ? (uint32_t)h : (uint32_t)(h >> 32); }
+
 // Home slot of a hash: multiplicative (Fibonacci) hashing of the full 64 bits.  The top bits
 // alone would crowd every real sketch into the bottom of the table: a bottom-s MinHash sketch
 // holds the s SMALLEST hashes of its genome, so their top bits are all zero.
@@ -138,6 +143,7 @@ __device__ __forceinline__ uint32_t ascii_of(uint32_t c) { return (0x54474341u >
 
 template <int K>
 __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
+    constexpr bool LO = K <= 16;  // 32-bit sketches: tables built with key_bits 32
     constexpr int NW = (K + 7) / 8;
     constexpr int TOPB = K - 8 * (NW - 1);
     constexpr uint64_t TOPMASK = TOPB == 8 ? ~0ull : ((1ull << (8 * TOPB)) - 1);
@@ -190,7 +196,7 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
                 for (;;) {
                     const uint64_t w = tab[s];
                     if (w == kEmpty) break;
-                    if ((w >> 32) == (h >> 32) && P.hashes[d][(uint32_t)w] == h) {
+                    if ((uint32_t)(w >> 32) == key_word(h, LO) && (LO || P.hashes[d][(uint32_t)w] == h)) {
                         atomicAdd(&P.counts[d][(uint32_t)w], 1u);
                         break;
                     }
@@ -213,18 +219,18 @@ __global__ __launch_bounds__(256) void screen_count_kernel(CountParams P) {
 // saw; canon_of[i] = i is written for every hash and fixed for the listed ones after.
 __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t *__restrict__ hashes, int64_t n,
                                                            unsigned long long *tab, uint64_t mask, int shift,
-                                                           int64_t *dups, int32_t *canon_of) {
+                                                           int64_t *dups, int32_t *canon_of, bool lo) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t h = hashes[i];
     canon_of[i] = h == kEmpty ? (int32_t)n : (int32_t)i;
     if (h == kEmpty) return;
-    const unsigned long long want = (h & 0xFFFFFFFF00000000ull) | (uint32_t)i;
+    const unsigned long long want = (uint64_t)key_word(h, lo) << 32 | (uint32_t)i;
     uint64_t s = home_slot(h, shift);
     for (;;) {
         const unsigned long long prev = atomicCAS(&tab[s], (unsigned long long)kEmpty, want);
         if (prev == kEmpty) return;  // claimed
-        if ((prev >> 32) == (h >> 32) && hashes[(uint32_t)prev] == h) {  // the key is there already
+        if ((uint32_t)(prev >> 32) == key_word(h, lo) && (lo || hashes[(uint32_t)prev] == h)) {  // the key is there already
             atomicMin(&tab[s], want);
             const unsigned long long k = atomicAdd(reinterpret_cast<unsigned long long *>(dups), 1ull);
             dups[1 + k] = (int64_t)((uint64_t)i << 32 | (uint32_t)prev);
@@ -238,7 +244,7 @@ __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t *__res
 // the key (the owner is found by the first duplicate to arrive), take the slot's final index
 __global__ __launch_bounds__(256) void dup_fix_kernel(const uint64_t *__restrict__ hashes, const int64_t *dups,
                                                       const unsigned long long *tab, uint64_t mask, int shift,
-                                                      int32_t *canon_of) {
+                                                      int32_t *canon_of, bool lo) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= dups[0]) return;
     const uint64_t e = (uint64_t)dups[1 + k];
@@ -248,7 +254,7 @@ __global__ __launch_bounds__(256) void dup_fix_kernel(const uint64_t *__restrict
     unsigned long long w;
     for (;;) {  // the key's slot (it is in the table: j's CAS found it)
         w = tab[s];
-        if ((w >> 32) == (h >> 32) && hashes[(uint32_t)w] == h) break;
+        if ((uint32_t)(w >> 32) == key_word(h, lo) && (lo || hashes[(uint32_t)w] == h)) break;
         s = (s + 1) & mask;
     }
     canon_of[j] = (int32_t)(uint32_t)w;
@@ -352,8 +358,10 @@ int64_t hymet_screen_table_slots(int64_t n_hashes) {
 }
 
 int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n, uint64_t *d_table, int64_t n_slots,
-                             int64_t *d_scratch, int32_t *d_canon_of) {
+                             int64_t *d_scratch, int32_t *d_canon_of, int key_bits) {
     HY_ARG(ctx && d_table && d_scratch && d_canon_of, "hymet_screen_table_build: null argument");
+    HY_ARG(key_bits == 32 || key_bits == 64, "hymet_screen_table_build: key_bits must be 32 or 64");
+    const bool lo = key_bits == 32;
     HY_ARG(n_slots >= 1024 && (n_slots & (n_slots - 1)) == 0, "hymet_screen_table_build: n_slots must be a power of two >= 1024");
     HY_ARG(n_slots >= 2 * n, "hymet_screen_table_build: n_slots must be >= 2*n_hashes");
     HY_ARG(n < (1ll << 31) - 1, "hymet_screen_table_build: more than 2^31 - 2 hashes");
@@ -365,10 +373,10 @@ int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n
     hymet::ProfScope _ps(ctx, "screen_table_build");
     const dim3 grid((unsigned)hymet::cdiv(n, 256));
     hipLaunchKernelGGL(table_insert_kernel, grid, dim3(256), 0, ctx->stream, d_hashes, n, (unsigned long long *)d_table,
-                       (uint64_t)(n_slots - 1), 64 - lg, d_scratch, d_canon_of);
+                       (uint64_t)(n_slots - 1), 64 - lg, d_scratch, d_canon_of, lo);
     HY_CHECK_LAUNCH("table_insert_kernel");
     hipLaunchKernelGGL(dup_fix_kernel, grid, dim3(256), 0, ctx->stream, d_hashes, (const int64_t *)d_scratch,
-                       (const unsigned long long *)d_table, (uint64_t)(n_slots - 1), 64 - lg, d_canon_of);
+                       (const unsigned long long *)d_table, (uint64_t)(n_slots - 1), 64 - lg, d_canon_of, lo);
     HY_CHECK_LAUNCH("dup_fix_kernel");
     return HYMET_OK;
 }

@@ -55,8 +55,15 @@ class ScreenTable:
         # the offsets first: a pageable upload waits for the stream's earlier work, and queued
         # behind the insert it would hold the host for the whole build
         self.ref_off = torch.from_numpy(np.ascontiguousarray(db.offsets, dtype=np.int64)).to(gpu.dev)
-        gpu.call("hymet_screen_table_build", ptr(d_h), n, ptr(self.table), self.n_slots, ptr(scratch), ptr(self.canon_of))
-        self.hashes = d_h          # probes check full keys here: it lives as long as the table
+        # 32-bit sketches (k <= 16) keep the whole key in the slot: no second, dependent load of
+        # the DB's hash per probe
+        key_bits = 32 if db.k <= 16 else 64
+        gpu.call("hymet_screen_table_build", ptr(d_h), n, ptr(self.table), self.n_slots, ptr(scratch), ptr(self.canon_of),
+                 key_bits)
+        # 64-bit keys: probes check full keys here; 32-bit: read by the (asynchronous) build only.
+        # Either way it lives as long as the table
+        self.hashes = d_h
+        self.key_bits = key_bits
         del scratch
 
 

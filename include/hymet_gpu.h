@@ -113,16 +113,20 @@ int hymet_name_hash(hymet_ctx *ctx, const uint8_t *d_raw, const int64_t *d_name_
  * sketch hashes of a DB, counts of every pooled canonical k-mer hash that hits it, and the
  * per-reference shared / median-depth statistics. */
 int64_t hymet_screen_table_slots(int64_t n_hashes);
-/* d_table: n_slots uint64 slots, each (key >> 32) << 32 | the smallest input index holding
- * the key (its canonical index), all ones when empty -- a probe matching the high word checks
- * the full key at d_hashes[index], so d_hashes must stay allocated while the table is used;
+/* d_table: n_slots uint64 slots, each key word << 32 | the smallest input index holding the
+ * key (its canonical index), all ones when empty.  key_bits 64 (Mash's 64-bit sketches, k > 16):
+ * the key word is the key's high 32 bits and a probe matching it checks the full key at
+ * d_hashes[index], so d_hashes must stay allocated while the table is used; key_bits 32 (the
+ * 32-bit sketches, k <= 16, the only tables hymet_screen_count probes for such k): the word is
+ * the whole key and d_hashes is not read after the build;
  * d_scratch: n_hashes + 1 int64 (the duplicate keys' list); d_canon_of: n_hashes int32, each
  * input hash's canonical index (n_hashes for the reserved all-ones key).  Hits are counted per
  * canonical index, so counts are in the DB's own order on every rank whatever slots parallel
  * insertion chose, and the ranks' partial counts add up as they are.  Resets
  * d_table. */
 int hymet_screen_table_build(hymet_ctx *ctx, const uint64_t *d_hashes, int64_t n_hashes,
-                             uint64_t *d_table, int64_t n_slots, int64_t *d_scratch, int32_t *d_canon_of);
+                             uint64_t *d_table, int64_t n_slots, int64_t *d_scratch, int32_t *d_canon_of,
+                             int key_bits);
 /* The library's stable LSD radix sort (8-bit digits) of device (key, value) pairs by key bits
  * [begin_bit, end_bit), in place (the sort behind the mapper's minimizer, group, chain and
  * anchor-segment orders and the LCA row order; no rocPRIM on the mapping path). */

