@@ -29,6 +29,8 @@ _SIGS = {
     "hymet_scratch_trim": (_i32, [_vp, _c.POINTER(_i64)]),
     "hymet_scratch_cached": (_i32, [_vp, _c.POINTER(_i64)]),
     "hymet_scratch_stats": (_i32, [_vp, _vp]),
+    "hymet_scratch_reserve": (_i32, [_vp, _i64]),
+    "hymet_set_oom_hook": (_i32, [_vp, _vp]),
     "hymet_copy_to_host": (_i32, [_vp, _vp, _vp, _i64, _i32]),
     "hymet_copy_to_device": (_i32, [_vp, _vp, _vp, _i64, _i32]),
     "hymet_pack": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
@@ -81,6 +83,17 @@ _SIGS = {
 }
 
 _lib = None
+_oom_hook = None   # kept referenced: the library holds the function pointer
+
+
+def _release_torch_cache(_user):
+    """The library's out-of-memory hook (hymet_set_oom_hook): its own scratch cache is already
+    dropped, so give back the blocks torch's caching allocator holds unused."""
+    try:
+        import torch
+        torch.cuda.empty_cache()
+    except Exception:   # a hook must not raise into C; the library then reports its OOM
+        pass
 
 
 class HymetError(RuntimeError):
@@ -102,6 +115,9 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    global _oom_hook
+    _oom_hook = _c.CFUNCTYPE(None, _vp)(_release_torch_cache)
+    lib.hymet_set_oom_hook(_c.cast(_oom_hook, _vp), None)
     _lib = lib
     return lib
 
@@ -188,11 +204,26 @@ class Gpu:
         check(self.lib.hymet_scratch_trim(self.ctx, _c.byref(out)), "hymet_scratch_trim")
         return out.value
 
+    def reserve(self, nbytes: int):
+        """Warm the library's scratch cache with one block of `nbytes` (hymet_scratch_reserve)."""
+        check(self.lib.hymet_scratch_reserve(self.ctx, int(nbytes)), "hymet_scratch_reserve")
+
+    def _alloc(self, fn, n, dtype):
+        # The library's scratch cache and torch's pool share the HBM: when torch runs out (after
+        # releasing its own unused blocks), the library's cached blocks go back and torch retries.
+        # The other direction is the library's OOM hook (_release_torch_cache).
+        try:
+            return fn(int(n), dtype=dtype, device=self.dev)
+        except self.torch.OutOfMemoryError:
+            if self.trim() == 0:
+                raise
+            return fn(int(n), dtype=dtype, device=self.dev)
+
     def empty(self, n, dtype):
-        return self.torch.empty(int(n), dtype=dtype, device=self.dev)
+        return self._alloc(self.torch.empty, n, dtype)
 
     def zeros(self, n, dtype):
-        return self.torch.zeros(int(n), dtype=dtype, device=self.dev)
+        return self._alloc(self.torch.zeros, n, dtype)
 
     def close(self):
         if self.ctx:

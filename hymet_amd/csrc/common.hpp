@@ -83,6 +83,7 @@ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // (hipMalloc/hipFree and the stream-ordered pool cost 0.1-0.4 s per large block on this
 // stack, at every mapping batch, hence the cache.)
 hipError_t scratch_alloc(size_t bytes, hipStream_t stream, void **p, size_t *cls);
+void set_oom_hook(void (*hook)(void *), void *user);
 void scratch_free(void *p, hipStream_t stream, size_t cls);
 }  // namespace hymet
 

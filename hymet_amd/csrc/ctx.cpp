@@ -36,6 +36,10 @@ struct CacheKey {
 static std::map<CacheKey, std::vector<void *>> g_cache;  // free blocks
 static size_t g_cached = 0;                                // bytes held in g_cache
 static int64_t g_stats[3] = {0, 0, 0};  // hipMalloc calls (cache misses), OOM cache drops, frees over the cap
+// Called when hipMalloc still fails after this allocator dropped its own cache: the host
+// releases what another caching allocator in the process (torch's) holds unused.
+static void (*g_oom_hook)(void *) = nullptr;
+static void *g_oom_user = nullptr;
 
 static size_t cache_cap() {
     static const size_t cap = [] {
@@ -92,12 +96,31 @@ hipError_t scratch_alloc(size_t bytes, hipStream_t stream, void **p, size_t *cls
     if (e == hipErrorOutOfMemory) {  // give the cached blocks of this device back and retry once
         (void)hipGetLastError();
         (void)hipDeviceSynchronize();
-        std::lock_guard<std::mutex> lk(g_cache_mu);
-        g_stats[1]++;
-        drop_cached(dev);
-        e = hipMalloc(p, *cls);
+        void (*hook)(void *) = nullptr;
+        void *user = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(g_cache_mu);
+            g_stats[1]++;
+            drop_cached(dev);
+            e = hipMalloc(p, *cls);
+            hook = g_oom_hook;
+            user = g_oom_user;
+        }
+        if (e == hipErrorOutOfMemory && hook) {  // then the other pool's, outside our lock
+            (void)hipGetLastError();
+            hook(user);
+            e = hipMalloc(p, *cls);
+        }
+        if (e != hipSuccess) (void)hipGetLastError();  // reported through the return value only:
+                                                       // a stale error would fail torch's next check
     }
     return e;
+}
+
+void set_oom_hook(void (*hook)(void *), void *user) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    g_oom_hook = hook;
+    g_oom_user = user;
 }
 
 void scratch_free(void *p, hipStream_t stream, size_t cls) {
@@ -255,8 +278,23 @@ int hymet_prof_names(hymet_ctx *ctx, char *buf, int64_t cap) {
 int hymet_scratch_trim(hymet_ctx *ctx, int64_t *freed_bytes) {
     HY_ARG(ctx != nullptr, "hymet_scratch_trim: null ctx");
     HY_HIP(hipSetDevice(ctx->device));
-    HY_HIP(hipStreamSynchronize(ctx->stream));
+    HY_HIP(hipDeviceSynchronize());  // cached blocks of every stream of the device go back
     return hymet::scratch_trim(ctx->device, freed_bytes);
+}
+
+int hymet_scratch_reserve(hymet_ctx *ctx, int64_t bytes) {
+    HY_ARG(ctx && bytes > 0, "hymet_scratch_reserve: bad argument");
+    HY_HIP(hipSetDevice(ctx->device));
+    void *p = nullptr;
+    size_t cls = 0;
+    HY_HIP(hymet::scratch_alloc((size_t)bytes, ctx->stream, &p, &cls));
+    hymet::scratch_free(p, ctx->stream, cls);
+    return HYMET_OK;
+}
+
+int hymet_set_oom_hook(void (*hook)(void *user), void *user) {
+    hymet::set_oom_hook(hook, user);
+    return HYMET_OK;
 }
 
 int hymet_scratch_stats(hymet_ctx *ctx, int64_t *counts) {

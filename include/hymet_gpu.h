@@ -56,10 +56,18 @@ int hymet_prof_names(hymet_ctx *ctx, char *buf, int64_t cap);
 /* The library's kernel scratch is a caching allocator keyed by (device, stream, size class)
  * (best fit up to twice the request) and capped at HYMET_SCRATCH_CAP_GB (default 160) of
  * cached blocks.  trim synchronises the
- * context stream and returns every cached block of the device to HIP (e.g. before torch
+ * device and returns every cached block of the device to HIP (e.g. before torch
  * allocates large tensors); cached reports the bytes held. */
 int hymet_scratch_trim(hymet_ctx *ctx, int64_t *freed_bytes);
 int hymet_scratch_cached(hymet_ctx *ctx, int64_t *bytes);
+/* Allocates `bytes` of scratch on the context's stream and returns them to the cache at once
+ * (warms the pool before a run; a cached block is reused by later requests of up to that size). */
+int hymet_scratch_reserve(hymet_ctx *ctx, int64_t bytes);
+/* Process-wide: when hipMalloc fails even after the scratch cache was dropped, call
+ * hook(user) once and retry.  The Python host sets it to torch.cuda.empty_cache, so the
+ * library's pool and torch's yield to each other (torch's side: hymet_amd._lib.Gpu.empty).
+ * NULL clears it. */
+int hymet_set_oom_hook(void (*hook)(void *user), void *user);
 /* counts[0..2]: the allocator's hipMalloc calls (cache misses), out-of-memory retries (each
  * synchronises the device and drops the cache) and frees past the cap (hipFree), since load. */
 int hymet_scratch_stats(hymet_ctx *ctx, int64_t *counts);
