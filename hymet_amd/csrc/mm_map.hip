@@ -651,6 +651,8 @@ __global__ void group_size_kernel(const int64_t *g_start, int32_t G, int min_cnt
 //    not depend on the list order).
 constexpr int kZs = 2048;
 constexpr int kZRuns = 16;
+constexpr int kZmLds = 6144;   // merge groups staged in LDS up to this many entries (48 KB: three blocks per CU)
+constexpr int kZmUnit = 2048;  // larger merge groups: units of this many entries, one block each
 constexpr int kZLane = 16;
 #ifndef HYMET_Z_DEPTH
 #define HYMET_Z_DEPTH 8
@@ -663,13 +665,16 @@ struct ZParams {
     const int32_t *order;  // all groups by descending size (the chaining work list, whole)
     int32_t G;
     int min_sc, max_runs;
+    int zm_lds, zm_unit;   // kZmLds / kZmUnit (HYMET_ZM_LDS / HYMET_ZM_UNIT in tests)
     uint64_t *zkey;        // n: (f << 32 | idx) at the group's compacted z positions
     int32_t *z_idx;        // n: the order, at the same positions
     int32_t *z_cnt;        // per group: number of z entries
     int32_t *z_runs;       // per group: ascending runs (0 when empty)
     int32_t *run_start;    // per group, kZRuns entries: run starts relative to g_start
-    int32_t *lists;        // [0] split, [1] mid count, [2] big count, [3] merge count, [4..5] big total (i64)
+    int32_t *lists;        // [0] split, [1] mid count, [2] big count, [3] merge count, [4..5] big total (i64),
+                           // [6] merge-unit count
     int32_t *merge_list;   // groups of 2..max_runs runs, for the merge
+    int64_t *mergeu_list;  // units (group << 32 | u) of kZmUnit entries of the merge groups above kZmLds
     int32_t *mid_list;     // groups for the block sort
     int32_t *big_list;     // groups for the radix path
     int64_t *big_off;      // their offsets in the radix arrays
@@ -791,7 +796,17 @@ __global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
             }
         }
         // (wave-uniform conditions)
-        if (runs > 1 && runs <= P.max_runs) push(0, g);
+        if (runs > 1 && runs <= P.max_runs) {
+            if (m <= P.zm_lds) {
+                push(0, g);
+            } else {  // a long merge is split over blocks (one block walking it was the launch's tail)
+                const int nu = (m + P.zm_unit - 1) / P.zm_unit;
+                int base = 0;
+                if (lane == 0) base = atomicAdd(P.lists + 6, nu);
+                base = __shfl(base, 0, 64);
+                for (int u = lane; u < nu; u += 64) P.mergeu_list[base + u] = (int64_t)g << 32 | (uint32_t)u;
+            }
+        }
         if (runs > P.max_runs) {
             if (m <= kZs) {
                 push(1, g);
@@ -837,29 +852,53 @@ __global__ __launch_bounds__(256) void zorder_lane_kernel(ZParams P) {
 // groups of 2..max_runs ascending runs: merge by ranks, one block per listed group (grid-stride
 // over the list; a flat pass over every anchor position read each one's group first).  An
 // entry's position is its offset in its own run plus, per other run, the count of smaller keys
-// there (a binary search); a group of up to kZmLds entries is staged in LDS first, so the
-// searches' dependent reads are LDS round trips instead of L2 ones (real repeats: groups of
-// many runs and thousands of entries)
-constexpr int kZmLds = 6144;  // 48 KB: three blocks per CU
-
-template <bool LDS>
-__device__ __forceinline__ void zmerge_group(const uint64_t *zk, const int32_t *rs, int K, int m, int32_t *out) {
-    for (int q = threadIdx.x; q < m; q += blockDim.x) {
+// there; a group of up to kZmLds entries is staged in LDS first (real repeats: groups of many
+// runs and thousands of entries).  Each thread takes a stripe of consecutive entries: within a
+// run the keys ascend, so each other run's count only moves forward from the previous entry's,
+// found by an exponential search from there (mostly one compare) instead of a full binary search
+// per entry and run; a new run (the key drops) restarts the counts at the run starts.
+// entries [qa, qb) of a group of m entries in K runs (rs: K + 1 run bounds)
+__device__ __forceinline__ void zmerge_group(const uint64_t *zk, const int32_t *rs, int K, int m, int qa, int qb,
+                                             int32_t *out) {
+    const int S = (qb - qa + (int)blockDim.x - 1) / (int)blockDim.x;  // entries per thread
+    const int q0 = qa + (int)threadIdx.x * S, q1 = min(q0 + S, qb);
+    if (q0 >= qb) return;
+    int rsr[kZRuns + 1], lo[kZRuns];
+#pragma unroll
+    for (int k = 0; k <= kZRuns; k++) rsr[k] = k <= K ? rs[k] : m;
+    int own = 0, own_s = 0;  // the run of entry q and its start (no dynamic register indexing)
+#pragma unroll
+    for (int k = 1; k < kZRuns; k++)
+        if (k < K && rsr[k] <= q0) own = k, own_s = rsr[k];
+    uint64_t prev = ~0ull;
+    for (int q = q0; q < q1; q++) {
         const uint64_t key = zk[q];
-        int pos = 0;
-        for (int k = 0; k < K; k++) {
-            const int s0 = rs[k], s1 = rs[k + 1];
-            if (q >= s0 && q < s1) {  // own run
-                pos += q - s0;
-                continue;
+        const bool restart = key < prev;  // the first entry, or the first of the next run
+        prev = key;
+        if (restart && q > q0) own++, own_s = q;  // a run start is exactly where the key drops
+        int pos = q - own_s;                       // the offset in its own run
+#pragma unroll
+        for (int k = 0; k < kZRuns; k++) {
+            if (k < K && k != own) {
+                const int s1 = rsr[k + 1];
+                int l = restart ? rsr[k] : lo[k];
+                if (l < s1 && zk[l] < key) {  // first entry >= key in (l, s1]: gallop, then bisect
+                    int b = 1;
+                    while (l + b < s1 && zk[l + b] < key) {
+                        l += b;
+                        b <<= 1;
+                    }
+                    int a = l + 1, e = min(l + b, s1);
+                    while (a < e) {
+                        const int mid = (a + e) >> 1;
+                        if (zk[mid] < key) a = mid + 1;
+                        else e = mid;
+                    }
+                    l = a;
+                }
+                lo[k] = l;
+                pos += l - rsr[k];
             }
-            int lo = s0, hi = s1;  // first entry >= key
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (zk[mid] < key) lo = mid + 1;
-                else hi = mid;
-            }
-            pos += lo - s0;
         }
         out[pos] = (int32_t)(uint32_t)key;
     }
@@ -868,13 +907,16 @@ __device__ __forceinline__ void zmerge_group(const uint64_t *zk, const int32_t *
 __global__ __launch_bounds__(256) void zmerge_kernel(ZParams P) {
     __shared__ uint64_t sk[kZmLds];
     __shared__ int32_t srs[kZRuns + 1];
-    const int n_list = P.lists[3];
+    const int n_list = P.lists[3], n_units = P.lists[6];
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // the lists are final (zorder_wave_kernel ran)
         P.mail[0] = P.lists[2];
         P.mail[1] = *reinterpret_cast<const int64_t *>(P.lists + 4);
     }
-    for (int w = blockIdx.x; w < n_list; w += gridDim.x) {
-        const int g = P.merge_list[w];
+    // units of the long merges first (they were the tail), then the staged groups
+    for (int w = blockIdx.x; w < n_units + n_list; w += gridDim.x) {
+        const bool unit = w < n_units;
+        const int64_t uw = unit ? P.mergeu_list[w] : 0;
+        const int g = unit ? (int)(uw >> 32) : P.merge_list[w - n_units];
         const int K = P.z_runs[g];
         const int64_t z0 = P.g_start[g];
         const int m = P.z_cnt[g];
@@ -882,11 +924,15 @@ __global__ __launch_bounds__(256) void zmerge_kernel(ZParams P) {
         const uint64_t *zk = P.zkey + z0;
         __syncthreads();  // the previous group's readers are done with sk / srs
         if (threadIdx.x <= K) srs[threadIdx.x] = threadIdx.x < K ? rs[threadIdx.x] : m;
-        if (m <= kZmLds)
+        if (!unit)
             for (int q = threadIdx.x; q < m; q += blockDim.x) sk[q] = zk[q];
         __syncthreads();
-        if (m <= kZmLds) zmerge_group<true>(sk, srs, K, m, P.z_idx + z0);
-        else zmerge_group<false>(zk, srs, K, m, P.z_idx + z0);
+        if (unit) {
+            const int qa = (int)(uint32_t)uw * P.zm_unit;
+            zmerge_group(zk, srs, K, m, qa, min(qa + P.zm_unit, m), P.z_idx + z0);
+        } else {
+            zmerge_group(sk, srs, K, m, 0, m, P.z_idx + z0);
+        }
     }
 }
 
@@ -1458,13 +1504,19 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
                           opt->rmq_inner_dist, bw, opt->max_chain_skip, opt->rmq_size_cap, pen_gap, pen_skip, n, G);
         if (rc) return rc;
         // z = anchors with f >= min_sc ordered by (group, f, idx), inside each group's range
-        DevBuf zkey, zidx, z_cnt, z_runs, run_start, merge_list, mid_list, big_list, big_off;
+        DevBuf zkey, zidx, z_cnt, z_runs, run_start, merge_list, mergeu_list, mid_list, big_list, big_off;
         HY_HIP(zkey.alloc(8 * (size_t)n, ctx->stream));
         HY_HIP(zidx.alloc(4 * (size_t)n, ctx->stream));
         HY_HIP(z_cnt.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(z_runs.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(run_start.alloc(4 * (size_t)G * kZRuns, ctx->stream));
         HY_HIP(merge_list.alloc(4 * (size_t)G, ctx->stream));
+        // HYMET_ZM_LDS / HYMET_ZM_UNIT (tests): stage merge groups up to that many entries, split
+        // the others into units of that many
+        const char *el = getenv("HYMET_ZM_LDS"), *eu = getenv("HYMET_ZM_UNIT");
+        const int zm_lds = el ? std::max(0, std::min(kZmLds, atoi(el))) : kZmLds;
+        const int zm_unit = eu ? std::max(1, atoi(eu)) : kZmUnit;
+        HY_HIP(mergeu_list.alloc(8 * (size_t)(n / zm_unit + G + 16), ctx->stream));  // >= sum of cdiv(m, unit)
         HY_HIP(mid_list.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(big_list.alloc(4 * (size_t)G, ctx->stream));
         HY_HIP(big_off.alloc(8 * (size_t)G, ctx->stream));
@@ -1475,8 +1527,9 @@ static int chain_set(hymet_ctx *ctx, const hymet_mm_opt *opt, float pen_gap, flo
             const char *ev = getenv("HYMET_Z_RUNS");
             const int max_runs = ev ? std::max(1, std::min(kZRuns, atoi(ev))) : kZRuns;
             ZParams Z{f.as<int32_t>(), g_start.as<int64_t>(), (const int32_t *)vp, (int32_t)G, opt->min_chain_score,
-                      max_runs, zkey.as<uint64_t>(), zidx.as<int32_t>(), z_cnt.as<int32_t>(), z_runs.as<int32_t>(),
-                      run_start.as<int32_t>(), zlists.as<int32_t>(), merge_list.as<int32_t>(), mid_list.as<int32_t>(), big_list.as<int32_t>(),
+                      max_runs, zm_lds, zm_unit, zkey.as<uint64_t>(), zidx.as<int32_t>(), z_cnt.as<int32_t>(), z_runs.as<int32_t>(),
+                      run_start.as<int32_t>(), zlists.as<int32_t>(), merge_list.as<int32_t>(), mergeu_list.as<int64_t>(),
+                      mid_list.as<int32_t>(), big_list.as<int32_t>(),
                       big_off.as<int64_t>(), mb_dev(ctx, kMbZBig)};
             hipLaunchKernelGGL(zsplit_kernel, dim3(1), dim3(64), 0, ctx->stream, Z);
             HY_CHECK_LAUNCH("zsplit_kernel");

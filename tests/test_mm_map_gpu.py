@@ -53,15 +53,21 @@ def _queries(rng, refs):
     return qs
 
 
-@pytest.mark.parametrize("bt_long,legacy,z_runs,resort", [(None, None, None, None), ("4", None, None, None),
-                                                         (None, "1", "1", None), (None, None, "2", None),
-                                                         (None, None, None, "1")])
-def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy, z_runs, resort):
+@pytest.mark.parametrize("bt_long,legacy,z_runs,resort,zm", [(None, None, None, None, None), ("4", None, None, None, None),
+                                                            (None, "1", "1", None, None), (None, None, "2", None, None),
+                                                            (None, None, None, "1", None), (None, None, None, None, "0,7")])
+def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy, z_runs, resort, zm):
     """bt_long = "4": nearly every chain group takes the wave-per-group backtrack path.
     legacy = "1": anchors take the two-key sort path (used when the one-key anchor sort key
     would exceed 64 bits).  z_runs: backtrack-order groups of more ascending runs than this
     take the sort fallbacks (block bitonic / global radix) instead of the run merge.
-    resort = "1": the long join re-sorts its anchors instead of compacting the first pass's."""
+    resort = "1": the long join re-sorts its anchors instead of compacting the first pass's.
+    zm = "0,7": no merge group is staged in LDS; each is split into units of 7 entries, one
+    block per unit (the path of merge groups above 6,144 entries)."""
+    if zm is not None:
+        lds, unit = zm.split(",")
+        monkeypatch.setenv("HYMET_ZM_LDS", lds)
+        monkeypatch.setenv("HYMET_ZM_UNIT", unit)
     if resort is not None:
         monkeypatch.setenv("HYMET_RECHAIN_SORT", resort)
     if bt_long is not None:
