@@ -724,59 +724,32 @@ __global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
         if (lane == np[l]) pend[l] = g;
         if (++np[l] == 64) flush(l);
     };
-    for (int w = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); w < split; w += nw) {
-        const int g = P.order[w];
-        const int64_t g0 = P.g_start[g], n = P.g_start[g + 1] - g0;
-        int32_t *rs = P.run_start + (int64_t)g * kZRuns;
-        int m = 0, K = 0;  // z entries so far, descents so far (wave-uniform)
-        uint64_t last = 0;
-        const uint64_t below = (1ull << lane) - 1;
-        // kZDepth chunks of f loaded together: a group of tens of thousands of anchors is one
-        // wave's serial walk, the launch's tail (one chunk ahead: a round trip per 64 anchors)
-        for (int64_t base0 = 0; base0 < n; base0 += 64 * kZDepth) {
-            int32_t fc[kZDepth];
-#pragma unroll
-            for (int d = 0; d < kZDepth; d++) {
-                const int64_t i = base0 + 64 * d + lane;
-                fc[d] = i < n ? P.f[g0 + i] : 0;
-            }
-#pragma unroll
-            for (int d = 0; d < kZDepth; d++) {
-                const int64_t i = base0 + 64 * d + lane;
-                const bool ok = i < n;
-                const int32_t fv = fc[d];
-                const bool z = ok && fv >= P.min_sc;
-                const uint64_t bal = __ballot(z);
-                if (bal == 0) continue;
-                const uint64_t key = (uint64_t)(uint32_t)fv << 32 | (uint32_t)(g0 + i);
-                const uint64_t lower = bal & below;
-                const int pos = m + __popcll(lower);
-                const int prev = lower ? 63 - __clzll((long long)lower) : lane;
-                uint64_t pk = shfl64(key, prev);
-                if (!lower) pk = last;
-                const bool desc = z && pos > 0 && key < pk;
-                const uint64_t dbal = __ballot(desc);
-                if (z) P.z_idx[g0 + pos] = (int32_t)(g0 + i);
-                if (desc) {
-                    const int r = K + 1 + __popcll(dbal & below);
-                    if (r < kZRuns) rs[r] = pos;
-                }
-                K += __popcll(dbal);
-                m += __popcll(bal);
-                last = shfl64(key, 63 - __clzll((long long)bal));
-            }
+    // The wave's groups are w0, w0 + nw, w0 + 2 nw, ...; each round loads the next 64 of them
+    // (list entry and bounds, lane r holding group r) in one round trip instead of two dependent
+    // ones per group -- most groups are a single chunk of f, so those round trips were half the
+    // wave's time.
+    for (int wb = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); wb < split; wb += 64 * nw) {
+        const int64_t wl = (int64_t)wb + (int64_t)lane * nw;
+        int gl = 0;
+        int64_t sl = 0, el = 0;
+        if (wl < split) {
+            gl = P.order[wl];
+            sl = P.g_start[gl];
+            el = P.g_start[gl + 1];
         }
-        const int runs = m > 0 ? K + 1 : 0;
-        if (lane == 0) {
-            rs[0] = 0;
-            P.z_cnt[g] = m;
-            P.z_runs[g] = runs;
-        }
-        if (runs > 1) {
-            // only the merge / sort paths read the keys: a group of one run (C4's colinear
-            // chains: most of them) writes its order alone, 4 B per z entry instead of 12, and
-            // the others write the keys in a second pass over f
-            int m2 = 0;
+        const int nr = (int)min((int64_t)64, ((int64_t)split - wb + nw - 1) / nw);  // groups this round
+        for (int r = 0; r < nr; r++) {
+            const int g = __builtin_amdgcn_readlane(gl, r);
+            const int64_t g0 = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(sl >> 32), r) << 32 |
+                                         (uint32_t)__builtin_amdgcn_readlane((int32_t)sl, r));
+            const int64_t n = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(el >> 32), r) << 32 |
+                                        (uint32_t)__builtin_amdgcn_readlane((int32_t)el, r)) - g0;
+            int32_t *rs = P.run_start + (int64_t)g * kZRuns;
+            int m = 0, K = 0;  // z entries so far, descents so far (wave-uniform)
+            uint64_t last = 0;
+            const uint64_t below = (1ull << lane) - 1;
+            // kZDepth chunks of f loaded together: a group of tens of thousands of anchors is one
+            // wave's serial walk, the launch's tail (one chunk ahead: a round trip per 64 anchors)
             for (int64_t base0 = 0; base0 < n; base0 += 64 * kZDepth) {
                 int32_t fc[kZDepth];
 #pragma unroll
@@ -787,34 +760,79 @@ __global__ __launch_bounds__(256) void zorder_wave_kernel(ZParams P) {
 #pragma unroll
                 for (int d = 0; d < kZDepth; d++) {
                     const int64_t i = base0 + 64 * d + lane;
-                    const bool z = i < n && fc[d] >= P.min_sc;
+                    const bool ok = i < n;
+                    const int32_t fv = fc[d];
+                    const bool z = ok && fv >= P.min_sc;
                     const uint64_t bal = __ballot(z);
                     if (bal == 0) continue;
-                    if (z) P.zkey[g0 + m2 + __popcll(bal & below)] = (uint64_t)(uint32_t)fc[d] << 32 | (uint32_t)(g0 + i);
-                    m2 += __popcll(bal);
+                    const uint64_t key = (uint64_t)(uint32_t)fv << 32 | (uint32_t)(g0 + i);
+                    const uint64_t lower = bal & below;
+                    const int pos = m + __popcll(lower);
+                    const int prev = lower ? 63 - __clzll((long long)lower) : lane;
+                    uint64_t pk = shfl64(key, prev);
+                    if (!lower) pk = last;
+                    const bool desc = z && pos > 0 && key < pk;
+                    const uint64_t dbal = __ballot(desc);
+                    if (z) P.z_idx[g0 + pos] = (int32_t)(g0 + i);
+                    if (desc) {
+                        const int r = K + 1 + __popcll(dbal & below);
+                        if (r < kZRuns) rs[r] = pos;
+                    }
+                    K += __popcll(dbal);
+                    m += __popcll(bal);
+                    last = shfl64(key, 63 - __clzll((long long)bal));
                 }
             }
-        }
-        // (wave-uniform conditions)
-        if (runs > 1 && runs <= P.max_runs) {
-            if (m <= P.zm_lds) {
-                push(0, g);
-            } else {  // a long merge is split over blocks (one block walking it was the launch's tail)
-                const int nu = (m + P.zm_unit - 1) / P.zm_unit;
-                int base = 0;
-                if (lane == 0) base = atomicAdd(P.lists + 6, nu);
-                base = __shfl(base, 0, 64);
-                for (int u = lane; u < nu; u += 64) P.mergeu_list[base + u] = (int64_t)g << 32 | (uint32_t)u;
+            const int runs = m > 0 ? K + 1 : 0;
+            if (lane == 0) {
+                rs[0] = 0;
+                P.z_cnt[g] = m;
+                P.z_runs[g] = runs;
             }
-        }
-        if (runs > P.max_runs) {
-            if (m <= kZs) {
-                push(1, g);
-            } else {
-                // list rank only: the radix arrays' offsets are a scan of the counts in rank
-                // order (zbig_count_kernel), since the sorted keys come out rank-major
-                push(2, g);
-                big_m += (unsigned long long)m;
+            if (runs > 1) {
+                // only the merge / sort paths read the keys: a group of one run (C4's colinear
+                // chains: most of them) writes its order alone, 4 B per z entry instead of 12, and
+                // the others write the keys in a second pass over f
+                int m2 = 0;
+                for (int64_t base0 = 0; base0 < n; base0 += 64 * kZDepth) {
+                    int32_t fc[kZDepth];
+#pragma unroll
+                    for (int d = 0; d < kZDepth; d++) {
+                        const int64_t i = base0 + 64 * d + lane;
+                        fc[d] = i < n ? P.f[g0 + i] : 0;
+                    }
+#pragma unroll
+                    for (int d = 0; d < kZDepth; d++) {
+                        const int64_t i = base0 + 64 * d + lane;
+                        const bool z = i < n && fc[d] >= P.min_sc;
+                        const uint64_t bal = __ballot(z);
+                        if (bal == 0) continue;
+                        if (z) P.zkey[g0 + m2 + __popcll(bal & below)] = (uint64_t)(uint32_t)fc[d] << 32 | (uint32_t)(g0 + i);
+                        m2 += __popcll(bal);
+                    }
+                }
+            }
+            // (wave-uniform conditions)
+            if (runs > 1 && runs <= P.max_runs) {
+                if (m <= P.zm_lds) {
+                    push(0, g);
+                } else {  // a long merge is split over blocks (one block walking it was the launch's tail)
+                    const int nu = (m + P.zm_unit - 1) / P.zm_unit;
+                    int base = 0;
+                    if (lane == 0) base = atomicAdd(P.lists + 6, nu);
+                    base = __shfl(base, 0, 64);
+                    for (int u = lane; u < nu; u += 64) P.mergeu_list[base + u] = (int64_t)g << 32 | (uint32_t)u;
+                }
+            }
+            if (runs > P.max_runs) {
+                if (m <= kZs) {
+                    push(1, g);
+                } else {
+                    // list rank only: the radix arrays' offsets are a scan of the counts in rank
+                    // order (zbig_count_kernel), since the sorted keys come out rank-major
+                    push(2, g);
+                    big_m += (unsigned long long)m;
+                }
             }
         }
     }
