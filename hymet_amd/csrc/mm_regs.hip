@@ -96,6 +96,7 @@ struct RegParams {
     const uint64_t *q_sumk;
     const uint32_t *skip_q;        // queries whose regions come from the long join (nullable)
     int wave_min;                  // queries of more chains than this take regions_wave_kernel
+    int lds_max;                   // ... and hold their regions in LDS up to this many (kRegSmall)
 };
 
 // (x0, y0): the chain's first anchor, (x1, y1): its last
@@ -662,25 +663,49 @@ __device__ __forceinline__ int64_t wave_sum_l(int64_t v) {
     for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
 }
-// descending bitonic sort of m (a power of two) 128-bit keys in LDS
+// descending bitonic sort of m (a power of two) 128-bit keys in LDS, or in the global scratch
+// of a query beyond the LDS capacity.  A pass's pairs are disjoint, so kSortU of each lane's
+// pairs are loaded before any is compared and stored: in global memory one round trip per
+// kSortU pairs instead of per pair (a 5,000-chain query's sort was one wave's serial walk of
+// ~6,000 round trips, the launch's tail).
+constexpr int kSortU = 4;
+__device__ __forceinline__ int bitonic_lo(int t, int d) { return (t / d) * 2 * d + (t % d); }
 __device__ void lds_sort_desc(U128 *a, int m) {
+    const int half = m >> 1;
     for (int s = 2; s <= m; s <<= 1)
         for (int d = s >> 1; d > 0; d >>= 1) {
-            for (int t = threadIdx.x; t < (m >> 1); t += 64) {
-                const int i = (t / d) * 2 * d + (t % d), j = i + d;
-                const U128 x = a[i], y = a[j];
-                if (((i & s) == 0) ? lt128(x, y) : lt128(y, x)) a[i] = y, a[j] = x;
+            for (int t0 = threadIdx.x; t0 < half; t0 += 64 * kSortU) {
+                U128 x[kSortU], y[kSortU];
+#pragma unroll
+                for (int u = 0; u < kSortU; u++) {
+                    const int t = t0 + 64 * u, i = bitonic_lo(t < half ? t : 0, d);
+                    x[u] = a[i], y[u] = a[i + d];
+                }
+#pragma unroll
+                for (int u = 0; u < kSortU; u++) {
+                    const int t = t0 + 64 * u, i = bitonic_lo(t < half ? t : 0, d);
+                    if (t < half && (((i & s) == 0) ? lt128(x[u], y[u]) : lt128(y[u], x[u]))) a[i] = y[u], a[i + d] = x[u];
+                }
             }
             wsync();
         }
 }
 __device__ void lds_sort_asc_u64(uint64_t *a, int m) {
+    const int half = m >> 1;
     for (int s = 2; s <= m; s <<= 1)
         for (int d = s >> 1; d > 0; d >>= 1) {
-            for (int t = threadIdx.x; t < (m >> 1); t += 64) {
-                const int i = (t / d) * 2 * d + (t % d), j = i + d;
-                const uint64_t x = a[i], y = a[j];
-                if (((i & s) == 0) ? y < x : x < y) a[i] = y, a[j] = x;
+            for (int t0 = threadIdx.x; t0 < half; t0 += 64 * kSortU) {
+                uint64_t x[kSortU], y[kSortU];
+#pragma unroll
+                for (int u = 0; u < kSortU; u++) {
+                    const int t = t0 + 64 * u, i = bitonic_lo(t < half ? t : 0, d);
+                    x[u] = a[i], y[u] = a[i + d];
+                }
+#pragma unroll
+                for (int u = 0; u < kSortU; u++) {
+                    const int t = t0 + 64 * u, i = bitonic_lo(t < half ? t : 0, d);
+                    if (t < half && (((i & s) == 0) ? y[u] < x[u] : x[u] < y[u])) a[i] = y[u], a[i + d] = x[u];
+                }
             }
             wsync();
         }
@@ -699,7 +724,7 @@ __global__ __launch_bounds__(64) void regions_wave_kernel(RegParams P, const int
     for (int w = blockIdx.x; w < nb; w += gridDim.x) {
         const int q = __builtin_amdgcn_readfirstlane(big[w]);
         const int n = (int)(P.qc[q + 1] - P.qc[q]);
-        if (n <= kRegSmall) {
+        if (n <= P.lds_max) {
             regions_wave(P, q, rsm, kRegSmall);
         } else {
             int m = 64;
@@ -1081,9 +1106,14 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
     }
     RegParams P{ax, ay, ids, cfirst, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
-                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk, skip_q, kRegWave};
-    static const int wave_min_env = getenv("HYMET_REG_WAVE") ? atoi(getenv("HYMET_REG_WAVE")) : -1;  // tests / A-B
-    if (wave_min_env >= 0) P.wave_min = wave_min_env;
+                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk, skip_q, kRegWave, kRegSmall};
+    // tests / A-B: HYMET_REG_WAVE (chains above which a query takes the wave kernel),
+    // HYMET_REG_LDS (chains up to which the wave kernel works in LDS; 32: every wave query on the
+    // global-scratch path from 33 chains: a query's share of that scratch, 2n entries, holds
+    // its power-of-two working size only from there)
+    const char *ew = getenv("HYMET_REG_WAVE"), *el = getenv("HYMET_REG_LDS");
+    if (ew && atoi(ew) >= 0) P.wave_min = atoi(ew);
+    if (el) P.lds_max = std::max(32, std::min(kRegSmall, atoi(el)));
     ProfScope _ps(ctx, "mm_regions", (double)NC * (8.0 + 8.0 + 4.0 * 5) + (double)n_q * 64.0);  // chain + stats reads, reg writes
     static const bool reg_stats = getenv("HYMET_REG_STATS") != nullptr;  // diagnostic: chains per query
     if (reg_stats) {

@@ -55,7 +55,8 @@ def _queries(rng, refs):
 
 @pytest.mark.parametrize("bt_long,legacy,z_runs,resort,zm", [(None, None, None, None, None), ("4", None, None, None, None),
                                                             (None, "1", "1", None, None), (None, None, "2", None, None),
-                                                            (None, None, None, "1", None), (None, None, None, None, "0,7")])
+                                                            (None, None, None, "1", None), (None, None, None, None, "0,7"),
+                                                            (None, None, None, None, "regions")])
 def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy, z_runs, resort, zm):
     """bt_long = "4": nearly every chain group takes the wave-per-group backtrack path.
     legacy = "1": anchors take the two-key sort path (used when the one-key anchor sort key
@@ -63,8 +64,13 @@ def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy, z_runs, resort, z
     take the sort fallbacks (block bitonic / global radix) instead of the run merge.
     resort = "1": the long join re-sorts its anchors instead of compacting the first pass's.
     zm = "0,7": no merge group is staged in LDS; each is split into units of 7 entries, one
-    block per unit (the path of merge groups above 6,144 entries)."""
-    if zm is not None:
+    block per unit (the path of merge groups above 6,144 entries).
+    zm = "regions": every query of more than one chain takes the regions wave kernel, and from
+    33 chains its global-scratch path (the path of queries above 256 chains)."""
+    if zm == "regions":
+        monkeypatch.setenv("HYMET_REG_WAVE", "1")
+        monkeypatch.setenv("HYMET_REG_LDS", "32")
+    elif zm is not None:
         lds, unit = zm.split(",")
         monkeypatch.setenv("HYMET_ZM_LDS", lds)
         monkeypatch.setenv("HYMET_ZM_UNIT", unit)
