@@ -97,6 +97,7 @@ struct RegParams {
     const uint32_t *skip_q;        // queries whose regions come from the long join (nullable)
     int wave_min;                  // queries of more chains than this take regions_wave_kernel
     int lds_max;                   // ... and hold their regions in LDS up to this many (kRegSmall)
+    unsigned long long *prof;      // HYMET_REG_PROF: wave-kernel cycles per step (nullptr = off)
 };
 
 // (x0, y0): the chain's first anchor, (x1, y1): its last
@@ -116,17 +117,6 @@ __device__ void set_coor(hymet_mm_reg *r, int32_t qlen, uint64_t x0, uint64_t y0
     }
     r->mlen = mlen;  // span(first) + sum over consecutive anchors (chain_stats_flat_kernel)
     r->blen = blen;
-}
-
-// chain index of a region: its anchors start at b0 + as (chains of the query: [c0, c1))
-__device__ __forceinline__ int64_t chain_of(const int64_t *cboff, int64_t c0, int64_t c1, int64_t a) {
-    int64_t lo = c0, hi = c1 - 1;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi + 1) >> 1;
-        if (cboff[mid] <= a) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
 }
 
 struct AnchorStatParams {
@@ -425,7 +415,8 @@ __device__ void regions_seq(const RegParams &P, int q) {
         const int64_t a = P.ids[P.cfirst[c0 + i] + (int32_t)u - 1];  // the chain's first anchor
         const uint32_t h = (uint32_t)hash64((hash64(P.ax[a]) + hash64(P.ay[a])) ^ hash);
         z[i].x = u ^ h;
-        z[i].y = (uint64_t)k << 32 | (uint32_t)(int32_t)u;
+        z[i].y = (uint64_t)k << 32 | (uint32_t)i;  // (mm_gen_regs: count; k is unique per chain, so
+                                                   // the low word never orders -- the chain index instead)
     }
     heap_sort(z, n, [](const U128 &a, const U128 &b) { return lt128(a, b); });
     for (int i = 0; i < n >> 1; ++i) {
@@ -439,15 +430,15 @@ __device__ void regions_seq(const RegParams &P, int q) {
         ri->parent = -1;
         ri->score = (int32_t)(z[i].x >> 32);
         ri->hash = (uint32_t)z[i].x;
-        ri->cnt = (int32_t)z[i].y;
+        const int64_t c = c0 + (uint32_t)z[i].y;
+        ri->cnt = (int32_t)P.cu[c];
         ri->as = (int32_t)(z[i].y >> 32);
         ri->div = -1.0f;
         ri->subsc = 0;
         ri->n_sub = 0;
         ri->strand_retained = 0;
         ri->mapq = 0;
-        ri->pad = 0;
-        const int64_t c = chain_of(P.cboff, c0, c1, b0 + ri->as);
+        ri->pad = (int32_t)(c - c0);  // the region's chain, until mm_est_err (cleared in mm_set_mapq)
         const int64_t a0 = P.ids[P.cfirst[c] + ri->cnt - 1], a1 = P.ids[P.cfirst[c]];  // first, last anchor
         set_coor(ri, qlen, P.ax[a0], P.ay[a0], P.ax[a1], P.ay[a1], P.c_mlen[c], P.c_blen[c]);
     }
@@ -544,7 +535,7 @@ __device__ void regions_seq(const RegParams &P, int q) {
                 hymet_mm_reg *ri = &r[i];
                 ri->div = -1.0f;
                 if (ri->cnt == 0) continue;
-                const int64_t c = chain_of(P.cboff, c0, c1, b0 + ri->as);
+                const int64_t c = c0 + ri->pad;
                 const int32_t st = P.c_st[c];
                 if (st < 0) continue;
                 const int32_t fv = P.c_fv[c] < ri->cnt ? P.c_fv[c] : ri->cnt;
@@ -579,6 +570,7 @@ __device__ void regions_seq(const RegParams &P, int q) {
         const float uniq_ratio = __fdiv_rn((float)sum_sc, (float)(sum_sc + P.rep_len[q]));
         for (int i = 0; i < n; ++i) {
             hymet_mm_reg *ri = &r[i];
+            ri->pad = 0;
             if (ri->parent == ri->id) {
                 const float pen_s1 = __fmul_rn(ri->score > 100 ? 1.0f : __fmul_rn(0.01f, (float)ri->score), uniq_ratio);
                 float pen_cm = ri->cnt > 10 ? 1.0f : __fmul_rn(0.1f, (float)ri->cnt);
@@ -739,6 +731,14 @@ __global__ __launch_bounds__(64) void regions_wave_kernel(RegParams P, const int
 
 __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned char *rsm, const int CAP) {
     const int lane = threadIdx.x;
+    // profiling: section k's cycles added to prof[k - 1] (prof[6]: queries, prof[7]: chains)
+    uint64_t rp_t = P.prof ? clock64() : 0;
+#define RPROF(k)                                                                       \
+    if (P.prof) {                                                                      \
+        const uint64_t rp_n = clock64();                                               \
+        if ((k) > 0) atomicAdd(P.prof + (k) - 1, lane == 0 ? (unsigned long long)(rp_n - rp_t) : 0ull); \
+        rp_t = rp_n;                                                                   \
+    }
     const int64_t c0 = P.qc[q], c1 = P.qc[q + 1];
     int n = (int)(c1 - c0);
     const int32_t qlen = (int32_t)P.qlen[q];
@@ -755,6 +755,7 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
     uint32_t hash = P.name_hash[q];
     hash ^= wang32((uint32_t)qlen) + wang32((uint32_t)P.seed);
     hash = wang32(hash);
+    RPROF(0);
     // ---- mm_gen_regs: keys (score<<32 | cnt) ^ hash, sorted descending (keys are distinct:
     // y holds the chain's anchor offset), padded to a power of two with (0, 0)
     int m = 64;
@@ -767,11 +768,12 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
             const int64_t a = P.ids[P.cfirst[c0 + i] + (int32_t)u - 1];
             const uint32_t h = (uint32_t)hash64((hash64(P.ax[a]) + hash64(P.ay[a])) ^ hash);
             zz.x = u ^ h;
-            zz.y = (uint64_t)k << 32 | (uint32_t)(int32_t)u;
+            zz.y = (uint64_t)k << 32 | (uint32_t)i;  // the chain index, not its count (as regions_seq)
         }
         zs[i] = zz;
     }
     wsync();
+    RPROF(1);
     lds_sort_desc(zs, m);
     for (int i = lane; i < n; i += 64) {
         const U128 zi = zs[i];
@@ -780,15 +782,15 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
         ri.parent = -1;
         ri.score = (int32_t)(zi.x >> 32);
         ri.hash = (uint32_t)zi.x;
-        ri.cnt = (int32_t)zi.y;
+        const int64_t c = c0 + (uint32_t)zi.y;
+        ri.cnt = (int32_t)P.cu[c];
         ri.as = (int32_t)(zi.y >> 32);
         ri.div = -1.0f;
         ri.subsc = 0;
         ri.n_sub = 0;
         ri.strand_retained = 0;
         ri.mapq = 0;
-        ri.pad = 0;
-        const int64_t c = chain_of(P.cboff, c0, c1, b0 + ri.as);
+        ri.pad = (int32_t)(c - c0);  // the region's chain, until mm_est_err (cleared in mm_set_mapq)
         const int64_t a0 = P.ids[P.cfirst[c] + ri.cnt - 1], a1 = P.ids[P.cfirst[c]];
         set_coor(&ri, qlen, P.ax[a0], P.ay[a0], P.ax[a1], P.ay[a1], P.c_mlen[c], P.c_blen[c]);
         r[i] = ri;
@@ -796,6 +798,7 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
         aux[i] = make_int4(ri.rid | ri.rev << 31, ri.rs, ri.re, 0);
     }
     wsync();
+    RPROF(2);
     // ---- mm_set_parent: sequential over regions; each region is tested against all primaries
     // so far lane-parallel (the sequential loop's first match = the lowest matching lane)
     {
@@ -891,6 +894,7 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
     }
     __threadfence_block();
     wsync();
+    RPROF(3);
     // ---- mm_select_sub (check_strand = 1) + mm_sync_regs.  The sequential loop compacts in
     // place and reads r[p] afterwards, so a parent position already overwritten by a kept
     // region holds THAT region: position p holds the p-th kept region once more than p are
@@ -972,6 +976,7 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
     }
     __threadfence_block();
     wsync();
+    RPROF(4);
     // ---- mm_est_err (per region)
     {
         const int64_t m0 = P.mp_off[q];
@@ -983,7 +988,7 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
                 hymet_mm_reg *ri = &r[i];
                 float div = -1.0f;
                 if (ri->cnt != 0) {
-                    const int64_t c = chain_of(P.cboff, c0, c1, b0 + ri->as);
+                    const int64_t c = c0 + ri->pad;
                     const int32_t st = P.c_st[c];
                     if (st >= 0) {
                         const int32_t fv = P.c_fv[c] < ri->cnt ? P.c_fv[c] : ri->cnt;
@@ -1002,6 +1007,7 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
     }
     __threadfence_block();
     wsync();
+    RPROF(5);
     // ---- mm_filter_strand_retained: exact in parallel up to the first dropped region (no
     // position has moved before it); from there the sequential loop (drops are rare)
     {
@@ -1042,6 +1048,7 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
         const float uniq_ratio = __fdiv_rn((float)sum_sc, (float)(sum_sc + P.rep_len[q]));
         for (int i = lane; i < n; i += 64) {
             hymet_mm_reg *ri = &r[i];
+            ri->pad = 0;
             if (ri->parent == ri->id) {
                 const float pen_s1 = __fmul_rn(ri->score > 100 ? 1.0f : __fmul_rn(0.01f, (float)ri->score), uniq_ratio);
                 float pen_cm = ri->cnt > 10 ? 1.0f : __fmul_rn(0.1f, (float)ri->cnt);
@@ -1056,6 +1063,12 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
                 ri->mapq = 0;
         }
     }
+    RPROF(6);
+    if (P.prof) {
+        atomicAdd(P.prof + 6, lane == 0 ? 1ull : 0ull);
+        atomicAdd(P.prof + 7, lane == 0 ? (unsigned long long)(c1 - c0) : 0ull);
+    }
+#undef RPROF
     if (lane == 0) P.n_regs[q] = n;
 }
 
@@ -1106,7 +1119,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
     }
     RegParams P{ax, ay, ids, cfirst, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
-                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk, skip_q, kRegWave, kRegSmall};
+                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk, skip_q, kRegWave, kRegSmall, nullptr};
     // tests / A-B: HYMET_REG_WAVE (chains above which a query takes the wave kernel),
     // HYMET_REG_LDS (chains up to which the wave kernel works in LDS; 32: every wave query on the
     // global-scratch path from 33 chains: a query's share of that scratch, 2n entries, holds
@@ -1131,6 +1144,10 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
                 n_q, (long long)NB, (long long)tot, (long long)mx, (long long)h[0], (long long)h[1], (long long)h[2], (long long)h[3],
                 (long long)h[4], (long long)h[5], (long long)big_tot);
     }
+    if (getenv("HYMET_REG_PROF")) {
+        HY_HIP(hipMalloc((void **)&P.prof, 8 * 8));
+        HY_HIP(hipMemsetAsync(P.prof, 0, 8 * 8, st));
+    }
     DevBuf big, gscr;
     HY_HIP(big.alloc(4 * (size_t)n_q, st));
     HY_HIP(gscr.alloc((size_t)kRegScrStride * (size_t)(NC + 1), st));
@@ -1143,6 +1160,14 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
                        (size_t)kRegSmall * kRegEntryBytes, st, P, (const int32_t *)big.as<int32_t>(), n_big,
                        mb_dev(ctx, kMbRegBig), gscr.as<unsigned char>());
     HY_CHECK_LAUNCH("regions_wave_kernel");
+    if (P.prof) {  // diagnostic: section cycles of the wave kernel's queries
+        unsigned long long h[8];
+        HY_HIP(hipMemcpyAsync(h, P.prof, sizeof h, hipMemcpyDeviceToHost, st));
+        HY_HIP(hipStreamSynchronize(st));
+        fprintf(stderr, "[regprof] queries %llu chains %llu | Mcycles keys %.1f sort+fill %.1f parent %.1f select %.1f est %.1f filter+mapq %.1f\n",
+                h[6], h[7], h[0] / 1e6, h[1] / 1e6, h[2] / 1e6, h[3] / 1e6, h[4] / 1e6, h[5] / 1e6);
+        (void)hipFree(P.prof);
+    }
     return HYMET_OK;
 }
 

@@ -13,3 +13,4 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/z
 python3 tools/lastrun.py $OUT/ztrace1 40 > $OUT/zymo_onestream_laststep.txt
 gzip -f $OUT/ztrace1/*kernel_trace.csv
 timeout -k 10 600 python3 bench.py --workload cami-medium-zymo --steps 3 --warmup 1 --no-cpu > $OUT/zymo_bench.json 2> $OUT/zymo_bench.err
+HYMET_REG_PROF=1 timeout -k 10 600 python3 bench.py --workload cami-medium-zymo --steps 1 --warmup 0 --no-cpu --map-streams 1 > $OUT/regprof_bench.json 2> $OUT/regprof_bench.err
