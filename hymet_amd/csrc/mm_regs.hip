@@ -98,6 +98,7 @@ struct RegParams {
     int wave_min;                  // queries of more chains than this take regions_wave_kernel
     int lds_max;                   // ... and hold their regions in LDS up to this many (kRegSmall)
     unsigned long long *prof;      // HYMET_REG_PROF: wave-kernel cycles per step (nullptr = off)
+    int prim_regs;                 // set_parent primaries held in registers (64; HYMET_REG_PRIM in tests)
 };
 
 // (x0, y0): the chain's first anchor, (x1, y1): its last
@@ -800,68 +801,127 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
     wsync();
     RPROF(2);
     // ---- mm_set_parent: sequential over regions; each region is tested against all primaries
-    // so far lane-parallel (the sequential loop's first match = the lowest matching lane)
+    // so far lane-parallel (the sequential loop's first match = the lowest matching lane).
+    // Primaries 0..63 live in registers (lane j: primary j's qs, qe, cnt, region index and
+    // its subsc / n_sub so far) and the regions' (qs, qe, score, cnt) come 64 at a time from
+    // LDS, so a query of up to 64 primaries runs its walk without an LDS round trip or barrier
+    // per region; primaries from the 65th on keep the LDS lists (wl / psub / pns).
+    // (P.prim_regs < 64, tests: fewer primaries in registers, the rest through the lists.)
     {
+        const int R = P.prim_regs;
+        int ps = 0, pe = 0, pc = 0, pw = 0, psb = 0, pnb = 0;  // lane j: primary j (j < 64)
+        if (lane == 0) {
+            const int4 s0 = slot[0];
+            ps = s0.x, pe = s0.y, pc = s0.w;
+            r[0].parent = 0;
+            if (R == 0) wl[0] = 0, psub[0] = 0, pns[0] = 0;
+        }
+        if (R == 0) wsync();
         int k = 1;
-        if (lane == 0) wl[0] = 0, psub[0] = 0, pns[0] = 0, r[0].parent = 0;
-        wsync();
+        int4 my = make_int4(0, 0, 0, 0);  // lane l: region (i & ~63) + l
         for (int i = 1; i < n; ++i) {
-            const int4 me = slot[i];
-            const int si = me.x, ei = me.y, sci = me.z, cnti = me.w;
-            // overlapping primaries, clipped, gathered in primary order
-            int ncov = 0;
-            for (int jb = 0; jb < k; jb += 64) {
-                const int j = jb + lane;
-                int sj = 0, ej = 0;
-                if (j < k) {
-                    const int4 o = slot[wl[j]];
-                    sj = o.x, ej = o.y;
-                }
-                const bool ov = j < k && !(ej <= si || sj >= ei);
-                const uint64_t mov = __ballot(ov);
-                if (ov) covb[ncov + __popcll(mov & ((1ull << lane) - 1))] = (uint64_t)(uint32_t)max(sj, si) << 32 | (uint32_t)min(ej, ei);
-                ncov += __popcll(mov);
-            }
-            wsync();
+            if (i == 1 || (i & 63) == 0) my = slot[min((i & ~63) + lane, n - 1)];
+            const int li = i & 63;
+            const int si = __builtin_amdgcn_readlane(my.x, li), ei = __builtin_amdgcn_readlane(my.y, li);
+            const int sci = __builtin_amdgcn_readlane(my.z, li), cnti = __builtin_amdgcn_readlane(my.w, li);
             int jfound = -1;
-            if (ncov > 0) {
-                // uncovered length of [si, ei]: the sorted sweep x = running max of ends
-                int uncov = 0, carry = si;
-                if (ncov == 1) {  // one overlapping primary: its clipped interval is the union
-                    const uint64_t kv = covb[0];
-                    const int s_ = (int)(kv >> 32), e_ = (int)(uint32_t)kv;
-                    uncov = s_ > si ? s_ - si : 0;
-                    carry = max(si, e_);
-                } else if (ncov <= 64) {
-                    const uint64_t kv = wave_sort_u64(lane < ncov ? covb[lane] : ~0ull);
-                    const int s_ = (int)(kv >> 32), e_ = lane < ncov ? (int)(uint32_t)kv : INT32_MIN;
-                    const int x = wave_excl_max(e_, si);
-                    uncov = wave_sum_i(lane < ncov && s_ > x ? s_ - x : 0);
-                    carry = max(si, wave_max_i(e_));
-                } else {
-                    int mm = 64;
-                    while (mm < ncov) mm <<= 1;
-                    for (int t = ncov + lane; t < mm; t += 64) covb[t] = ~0ull;
-                    wsync();
-                    lds_sort_asc_u64(covb, mm);
-                    for (int tb = 0; tb < ncov; tb += 64) {
-                        const int t = tb + lane;
-                        const uint64_t kv = t < ncov ? covb[t] : ~0ull;
-                        const int s_ = (int)(kv >> 32), e_ = t < ncov ? (int)(uint32_t)kv : INT32_MIN;
-                        const int x = wave_excl_max(e_, carry);
-                        uncov += wave_sum_i(t < ncov && s_ > x ? s_ - x : 0);
-                        carry = max(carry, wave_max_i(e_));
+            if (k <= R) {
+                const bool ov = lane < k && !(pe <= si || ps >= ei);
+                const uint64_t mov = __ballot(ov);
+                if (mov) {
+                    // uncovered length of [si, ei]: the sorted sweep x = running max of ends
+                    const uint64_t kvl = ov ? (uint64_t)(uint32_t)max(ps, si) << 32 | (uint32_t)min(pe, ei) : ~0ull;
+                    const int ncov = __popcll(mov);
+                    int uncov = 0, carry = si;
+                    if (ncov == 1) {  // one overlapping primary: its clipped interval is the union
+                        const int l1 = __ffsll((unsigned long long)mov) - 1;
+                        const int s_ = (int)__builtin_amdgcn_readlane((int)(kvl >> 32), l1);
+                        const int e_ = (int)__builtin_amdgcn_readlane((int)(uint32_t)kvl, l1);
+                        uncov = s_ > si ? s_ - si : 0;
+                        carry = max(si, e_);
+                    } else {
+                        const uint64_t kv = wave_sort_u64(kvl);
+                        const int s_ = (int)(kv >> 32), e_ = lane < ncov ? (int)(uint32_t)kv : INT32_MIN;
+                        const int x = wave_excl_max(e_, si);
+                        uncov = wave_sum_i(lane < ncov && s_ > x ? s_ - x : 0);
+                        carry = max(si, wave_max_i(e_));
                     }
-                }
-                if (ei > carry) uncov += ei - carry;
-                // the first primary (in order) that region i is a secondary of
-                for (int jb = 0; jb < k && jfound < 0; jb += 64) {
-                    const int j = jb + lane;
+                    if (ei > carry) uncov += ei - carry;
                     bool hit = false;
-                    if (j < k) {
-                        const int4 o = slot[wl[j]];
-                        const int sj = o.x, ej = o.y;
-                        if (!(ej <= si || sj >= ei)) {
+                    if (ov) {
+                        const int sj = ps, ej = pe;
+                        const int mn = ej - sj < ei - si ? ej - sj : ei - si;
+                        const int mx = ej - sj > ei - si ? ej - sj : ei - si;
+                        const int ol = si < sj ? (ei < sj ? 0 : ei < ej ? ei - sj : ej - sj)
+                                               : (ej < si ? 0 : ej < ei ? ej - si : ei - si);
+                        hit = __fsub_rn(__fdiv_rn((float)ol, (float)mn), __fdiv_rn((float)uncov, (float)mx)) > P.mask_level &&
+                              uncov <= P.mask_len;
+                    }
+                    const uint64_t mh = __ballot(hit);
+                    if (mh) jfound = __ffsll((unsigned long long)mh) - 1;
+                }
+            } else {
+                // overlapping primaries, clipped, gathered in primary order (chunk 0 from registers)
+                int ncov = 0;
+                for (int jb = 0; jb < k; jb += 64) {
+                    const int j = jb + lane;
+                    int sj = ps, ej = pe;
+                    if (j >= R) {
+                        sj = 0, ej = 0;
+                        if (j < k) {
+                            const int4 o = slot[wl[j]];
+                            sj = o.x, ej = o.y;
+                        }
+                    }
+                    const bool ov = j < k && !(ej <= si || sj >= ei);
+                    const uint64_t mov = __ballot(ov);
+                    if (ov) covb[ncov + __popcll(mov & ((1ull << lane) - 1))] = (uint64_t)(uint32_t)max(sj, si) << 32 | (uint32_t)min(ej, ei);
+                    ncov += __popcll(mov);
+                }
+                wsync();
+                if (ncov > 0) {
+                    int uncov = 0, carry = si;
+                    if (ncov == 1) {
+                        const uint64_t kv = covb[0];
+                        const int s_ = (int)(kv >> 32), e_ = (int)(uint32_t)kv;
+                        uncov = s_ > si ? s_ - si : 0;
+                        carry = max(si, e_);
+                    } else if (ncov <= 64) {
+                        const uint64_t kv = wave_sort_u64(lane < ncov ? covb[lane] : ~0ull);
+                        const int s_ = (int)(kv >> 32), e_ = lane < ncov ? (int)(uint32_t)kv : INT32_MIN;
+                        const int x = wave_excl_max(e_, si);
+                        uncov = wave_sum_i(lane < ncov && s_ > x ? s_ - x : 0);
+                        carry = max(si, wave_max_i(e_));
+                    } else {
+                        int mm = 64;
+                        while (mm < ncov) mm <<= 1;
+                        for (int t = ncov + lane; t < mm; t += 64) covb[t] = ~0ull;
+                        wsync();
+                        lds_sort_asc_u64(covb, mm);
+                        for (int tb = 0; tb < ncov; tb += 64) {
+                            const int t = tb + lane;
+                            const uint64_t kv = t < ncov ? covb[t] : ~0ull;
+                            const int s_ = (int)(kv >> 32), e_ = t < ncov ? (int)(uint32_t)kv : INT32_MIN;
+                            const int x = wave_excl_max(e_, carry);
+                            uncov += wave_sum_i(t < ncov && s_ > x ? s_ - x : 0);
+                            carry = max(carry, wave_max_i(e_));
+                        }
+                    }
+                    if (ei > carry) uncov += ei - carry;
+                    // the first primary (in order) that region i is a secondary of
+                    for (int jb = 0; jb < k && jfound < 0; jb += 64) {
+                        const int j = jb + lane;
+                        bool hit = false;
+                        int sj = ps, ej = pe;
+                        bool in = true;
+                        if (j >= R) {
+                            in = j < k;
+                            if (in) {
+                                const int4 o = slot[wl[j]];
+                                sj = o.x, ej = o.y;
+                            }
+                        }
+                        if (in && !(ej <= si || sj >= ei)) {
                             const int mn = ej - sj < ei - si ? ej - sj : ei - si;
                             const int mx = ej - sj > ei - si ? ej - sj : ei - si;
                             const int ol = si < sj ? (ei < sj ? 0 : ei < ej ? ei - sj : ej - sj)
@@ -869,25 +929,44 @@ __device__ __forceinline__ void regions_wave(const RegParams &P, int q, unsigned
                             hit = __fsub_rn(__fdiv_rn((float)ol, (float)mn), __fdiv_rn((float)uncov, (float)mx)) > P.mask_level &&
                                   uncov <= P.mask_len;
                         }
+                        const uint64_t mh = __ballot(hit);
+                        if (mh) jfound = jb + __ffsll((unsigned long long)mh) - 1;
                     }
-                    const uint64_t mh = __ballot(hit);
-                    if (mh) jfound = jb + __ffsll((unsigned long long)mh) - 1;
                 }
             }
             if (jfound >= 0) {
-                const int p = wl[jfound];
-                if (lane == 0) {
-                    r[i].parent = p;
-                    psub[jfound] = psub[jfound] > sci ? psub[jfound] : sci;
-                    if (cnti >= slot[p].w) ++pns[jfound];
+                if (jfound < R) {
+                    const int p = __builtin_amdgcn_readlane(pw, jfound);
+                    if (lane == 0) r[i].parent = p;
+                    if (lane == jfound) {
+                        psb = psb > sci ? psb : sci;
+                        if (cnti >= pc) ++pnb;
+                    }
+                } else {
+                    const int p = wl[jfound];
+                    if (lane == 0) {
+                        r[i].parent = p;
+                        psub[jfound] = psub[jfound] > sci ? psub[jfound] : sci;
+                        if (cnti >= slot[p].w) ++pns[jfound];
+                    }
+                    wsync();
                 }
             } else {
-                if (lane == 0) wl[k] = i, psub[k] = 0, pns[k] = 0, r[i].parent = i;
+                if (k < R) {
+                    if (lane == k) ps = si, pe = ei, pc = cnti, pw = i, psb = 0, pnb = 0;
+                } else {
+                    if (lane == 0) wl[k] = i, psub[k] = 0, pns[k] = 0;
+                }
+                if (lane == 0) r[i].parent = i;
                 ++k;
+                if (k > R) wsync();
             }
-            wsync();
         }
-        for (int j = lane; j < k; j += 64) {
+        if (lane < k && lane < R) {
+            r[pw].subsc = psb;
+            r[pw].n_sub = pnb;
+        }
+        for (int j = R + lane; j < k; j += 64) {
             r[wl[j]].subsc = psub[j];
             r[wl[j]].n_sub = pns[j];
         }
@@ -1119,7 +1198,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
     }
     RegParams P{ax, ay, ids, cfirst, cu, cboff, qc, qb, mini_pos, mp_off, qlen, name_hash, rep_len, ref_len, n_q, o->seed, k,
                 o->mask_level, o->pri_ratio, o->mask_len, o->best_n, o->max_gap, o->min_chain_score, (U128 *)z, regs, w, cov,
-                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk, skip_q, kRegWave, kRegSmall, nullptr};
+                tmp, n_regs, c_mlen, c_blen, c_st, c_last, c_fv, sumk, skip_q, kRegWave, kRegSmall, nullptr, 64};
     // tests / A-B: HYMET_REG_WAVE (chains above which a query takes the wave kernel),
     // HYMET_REG_LDS (chains up to which the wave kernel works in LDS; 32: every wave query on the
     // global-scratch path from 33 chains: a query's share of that scratch, 2n entries, holds
@@ -1127,6 +1206,7 @@ int launch_regions(hymet_ctx *ctx, const uint64_t *ax, const uint64_t *ay, const
     const char *ew = getenv("HYMET_REG_WAVE"), *el = getenv("HYMET_REG_LDS");
     if (ew && atoi(ew) >= 0) P.wave_min = atoi(ew);
     if (el) P.lds_max = std::max(32, std::min(kRegSmall, atoi(el)));
+    if (const char *ep = getenv("HYMET_REG_PRIM")) P.prim_regs = std::max(0, std::min(64, atoi(ep)));
     ProfScope _ps(ctx, "mm_regions", (double)NC * (8.0 + 8.0 + 4.0 * 5) + (double)n_q * 64.0);  // chain + stats reads, reg writes
     static const bool reg_stats = getenv("HYMET_REG_STATS") != nullptr;  // diagnostic: chains per query
     if (reg_stats) {

@@ -56,7 +56,8 @@ def _queries(rng, refs):
 @pytest.mark.parametrize("bt_long,legacy,z_runs,resort,zm", [(None, None, None, None, None), ("4", None, None, None, None),
                                                             (None, "1", "1", None, None), (None, None, "2", None, None),
                                                             (None, None, None, "1", None), (None, None, None, None, "0,7"),
-                                                            (None, None, None, None, "regions")])
+                                                            (None, None, None, None, "regions"),
+                                                            (None, None, None, None, "regions_prim1")])
 def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy, z_runs, resort, zm):
     """bt_long = "4": nearly every chain group takes the wave-per-group backtrack path.
     legacy = "1": anchors take the two-key sort path (used when the one-key anchor sort key
@@ -66,10 +67,14 @@ def test_map_matches_oracle(gpu, monkeypatch, bt_long, legacy, z_runs, resort, z
     zm = "0,7": no merge group is staged in LDS; each is split into units of 7 entries, one
     block per unit (the path of merge groups above 6,144 entries).
     zm = "regions": every query of more than one chain takes the regions wave kernel, and from
-    33 chains its global-scratch path (the path of queries above 256 chains)."""
-    if zm == "regions":
+    33 chains its global-scratch path (the path of queries above 256 chains).
+    zm = "regions_prim1": the same, with one set_parent primary in registers and the rest in the
+    LDS lists (the path of queries of more than 64 primaries)."""
+    if zm in ("regions", "regions_prim1"):
         monkeypatch.setenv("HYMET_REG_WAVE", "1")
         monkeypatch.setenv("HYMET_REG_LDS", "32")
+        if zm == "regions_prim1":
+            monkeypatch.setenv("HYMET_REG_PRIM", "1")
     elif zm is not None:
         lds, unit = zm.split(",")
         monkeypatch.setenv("HYMET_ZM_LDS", lds)
